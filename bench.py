@@ -1,0 +1,182 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json configs[1]: Src7 4024x3036 / Dst7 762x521, ToleranceAngle 180, TargetNum 3.
+
+A step is one full TemplateMatcher::match pass (pyramid -> top-layer rotation sweep -> NCC -> peaks -> pyramid
+refinement -> host filters) over a batch of ``--batch`` synthetic Src7 sources per GPU that are already
+resident in HBM (staged before timing; the PCIe upload is not in ``value``).  ``value`` = searches/s over all
+ranks.  Multi-GPU: one process per GPU (torchrun), every rank searches its own sources (weak scaling, no
+data-path collective); barrier + synchronize bracket the K timed steps and the max time over ranks is used.
+
+Also reported: the dominant kernel's roofline (HIP events around every launch on the library's stream, in a
+second pass of K steps so the timed pass carries no event overhead) and the CPU baseline (the oracle
+restatement, single thread, on a bounded sample of the same workload, rank 0 at N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "template matches/sec + ms/search, 4024×3036 src ±180°; HBM GB/s vs roofline"
+README_MS_PER_SEARCH = 76.0          # README.md:45-48 (MFC build), BASELINE.md row 1
+HBM_PEAK_GBS = 8000.0                # MI355X_MICROARCH.md chip table (spec)
+PARAMS = dict(max_pos=3, tolerance_angle=180.0, score=0.7, min_reduce_area=256, max_overlap=0.0, use_simd=1)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_sources(templ, n, seed0):
+    from fastest_image_pattern_matching_amd import synth
+
+    return [synth.src7_scene(templ, seed=seed0 + i)[0] for i in range(n)]
+
+
+def cpu_baseline(templ, src, budget_s):
+    """Oracle (CPU port of the reference, SSE2 IM_Conv, 1 thread) on repeated searches of one Src7 source."""
+    from tests import oracle
+
+    o = oracle.OracleMatcher().set(**PARAMS)
+    o.learnPattern(templ)
+    o.match(src)                       # warm
+    n, t0 = 0, time.perf_counter()
+    while True:
+        o.match(src)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 200:
+            break
+    return {"value": n / el, "unit": "searches/s", "cores": 1, "kind": "port",
+            "sample": f"{n} sequential searches of one Src7 surrogate source ({el:.1f} s), oracle/fpm_oracle.cpp "
+                      f"-O3 SSE2, single thread (the reference's OpenMP code is dead)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=8, help="Src7 sources searched per GPU per step")
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (0 = skip)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier_sync():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    from fastest_image_pattern_matching_amd import TemplateMatcher, synth
+    from fastest_image_pattern_matching_amd import _lib as L
+
+    templ = synth.load_templates()["Dst7"]
+    log(f"[rank {rank}] generating {args.batch} Src7 surrogate sources")
+    sources = make_sources(templ, args.batch, 7 + 1000 * rank)
+
+    m = TemplateMatcher(local)
+    for k, v in PARAMS.items():
+        setattr(m._params, k, v)
+    assert m.learnPattern(templ)
+    # single-search latency (upload included) for the record
+    t0 = time.perf_counter()
+    single = m.match(sources[0])
+    lat_e2e = time.perf_counter() - t0
+    m.stage(sources)
+    for _ in range(args.warmup):
+        m.match_staged()
+    log(f"[rank {rank}] warm; timing {args.steps} steps x {args.batch} sources")
+
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = m.match_staged()
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    n_matches = [len(r) for r in res]
+
+    # kernel-level pass with HIP events around every launch
+    m.profile(True)
+    m.profile_reset()
+    for _ in range(args.steps):
+        m.match_staged()
+    m.profile(False)
+    kern = {}
+    for k, name in enumerate(L.KERNEL_NAMES):
+        ms, launches, b = m.profile_get(k)
+        if launches:
+            kern[name] = {"ms_total": ms, "launches": launches, "bytes": b}
+    dom = max(kern, key=lambda k: kern[k]["ms_total"])
+    d = kern[dom]
+    avg_s = d["ms_total"] / d["launches"] * 1e-3
+    bytes_per_launch = d["bytes"] / d["launches"]
+    achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
+    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": dom,
+                "avg_launch_us": round(avg_s * 1e6, 3), "algorithmic_bytes_per_launch": int(bytes_per_launch)}
+
+    searches = world * args.batch * args.steps
+    value = searches / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "searches/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / (1000.0 / README_MS_PER_SEARCH), 3),
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {
+            "workload": "Src7 surrogate (4024x3036, 235+N(0,2) background, 3 rotated Dst7 762x521 copies at the "
+                        "README poses), ToleranceAngle 180, TargetNum 3, Score 0.7, MinReduceArea 256, Overlap 0, "
+                        "SIMD fold on",
+            "sources_per_gpu_per_step": args.batch,
+            "global_batch": args.batch * world,
+            "parallelism": f"sources sharded over {world} GPU(s), one process per GPU",
+        },
+        "ms_per_search": round(elapsed * 1e3 / (args.batch * args.steps), 4),
+        "single_search_ms_end_to_end": round(lat_e2e * 1e3, 3),
+        "matches_per_search": n_matches,
+        "kernels": kern,
+        "roofline": roofline,
+    }
+    if world == 1 and rank == 0 and args.cpu_budget > 0:
+        log("[rank 0] CPU baseline (oracle restatement, 1 thread)")
+        out["cpu_baseline"] = cpu_baseline(templ, sources[0], args.cpu_budget)
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    del single
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,1047 @@
+// fpm_engine.hip — host orchestration of the MI355X template matcher and the C ABI (include/fpm.h).
+//
+// Mirrors TemplateMatcher::learnPattern / match (src/TemplateMatcher.cpp:45-437) with this split:
+//   host, once per (template, params, source size):  angle list (:130-144), per-angle canvas size and
+//       warp matrix (:163-173, :901-969), refinement angle tree with glibc cos/sin (:282-298), buffer layout;
+//   device, per search (one stream, no host sync until the end):  pyramid (K1), top-layer rotation + NCC +
+//       peak extraction for every (source, angle) (K2-K5), candidate init, and the layer loop
+//       L-1 .. 0 (K6-K8 fused + best-of-3 step) over a device-compacted live-candidate list;
+//   host, after ONE device->host copy:  reference-order candidate sort (:214), layer-0 decision / sub-pixel /
+//       back-mapping (:331-358), filterWithScore, filterWithRotatedRect, final sort and s_SingleTargetMatch
+//       conversion (:373-432).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cfloat>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/fpm.h"
+#include "fpm_host.h"
+#include "fpm_kernels.h"
+
+using namespace fpm;
+
+namespace {
+
+inline int round_up(int v, int a) { return (v + a - 1) / a * a; }
+inline size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= n && p) return hipSuccess;
+        if (p) { (void)hipFree(p); p = nullptr; n = 0; }
+        if (bytes == 0) bytes = 256;
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e == hipSuccess) n = bytes;
+        return e;
+    }
+    void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
+    template <class T> T* as(size_t byte_off = 0) const { return (T*)((char*)p + byte_off); }
+};
+
+struct PinBuf {
+    void* p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= n && p) return hipSuccess;
+        if (p) { (void)hipHostFree(p); p = nullptr; n = 0; }
+        if (bytes == 0) bytes = 256;
+        hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+        if (e == hipSuccess) n = bytes;
+        return e;
+    }
+    void release() { if (p) (void)hipHostFree(p); p = nullptr; n = 0; }
+    template <class T> T* as(size_t byte_off = 0) const { return (T*)((char*)p + byte_off); }
+};
+
+struct TmplLevel {
+    int w, h, pitch;
+    size_t off;              // offset in the device template slab
+    double mean, norm, inv_area;
+    bool equal1;
+    std::vector<uint8_t> px; // host copy (dense)
+};
+
+struct SrcLevel {
+    int w, h, pitch;
+    size_t img_bytes;        // pitch * h (rounded), per source image
+    size_t off;              // offset of source 0 in the device source slab
+};
+
+// Everything that depends only on (template, params, source size, batch size).
+struct Plan {
+    bool valid = false;
+    int sw = 0, sh = 0, S = 0, L = 0;
+    fpm_params prm{};
+    int nang = 0, cap = 0, n3 = 1, C = 0;      // C = S * nang * cap candidate slots
+    bool by_block = false;
+    std::vector<double> angles, layer_score;
+    std::vector<TopAngle> top;
+    std::vector<AngleNode> top_nodes;
+    std::vector<std::vector<AngleNode>> nodes;  // [d], d = 0 <-> layer L-1
+    std::vector<size_t> node_off;                // device offsets (elements)
+    F2 center;
+    // top-layer layout (per source)
+    std::vector<size_t> canvas_off, map_off, blk_off;
+    std::vector<int> canvas_pitch, map_w, map_h, nblk;
+    size_t canvas_bytes = 0, map_floats = 0, blk_count = 0;
+    int max_canvas = 0, max_map = 0;
+    // device buffers owned by the plan
+    DevBuf d_canvas, d_map, d_bmax, d_bloc, d_jobs, d_nodes, d_top, d_topn, d_peaks, d_counts, d_state,
+        d_live, d_livecnt, d_rec;
+    size_t off_warp = 0, off_ncc = 0, off_nms = 0;
+    PinBuf h_out;
+    size_t h_counts = 0, h_peaks = 0, h_state = 0, h_rec = 0, h_live = 0, h_total = 0;
+    void release() {
+        for (DevBuf* b : {&d_canvas, &d_map, &d_bmax, &d_bloc, &d_jobs, &d_nodes, &d_top, &d_topn, &d_peaks,
+                          &d_counts, &d_state, &d_live, &d_livecnt, &d_rec})
+            b->release();
+        h_out.release();
+        valid = false;
+    }
+};
+
+struct KProf {
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+    size_t used = 0;
+    double ms = 0;
+    int64_t launches = 0, bytes = 0;
+};
+
+}  // namespace
+
+struct fpm_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    fpm_params prm{};
+    std::string err;
+    // template (s_TemplData)
+    bool learned = false;
+    int border = 0;
+    std::vector<TmplLevel> tmpl;
+    DevBuf d_tmpl;
+    uint64_t tmpl_gen = 0;
+    // staged sources
+    int S = 0, sw = 0, sh = 0, src_L = -1;
+    std::vector<SrcLevel> src;
+    DevBuf d_src;
+    // plan
+    Plan plan;
+    uint64_t plan_gen = ~0ull;
+    // op scratch
+    DevBuf d_op_a, d_op_b, d_op_job;
+    // last search stats
+    std::vector<int64_t> stats;
+    // profiling
+    bool prof = false;
+    KProf kp[FPM_K_COUNT];
+};
+
+#define HIP_TRY(expr)                                                                   \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess) {                                                         \
+            ctx->err = std::string(#expr) + ": " + hipGetErrorString(e_);               \
+            return FPM_E_DEVICE;                                                        \
+        }                                                                               \
+    } while (0)
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------------------
+// profiling helpers
+// ---------------------------------------------------------------------------------------------------------
+struct ProfScope {
+    fpm_ctx* ctx;
+    int k;
+    hipEvent_t b = nullptr, e = nullptr;
+    ProfScope(fpm_ctx* c, int kk, int64_t bytes) : ctx(c), k(kk) {
+        if (!ctx->prof) return;
+        KProf& p = ctx->kp[k];
+        if (p.used == p.ev.size()) {
+            hipEvent_t x, y;
+            if (hipEventCreate(&x) != hipSuccess || hipEventCreate(&y) != hipSuccess) return;
+            p.ev.push_back({x, y});
+        }
+        b = p.ev[p.used].first;
+        e = p.ev[p.used].second;
+        p.used++;
+        p.launches++;
+        p.bytes += bytes;
+        (void)hipEventRecord(b, ctx->stream);
+    }
+    ~ProfScope() {
+        if (b) (void)hipEventRecord(e, ctx->stream);
+    }
+};
+
+void prof_collect(fpm_ctx* ctx) {
+    if (!ctx->prof) return;
+    for (int k = 0; k < FPM_K_COUNT; ++k) {
+        KProf& p = ctx->kp[k];
+        for (size_t i = 0; i < p.used; ++i) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, p.ev[i].first, p.ev[i].second) == hipSuccess) p.ms += ms;
+        }
+        p.used = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// host restatements of reference helpers
+// ---------------------------------------------------------------------------------------------------------
+int top_layer(int w, int h, int min_len) {   // getTopLayer (TemplateMatcher.cpp:445-455)
+    int L = 0, mra = min_len * min_len, area = w * h;
+    while (area > mra) { area /= 4; ++L; }
+    return L;
+}
+
+void mean_stddev(const std::vector<uint8_t>& px, double* mean, double* sdv) {  // cv::meanStdDev, 8UC1
+    int64_t s = 0, q = 0;
+    for (uint8_t v : px) { s += v; q += (int64_t)v * v; }
+    const double scale = px.empty() ? 0. : 1. / (double)px.size();
+    const double m = (double)s * scale;
+    *mean = m;
+    *sdv = std::sqrt(std::max((double)q * scale - m * m, 0.));
+}
+
+// getBestRotationSize (TemplateMatcher.cpp:901-969); ptRotatePt2f with glibc trig of angle*D2R
+void best_rotation_size(int sw, int sh, int dw, int dh, double ang, int* ow, int* oh) {
+    const double rad = ang * kD2R, c = std::cos(rad), s = std::sin(rad);
+    const F2 ctr = f2((sw - 1) / 2.0f, (sh - 1) / 2.0f);
+    const F2 lt = rotate_pt(f2(0.f, 0.f), ctr, c, s);
+    const F2 lb = rotate_pt(f2(0.f, (float)(sh - 1)), ctr, c, s);
+    const F2 rb = rotate_pt(f2((float)(sw - 1), (float)(sh - 1)), ctr, c, s);
+    const F2 rt = rotate_pt(f2((float)(sw - 1), 0.f), ctr, c, s);
+    const float top = std::max(std::max(lt.y, lb.y), std::max(rb.y, rt.y));
+    const float bottom = std::min(std::min(lt.y, lb.y), std::min(rb.y, rt.y));
+    const float right = std::max(std::max(lt.x, lb.x), std::max(rb.x, rt.x));
+    const float left = std::min(std::min(lt.x, lb.x), std::min(rb.x, rt.x));
+    if (ang > 360) ang -= 360;
+    else if (ang < 0) ang += 360;
+    if (std::fabs(std::fabs(ang) - 90) < kVisionTol || std::fabs(std::fabs(ang) - 270) < kVisionTol) {
+        *ow = sh; *oh = sw;
+        return;
+    }
+    if (std::fabs(ang) < kVisionTol || std::fabs(std::fabs(ang) - 180) < kVisionTol) {
+        *ow = sw; *oh = sh;
+        return;
+    }
+    double a = ang;
+    if (a > 90 && a < 180) a -= 90;
+    else if (a > 180 && a < 270) a -= 180;
+    else if (a > 270 && a < 360) a -= 270;
+    const float h1 = dw * std::sin(a * kD2R) * std::cos(a * kD2R);
+    const float h2 = dh * std::sin(a * kD2R) * std::cos(a * kD2R);
+    const int half_h = (int)std::ceil(top - ctr.y - h1);
+    const int half_w = (int)std::ceil(right - ctr.x - h2);
+    int rw = half_w * 2, rh = half_h * 2;
+    const bool wrong = (dw < rw && dh > rh) || ((dw > rw && dh < rh) || (int64_t)dw * dh > (int64_t)rw * rh);
+    if (wrong) { rw = int(right - left + 0.5); rh = int(top - bottom + 0.5); }
+    *ow = rw;
+    *oh = rh;
+}
+
+AngleNode make_node(double angle) {
+    AngleNode n;
+    n.angle = angle;
+    const double r = angle * kD2R;
+    n.c = std::cos(r); n.s = std::sin(r);
+    n.cn = std::cos(-r); n.sn = std::sin(-r);
+    return n;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// plan
+// ---------------------------------------------------------------------------------------------------------
+bool same_search_params(const fpm_params& a, const fpm_params& b) {
+    return a.max_pos == b.max_pos && a.min_reduce_area == b.min_reduce_area && a.max_overlap == b.max_overlap &&
+           a.score == b.score && a.tolerance_angle == b.tolerance_angle && a.use_simd == b.use_simd &&
+           a.tolerance_range == b.tolerance_range;
+}
+
+int build_plan(fpm_ctx* ctx) {
+    Plan& P = ctx->plan;
+    const int L = ctx->src_L;
+    if (P.valid && ctx->plan_gen == ctx->tmpl_gen && P.sw == ctx->sw && P.sh == ctx->sh && P.S == ctx->S &&
+        P.L == L && same_search_params(P.prm, ctx->prm))
+        return FPM_OK;
+    P.valid = false;
+    P.sw = ctx->sw; P.sh = ctx->sh; P.S = ctx->S; P.L = L; P.prm = ctx->prm;
+    const fpm_params& prm = ctx->prm;
+    const TmplLevel& tt = ctx->tmpl[L];
+    // angle list (TemplateMatcher.cpp:130-144)
+    const double step = std::atan(2.0 / std::max(tt.w, tt.h)) * kR2D;
+    P.angles.clear();
+    if (prm.tolerance_angle < kVisionTol) {
+        P.angles.push_back(0.0);
+    } else {
+        for (double a = 0; a < prm.tolerance_angle + step; a += step) P.angles.push_back(a);
+        for (double a = -step; a > -prm.tolerance_angle - step; a -= step) P.angles.push_back(a);
+    }
+    P.nang = (int)P.angles.size();
+    P.layer_score.assign(L + 1, prm.score);
+    for (int l = 1; l <= L; ++l) P.layer_score[l] = P.layer_score[l - 1] * 0.9;
+    const SrcLevel& top = ctx->src[L];
+    P.center = f2((top.w - 1) / 2.0f, (top.h - 1) / 2.0f);
+    P.by_block = ((top.w * top.h) / (tt.w * tt.h) > 500) && prm.max_pos > 10;
+    P.cap = std::max(prm.max_pos + kMatchCandidateNum, 1);
+    P.n3 = (prm.tolerance_range || prm.tolerance_angle >= kVisionTol) ? 3 : 1;
+    P.C = ctx->S * P.nang * P.cap;
+    // per-angle canvas geometry (TemplateMatcher.cpp:163-175)
+    P.top.resize(P.nang);
+    P.top_nodes.resize(P.nang);
+    P.canvas_off.resize(P.nang); P.map_off.resize(P.nang); P.blk_off.resize(P.nang);
+    P.canvas_pitch.resize(P.nang); P.map_w.resize(P.nang); P.map_h.resize(P.nang); P.nblk.resize(P.nang);
+    std::vector<std::array<double, 6>> mats(P.nang);
+    size_t co = 0, mo = 0, bo = 0;
+    P.max_canvas = 0; P.max_map = 0;
+    for (int a = 0; a < P.nang; ++a) {
+        int bw, bh;
+        best_rotation_size(top.w, top.h, tt.w, tt.h, P.angles[a], &bw, &bh);
+        TopAngle& ta = P.top[a];
+        ta.bw = bw; ta.bh = bh;
+        ta.tx = (bw - 1) / 2.0f - P.center.x;
+        ta.ty = (bh - 1) / 2.0f - P.center.y;
+        const double r = P.angles[a] * kD2R;
+        double m[6];
+        rotation_matrix(P.center, std::cos(r), std::sin(r), m);
+        m[2] += ta.tx;
+        m[5] += ta.ty;
+        invert_affine(m);
+        std::copy(m, m + 6, mats[a].begin());
+        P.top_nodes[a] = make_node(P.angles[a]);
+        const bool ok = bw >= tt.w && bh >= tt.h && bw > 0 && bh > 0;
+        P.canvas_pitch[a] = round_up(std::max(bw, 1), 64);
+        P.canvas_off[a] = co;
+        co += round_up((size_t)P.canvas_pitch[a] * std::max(bh, 1), (size_t)256);
+        P.map_w[a] = ok ? bw - tt.w + 1 : 0;
+        P.map_h[a] = ok ? bh - tt.h + 1 : 0;
+        P.map_off[a] = mo;
+        mo += round_up((size_t)P.map_w[a] * P.map_h[a], (size_t)64);
+        int nb = 0;
+        if (P.by_block && ok) {
+            const int ncol = P.map_w[a] / tt.w, nrow = P.map_h[a] / tt.h;
+            const int rw = P.map_w[a] - ncol * tt.w, rh = P.map_h[a] - nrow * tt.h;
+            nb = ncol * nrow + (rw > 0) + (rh > 0) + (rw > 0 && rh > 0);
+        }
+        P.nblk[a] = nb;
+        P.blk_off[a] = bo;
+        bo += round_up((size_t)nb, (size_t)64);
+        P.max_canvas = std::max(P.max_canvas, bw * bh);
+        P.max_map = std::max(P.max_map, P.map_w[a] * P.map_h[a]);
+    }
+    P.canvas_bytes = co; P.map_floats = mo; P.blk_count = bo;
+    // refinement angle tree: level d has nang * n3^(d+1) nodes (TemplateMatcher.cpp:282-298)
+    P.nodes.assign(L, {});
+    P.node_off.assign(L, 0);
+    size_t noff = 0;
+    for (int d = 0; d < L; ++d) {
+        const int layer = L - 1 - d;
+        const double astep = std::atan(2.0 / std::max(ctx->tmpl[layer].w, ctx->tmpl[layer].h)) * kR2D;
+        const size_t parents = d == 0 ? (size_t)P.nang : P.nodes[d - 1].size();
+        std::vector<AngleNode>& lv = P.nodes[d];
+        lv.resize(parents * P.n3);
+        for (size_t p = 0; p < parents; ++p) {
+            const double matched = d == 0 ? P.angles[p] : P.nodes[d - 1][p].angle;
+            for (int j = 0; j < P.n3; ++j) {
+                double ang;
+                if (P.n3 == 1) ang = 0.0;
+                else ang = matched + astep * (j - 1);
+                lv[p * P.n3 + j] = make_node(ang);
+            }
+        }
+        P.node_off[d] = noff;
+        noff += lv.size();
+    }
+    // device buffers
+    const int S = ctx->S, J = S * P.nang;
+    HIP_TRY(P.d_canvas.ensure(P.canvas_bytes * S));
+    HIP_TRY(P.d_map.ensure(sizeof(float) * P.map_floats * S));
+    HIP_TRY(P.d_bmax.ensure(sizeof(float) * std::max<size_t>(P.blk_count, 1) * S));
+    HIP_TRY(P.d_bloc.ensure(sizeof(int32_t) * std::max<size_t>(P.blk_count, 1) * S));
+    P.off_warp = 0;
+    P.off_ncc = round_up(sizeof(WarpJob) * J, (size_t)256);
+    P.off_nms = P.off_ncc + round_up(sizeof(NccJob) * J, (size_t)256);
+    HIP_TRY(P.d_jobs.ensure(P.off_nms + sizeof(NmsJob) * J));
+    HIP_TRY(P.d_nodes.ensure(sizeof(AngleNode) * std::max<size_t>(noff, 1)));
+    HIP_TRY(P.d_top.ensure(sizeof(TopAngle) * P.nang));
+    HIP_TRY(P.d_topn.ensure(sizeof(AngleNode) * P.nang));
+    HIP_TRY(P.d_peaks.ensure(sizeof(Peak) * (size_t)P.C));
+    HIP_TRY(P.d_counts.ensure(sizeof(int32_t) * J));
+    HIP_TRY(P.d_state.ensure(sizeof(CandState) * (size_t)P.C));
+    HIP_TRY(P.d_live.ensure(sizeof(int32_t) * (size_t)P.C * 2));
+    HIP_TRY(P.d_livecnt.ensure(sizeof(int32_t) * (L + 2)));
+    HIP_TRY(P.d_rec.ensure(sizeof(RoiRecord) * (size_t)P.C * P.n3));
+    // job tables
+    std::vector<WarpJob> wj(J);
+    std::vector<NccJob> nj(J);
+    std::vector<NmsJob> mj(J);
+    const uint8_t* dsrc = ctx->d_src.as<uint8_t>();
+    for (int s = 0; s < S; ++s)
+        for (int a = 0; a < P.nang; ++a) {
+            const int k = s * P.nang + a;
+            uint8_t* canvas = P.d_canvas.as<uint8_t>() + P.canvas_bytes * s + P.canvas_off[a];
+            float* map = P.d_map.as<float>() + P.map_floats * s + P.map_off[a];
+            WarpJob& w = wj[k];
+            w.src = dsrc + top.off + top.img_bytes * s;
+            w.sw = top.w; w.sh = top.h; w.sp = top.pitch;
+            w.dst = canvas;
+            w.dw = P.top[a].bw; w.dh = P.top[a].bh; w.dp = P.canvas_pitch[a];
+            w.border = ctx->border;
+            w.pad = 0;
+            std::copy(mats[a].begin(), mats[a].end(), w.M);
+            NccJob& n = nj[k];
+            n.img = canvas; n.iw = w.dw; n.ih = w.dh; n.ip = w.dp;
+            n.tmpl = ctx->d_tmpl.as<uint8_t>() + tt.off; n.tw = tt.w; n.th = tt.h; n.tp = tt.pitch;
+            n.out = map; n.ow = P.map_w[a]; n.oh = P.map_h[a];
+            n.fold = 0;   // top layer: cv::matchTemplate(TM_CCORR) (:177 -> :514)
+            n.equal1 = tt.equal1 ? 1 : 0;
+            n.mean = tt.mean; n.norm = tt.norm; n.inv_area = tt.inv_area;
+            NmsJob& m = mj[k];
+            m.map = map; m.mw = P.map_w[a]; m.mh = P.map_h[a];
+            m.bmax = P.d_bmax.as<float>() + P.blk_count * s + P.blk_off[a];
+            m.bloc = P.d_bloc.as<int32_t>() + P.blk_count * s + P.blk_off[a];
+        }
+    HIP_TRY(hipMemcpyAsync(P.d_jobs.as<char>(P.off_warp), wj.data(), sizeof(WarpJob) * J, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(P.d_jobs.as<char>(P.off_ncc), nj.data(), sizeof(NccJob) * J, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(P.d_jobs.as<char>(P.off_nms), mj.data(), sizeof(NmsJob) * J, hipMemcpyHostToDevice, ctx->stream));
+    for (int d = 0; d < L; ++d)
+        HIP_TRY(hipMemcpyAsync(P.d_nodes.as<AngleNode>() + P.node_off[d], P.nodes[d].data(),
+                               sizeof(AngleNode) * P.nodes[d].size(), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(P.d_top.p, P.top.data(), sizeof(TopAngle) * P.nang, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(P.d_topn.p, P.top_nodes.data(), sizeof(AngleNode) * P.nang, hipMemcpyHostToDevice, ctx->stream));
+    // pinned host staging for the single device->host copy
+    P.h_counts = 0;
+    P.h_peaks = round_up(sizeof(int32_t) * J, (size_t)256);
+    P.h_state = P.h_peaks + round_up(sizeof(Peak) * (size_t)P.C, (size_t)256);
+    P.h_rec = P.h_state + round_up(sizeof(CandState) * (size_t)P.C, (size_t)256);
+    P.h_live = P.h_rec + round_up(sizeof(RoiRecord) * (size_t)P.C * P.n3, (size_t)256);
+    P.h_total = P.h_live + sizeof(int32_t) * (L + 2);
+    HIP_TRY(P.h_out.ensure(P.h_total));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    P.valid = true;
+    ctx->plan_gen = ctx->tmpl_gen;
+    return FPM_OK;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// sources
+// ---------------------------------------------------------------------------------------------------------
+int layout_sources(fpm_ctx* ctx, int count, int w, int h) {
+    const int L = top_layer(ctx->tmpl[0].w, ctx->tmpl[0].h, (int)std::sqrt((double)ctx->prm.min_reduce_area));
+    if (L >= (int)ctx->tmpl.size()) {
+        ctx->err = "MinReduceArea changed after learnPattern: template pyramid too shallow";
+        return FPM_E_INVALID_ARG;
+    }
+    ctx->S = count; ctx->sw = w; ctx->sh = h; ctx->src_L = L;
+    ctx->src.assign(L + 1, {});
+    size_t off = 0;
+    int lw = w, lh = h;
+    for (int l = 0; l <= L; ++l) {
+        SrcLevel& s = ctx->src[l];
+        s.w = lw; s.h = lh;
+        s.pitch = round_up(lw + 4, 64);          // +4: aligned dword over-reads stay in the row
+        s.img_bytes = round_up((size_t)s.pitch * (lh + 1), (size_t)256);
+        s.off = off;
+        off += s.img_bytes * count;
+        lw = (lw + 1) / 2;
+        lh = (lh + 1) / 2;
+    }
+    HIP_TRY(ctx->d_src.ensure(off));
+    return FPM_OK;
+}
+
+int check_sizes(fpm_ctx* ctx, int w, int h) {   // TemplateMatcher.cpp:99-114
+    if (!ctx->learned) { ctx->err = "template not learned"; return FPM_E_NOT_LEARNED; }
+    const TmplLevel& t = ctx->tmpl[0];
+    if ((t.w < w && t.h > h) || (t.w > w && t.h < h)) { ctx->err = "template/source orientation mismatch"; return FPM_E_SIZE; }
+    if ((int64_t)t.w * t.h > (int64_t)w * h) { ctx->err = "template larger than source"; return FPM_E_SIZE; }
+    return FPM_OK;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// search
+// ---------------------------------------------------------------------------------------------------------
+int enqueue_search(fpm_ctx* ctx) {
+    Plan& P = ctx->plan;
+    const int L = P.L, S = P.S, J = S * P.nang;
+    hipStream_t st = ctx->stream;
+    uint8_t* dsrc = ctx->d_src.as<uint8_t>();
+    // K1: source pyramid (all staged sources per launch)
+    for (int l = 1; l <= L; ++l) {
+        const SrcLevel& a = ctx->src[l - 1];
+        const SrcLevel& b = ctx->src[l];
+        ProfScope ps(ctx, FPM_K_PYR, (int64_t)S * ((int64_t)a.w * a.h + (int64_t)b.w * b.h));
+        launch_pyr_down(dsrc + a.off, a.w, a.h, a.pitch, a.img_bytes, dsrc + b.off, b.w, b.h, b.pitch, b.img_bytes, S, st);
+    }
+    const SrcLevel& top = ctx->src[L];
+    const TmplLevel& tt = ctx->tmpl[L];
+    {
+        int64_t bytes = 0;
+        for (int a = 0; a < P.nang; ++a) bytes += (int64_t)top.w * top.h + (int64_t)P.top[a].bw * P.top[a].bh;
+        ProfScope ps(ctx, FPM_K_TOP_WARP, bytes * S);
+        launch_warp(P.d_jobs.as<WarpJob>(P.off_warp), J, P.max_canvas, st);
+    }
+    {
+        int64_t bytes = 0;
+        for (int a = 0; a < P.nang; ++a)
+            bytes += (int64_t)P.top[a].bw * P.top[a].bh + (int64_t)tt.w * tt.h + 4LL * P.map_w[a] * P.map_h[a];
+        ProfScope ps(ctx, FPM_K_TOP_NCC, bytes * S);
+        launch_ncc_map(P.d_jobs.as<NccJob>(P.off_ncc), J, P.max_map, tt.w * tt.h, st);
+    }
+    {
+        int64_t bytes = 0;
+        for (int a = 0; a < P.nang; ++a) bytes += 4LL * P.map_w[a] * P.map_h[a];
+        ProfScope ps(ctx, FPM_K_TOP_NMS, bytes * S);
+        NmsArgs na;
+        na.jobs = P.d_jobs.as<NmsJob>(P.off_nms);
+        na.peaks = P.d_peaks.as<Peak>();
+        na.counts = P.d_counts.as<int32_t>();
+        na.tw = tt.w; na.th = tt.h; na.cap = P.cap; na.by_block = P.by_block ? 1 : 0;
+        na.thr = P.layer_score[L]; na.overlap = ctx->prm.max_overlap;
+        launch_nms(na, J, P.max_map, st);
+    }
+    HIP_TRY(hipMemsetAsync(P.d_livecnt.p, 0, sizeof(int32_t) * (L + 2), st));
+    int32_t* live[2] = {P.d_live.as<int32_t>(), P.d_live.as<int32_t>() + P.C};
+    int32_t* livecnt = P.d_livecnt.as<int32_t>();
+    {
+        CandInitArgs ca;
+        ca.peaks = P.d_peaks.as<Peak>();
+        ca.counts = P.d_counts.as<int32_t>();
+        ca.angles = P.d_top.as<TopAngle>();
+        ca.top_nodes = P.d_topn.as<AngleNode>();
+        ca.state = P.d_state.as<CandState>();
+        ca.live = live[0];
+        ca.live_count = livecnt + 0;
+        ca.nang = P.nang; ca.cap = P.cap; ca.total = P.C;
+        ca.center = P.center;
+        ca.refine = L > 0 ? (L == 1 ? 2 : 1) : 0;
+        launch_cand_init(ca, st);
+    }
+    for (int l = L - 1; l >= 0; --l) {
+        const int d = L - 1 - l;
+        const SrcLevel& lv = ctx->src[l];
+        const TmplLevel& tl = ctx->tmpl[l];
+        {
+            ProfScope ps(ctx, FPM_K_ROI_CORR, 0);
+            RoiArgs ra;
+            ra.level = dsrc + lv.off; ra.level_stride = lv.img_bytes;
+            ra.W = lv.w; ra.H = lv.h; ra.P = lv.pitch;
+            ra.tmpl = ctx->d_tmpl.as<uint8_t>() + tl.off; ra.tw = tl.w; ra.th = tl.h; ra.tp = tl.pitch;
+            ra.n3 = P.n3;
+            ra.rc = roi_pick_rc(tl.w, tl.h);
+            ra.fold = ctx->prm.use_simd ? 1 : 0;
+            ra.equal1 = tl.equal1 ? 1 : 0;
+            ra.per_source = P.nang * P.cap;
+            ra.mean = tl.mean; ra.norm = tl.norm; ra.inv_area = tl.inv_area;
+            ra.live = live[d & 1];
+            ra.live_count = livecnt + d;
+            ra.state = P.d_state.as<CandState>();
+            ra.nodes = P.d_nodes.as<AngleNode>() + P.node_off[d];
+            ra.rec = P.d_rec.as<RoiRecord>();
+            launch_roi_corr(ra, P.C * P.n3, st);
+        }
+        if (l > 0) {
+            ProfScope ps(ctx, FPM_K_ROI_EVAL, 0);
+            StepArgs sa;
+            sa.live_in = live[d & 1];
+            sa.live_in_count = livecnt + d;
+            sa.live_out = live[(d + 1) & 1];
+            sa.live_out_count = livecnt + d + 1;
+            sa.state = P.d_state.as<CandState>();
+            sa.rec = P.d_rec.as<RoiRecord>();
+            sa.nodes = P.d_nodes.as<AngleNode>() + P.node_off[d];
+            sa.n3 = P.n3;
+            sa.W = lv.w; sa.H = lv.h;
+            sa.mark_reached0 = l - 1 == 0 ? 1 : 0;
+            sa.thr = P.layer_score[l];
+            launch_cand_step(sa, P.C, st);
+        }
+    }
+    HIP_TRY(hipGetLastError());
+    // the single device -> host copy
+    char* h = P.h_out.as<char>();
+    HIP_TRY(hipMemcpyAsync(h + P.h_counts, P.d_counts.p, sizeof(int32_t) * J, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(h + P.h_peaks, P.d_peaks.p, sizeof(Peak) * (size_t)P.C, hipMemcpyDeviceToHost, st));
+    if (L > 0) {
+        HIP_TRY(hipMemcpyAsync(h + P.h_state, P.d_state.p, sizeof(CandState) * (size_t)P.C, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(h + P.h_rec, P.d_rec.p, sizeof(RoiRecord) * (size_t)P.C * P.n3, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(h + P.h_live, P.d_livecnt.p, sizeof(int32_t) * (L + 2), hipMemcpyDeviceToHost, st));
+    }
+    return FPM_OK;
+}
+
+// host finish for source s (TemplateMatcher.cpp:214-432)
+void finish_source(fpm_ctx* ctx, int s, std::vector<fpm_result>& out) {
+    Plan& P = ctx->plan;
+    const int L = P.L;
+    const char* h = P.h_out.as<char>();
+    const int32_t* counts = (const int32_t*)(h + P.h_counts);
+    const Peak* peaks = (const Peak*)(h + P.h_peaks);
+    const CandState* state = (const CandState*)(h + P.h_state);
+    const RoiRecord* rec = (const RoiRecord*)(h + P.h_rec);
+    struct TopCand { double score; int id; };
+    std::vector<HostMatch> cand;
+    std::vector<int> ids;
+    for (int a = 0; a < P.nang; ++a) {
+        const int job = s * P.nang + a;
+        for (int r = 0; r < counts[job]; ++r) {
+            const int id = job * P.cap + r;
+            const Peak& pk = peaks[id];
+            HostMatch m{};
+            const F2 pt = f2((float)pk.x - P.top[a].tx, (float)pk.y - P.top[a].ty);
+            m.ptx = pt.x; m.pty = pt.y;
+            m.score = pk.score;
+            m.angle = P.angles[a];
+            cand.push_back(m);
+            ids.push_back(id);
+        }
+    }
+    // std::sort(vecMatchParameter, compareScoreBig2Small) (:214): sort an index permutation with the same
+    // comparator and sequence so ties resolve exactly as the reference's introsort does.
+    std::vector<std::pair<HostMatch, int>> order(cand.size());
+    for (size_t i = 0; i < cand.size(); ++i) order[i] = {cand[i], ids[i]};
+    std::sort(order.begin(), order.end(),
+              [](const std::pair<HostMatch, int>& l, const std::pair<HostMatch, int>& r) { return l.first.score > r.first.score; });
+    std::vector<HostMatch> all;
+    const TmplLevel& t0 = ctx->tmpl[0];
+    for (auto& oc : order) {
+        HostMatch& c = oc.first;
+        const int id = oc.second;
+        if (L == 0) {   // iTopLayer <= iStopLayer (:272-276)
+            const double rad = -c.angle * kD2R;
+            const F2 lt = rotate_pt(f2((float)c.ptx, (float)c.pty), P.center, std::cos(rad), std::sin(rad));
+            c.ptx = lt.x; c.pty = lt.y;
+            all.push_back(c);
+            continue;
+        }
+        const CandState& cs = state[id];
+        if (!cs.reached0) continue;     // broke out at a layer > 0 (:331-332)
+        // layer 0 (:282-358) from the device's ROI records
+        const int d = L - 1;
+        const double astep = std::atan(2.0 / std::max(t0.w, t0.h)) * kR2D;
+        const SrcLevel& lv = ctx->src[0];
+        std::vector<HostMatch> nm(P.n3);
+        int imax = 0;
+        double big = -1;
+        for (int j = 0; j < P.n3; ++j) {
+            const RoiRecord& r = rec[(size_t)id * P.n3 + j];
+            HostMatch m{};
+            m.ptx = r.mx; m.pty = r.my;
+            m.score = r.score;
+            m.angle = P.nodes[d][(size_t)cs.node * P.n3 + j].angle;
+            m.on_border = r.on_border != 0;
+            for (int x = 0; x < 3; ++x)
+                for (int y = 0; y < 3; ++y) m.vec[x][y] = r.vec[x * 3 + y];
+            nm[j] = m;
+            if (nm[j].score > big) { imax = j; big = nm[j].score; }
+        }
+        if (nm[imax].score < P.layer_score[0]) continue;
+        if (ctx->prm.subpixel && !nm[imax].on_border && imax != 0 && imax != 2) {
+            double nx = 0, ny = 0, na = 0;
+            subpix_estimation(nm, &nx, &ny, &na, astep, imax);
+            nm[imax].ptx = nx; nm[imax].pty = ny;
+            nm[imax].angle = na;
+        }
+        const double nang = nm[imax].angle;
+        const F2 sc = f2((lv.w - 1) / 2.0f, (lv.h - 1) / 2.0f);
+        const double rad = nang * kD2R;
+        const F2 r0 = rotate_pt(f2(cs.lt.x * 2, cs.lt.y * 2), sc, std::cos(rad), std::sin(rad));
+        const F2 pad = f2(r0.x - 3, r0.y - 3);
+        F2 p = f2((float)(nm[imax].ptx + pad.x), (float)(nm[imax].pty + pad.y));
+        const double nrad = -nang * kD2R;
+        p = rotate_pt(p, sc, std::cos(nrad), std::sin(nrad));
+        nm[imax].ptx = p.x; nm[imax].pty = p.y;
+        all.push_back(nm[imax]);
+    }
+    filter_with_score(all, ctx->prm.score);
+    const int dstW = t0.w, dstH = t0.h;
+    for (HostMatch& m : all) {   // :380-390
+        const double rad = -m.angle * kD2R;
+        const F2 lt = f2((float)m.ptx, (float)m.pty);
+        const F2 rt = f2(lt.x + dstW * (float)std::cos(rad), lt.y - dstW * (float)std::sin(rad));
+        const F2 rb = f2(rt.x + dstH * (float)std::sin(rad), rt.y + dstH * (float)std::cos(rad));
+        m.rect = rrect_from3(lt, rt, rb);
+        m.del = false;
+    }
+    filter_with_rotated_rect(all, ctx->prm.max_overlap);
+    std::sort(all.begin(), all.end(), score_big2small);
+    out.clear();
+    for (const HostMatch& m : all) {   // :406-432
+        const double rad = -m.angle * kD2R;
+        const F2 lt = f2((float)m.ptx, (float)m.pty);
+        const F2 rt = f2(lt.x + t0.w * (float)std::cos(rad), lt.y - t0.w * (float)std::sin(rad));
+        const F2 lb = f2(lt.x + t0.h * (float)std::sin(rad), lt.y + t0.h * (float)std::cos(rad));
+        const F2 rb = f2(rt.x + t0.h * (float)std::sin(rad), rt.y + t0.h * (float)std::cos(rad));
+        const F2 c = f2((lt.x + rt.x + lb.x + rb.x) / 4.0f, (lt.y + rt.y + lb.y + rb.y) / 4.0f);
+        fpm_result o;
+        o.lt_x = lt.x; o.lt_y = lt.y; o.rt_x = rt.x; o.rt_y = rt.y;
+        o.rb_x = rb.x; o.rb_y = rb.y; o.lb_x = lb.x; o.lb_y = lb.y;
+        o.cx = c.x; o.cy = c.y; o.angle = m.angle; o.score = m.score;
+        out.push_back(o);
+    }
+}
+
+int run_staged(fpm_ctx* ctx, std::vector<std::vector<fpm_result>>& results) {
+    int rc = build_plan(ctx);
+    if (rc != FPM_OK) return rc;
+    rc = enqueue_search(ctx);
+    if (rc != FPM_OK) return rc;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    prof_collect(ctx);
+    Plan& P = ctx->plan;
+    results.assign(P.S, {});
+    for (int s = 0; s < P.S; ++s) finish_source(ctx, s, results[s]);
+    // stats: [angles, top candidates, live entering layer L-1 .. 0] (totals over the batch)
+    const char* h = P.h_out.as<char>();
+    const int32_t* counts = (const int32_t*)(h + P.h_counts);
+    int64_t topc = 0;
+    for (int k = 0; k < P.S * P.nang; ++k) topc += counts[k];
+    ctx->stats.assign({(int64_t)P.nang, topc});
+    const int32_t* lc = (const int32_t*)(h + P.h_live);
+    for (int d = 0; d < P.L; ++d) ctx->stats.push_back(lc[d]);
+    if (ctx->prof) {   // refinement bytes need the live counts
+        for (int d = 0; d < P.L; ++d) {
+            const int l = P.L - 1 - d;
+            const TmplLevel& t = ctx->tmpl[l];
+            const int64_t rois = (int64_t)lc[d] * P.n3;
+            ctx->kp[FPM_K_ROI_CORR].bytes += rois * ((int64_t)(t.w + 6) * (t.h + 6) + (int64_t)t.w * t.h + 49 * 4);
+        }
+    }
+    return FPM_OK;
+}
+
+int upload_sources(fpm_ctx* ctx, const uint8_t* const* grays, int count, int w, int h, size_t stride) {
+    int rc = layout_sources(ctx, count, w, h);
+    if (rc != FPM_OK) return rc;
+    const SrcLevel& l0 = ctx->src[0];
+    for (int s = 0; s < count; ++s)
+        HIP_TRY(hipMemcpy2DAsync(ctx->d_src.as<uint8_t>() + l0.off + l0.img_bytes * s, l0.pitch, grays[s], stride, w, h,
+                                 hipMemcpyHostToDevice, ctx->stream));
+    return FPM_OK;
+}
+
+}  // namespace
+
+// =========================================================================================================
+// C ABI
+// =========================================================================================================
+extern "C" {
+
+void fpm_params_default(fpm_params* p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    p->max_pos = 70;            // TemplateMatcher.cpp:29
+    p->max_overlap = 0.0;       // :30
+    p->score = 0.7;             // :31
+    p->tolerance_angle = 0.0;   // :32
+    p->min_reduce_area = 256;   // :33
+    p->use_simd = 1;            // :34
+    p->subpixel = 0;            // :35
+    p->tolerance_range = 0;     // :38
+}
+
+int fpm_abi_version(void) { return FPM_ABI_VERSION; }
+
+int fpm_create(int device, fpm_ctx** out) {
+    if (!out) return FPM_E_INVALID_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) return FPM_E_DEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return FPM_E_DEVICE;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return FPM_E_DEVICE;
+    fpm_ctx* ctx = new (std::nothrow) fpm_ctx();
+    if (!ctx) return FPM_E_INTERNAL;
+    ctx->device = device;
+    fpm_params_default(&ctx->prm);
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return FPM_E_DEVICE;
+    }
+    *out = ctx;
+    return FPM_OK;
+}
+
+int fpm_destroy(fpm_ctx* ctx) {
+    if (!ctx) return FPM_E_INVALID_ARG;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    ctx->plan.release();
+    ctx->d_tmpl.release(); ctx->d_src.release();
+    ctx->d_op_a.release(); ctx->d_op_b.release(); ctx->d_op_job.release();
+    for (auto& k : ctx->kp)
+        for (auto& e : k.ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return FPM_OK;
+}
+
+const char* fpm_last_error(const fpm_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int fpm_set_params(fpm_ctx* ctx, const fpm_params* p) {
+    if (!ctx || !p) return FPM_E_INVALID_ARG;
+    ctx->prm = *p;
+    return FPM_OK;
+}
+
+int fpm_get_params(const fpm_ctx* ctx, fpm_params* p) {
+    if (!ctx || !p) return FPM_E_INVALID_ARG;
+    *p = ctx->prm;
+    return FPM_OK;
+}
+
+// TemplateMatcher::learnPattern (TemplateMatcher.cpp:45-95)
+int fpm_learn(fpm_ctx* ctx, const uint8_t* gray, int32_t w, int32_t h, size_t stride) {
+    if (!ctx) return FPM_E_INVALID_ARG;
+    if (!gray || w <= 0 || h <= 0 || stride < (size_t)w) { ctx->err = "empty template"; return FPM_E_INVALID_ARG; }
+    HIP_TRY(hipSetDevice(ctx->device));
+    ctx->learned = false;
+    ctx->tmpl.clear();
+    const int L = top_layer(w, h, (int)std::sqrt((double)ctx->prm.min_reduce_area));
+    std::vector<TmplLevel> lv(L + 1);
+    size_t off = 0;
+    int lw = w, lh = h;
+    for (int l = 0; l <= L; ++l) {
+        lv[l].w = lw; lv[l].h = lh;
+        lv[l].pitch = round_up(lw + 4, 64);
+        lv[l].off = off;
+        off += round_up((size_t)lv[l].pitch * (lh + 1), (size_t)256);
+        lw = (lw + 1) / 2;
+        lh = (lh + 1) / 2;
+    }
+    HIP_TRY(ctx->d_tmpl.ensure(off));
+    uint8_t* base = ctx->d_tmpl.as<uint8_t>();
+    HIP_TRY(hipMemsetAsync(base, 0, off, ctx->stream));
+    HIP_TRY(hipMemcpy2DAsync(base + lv[0].off, lv[0].pitch, gray, stride, w, h, hipMemcpyHostToDevice, ctx->stream));
+    for (int l = 1; l <= L; ++l)   // cv::buildPyramid (:55) on the device
+        launch_pyr_down(base + lv[l - 1].off, lv[l - 1].w, lv[l - 1].h, lv[l - 1].pitch, 0, base + lv[l].off, lv[l].w,
+                        lv[l].h, lv[l].pitch, 0, 1, ctx->stream);
+    HIP_TRY(hipGetLastError());
+    for (int l = 0; l <= L; ++l) {
+        lv[l].px.resize((size_t)lv[l].w * lv[l].h);
+        HIP_TRY(hipMemcpy2DAsync(lv[l].px.data(), lv[l].w, base + lv[l].off, lv[l].pitch, lv[l].w, lv[l].h,
+                                 hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    double m0, s0;
+    mean_stddev(lv[0].px, &m0, &s0);
+    ctx->border = m0 < 128 ? 255 : 0;   // :58-59
+    for (int l = 0; l <= L; ++l) {      // :66-91
+        const double inv_area = 1.0 / ((double)lv[l].h * lv[l].w);
+        double mean, sdv;
+        mean_stddev(lv[l].px, &mean, &sdv);
+        double norm = sdv * sdv;
+        lv[l].equal1 = norm < DBL_EPSILON;
+        norm = std::sqrt(norm);
+        norm /= std::sqrt(inv_area);
+        lv[l].mean = mean; lv[l].norm = norm; lv[l].inv_area = inv_area;
+    }
+    ctx->tmpl = std::move(lv);
+    ctx->learned = true;
+    ctx->tmpl_gen++;
+    return FPM_OK;
+}
+
+int fpm_clear_pattern(fpm_ctx* ctx) {
+    if (!ctx) return FPM_E_INVALID_ARG;
+    ctx->learned = false;
+    ctx->tmpl.clear();
+    ctx->tmpl_gen++;
+    return FPM_OK;
+}
+
+int fpm_is_learned(const fpm_ctx* ctx) { return ctx && ctx->learned ? 1 : 0; }
+
+int fpm_stage_sources(fpm_ctx* ctx, const uint8_t* const* grays, int32_t count, int32_t w, int32_t h, size_t stride) {
+    if (!ctx) return FPM_E_INVALID_ARG;
+    if (!grays || count <= 0 || w <= 0 || h <= 0 || stride < (size_t)w) { ctx->err = "bad sources"; return FPM_E_INVALID_ARG; }
+    for (int i = 0; i < count; ++i)
+        if (!grays[i]) { ctx->err = "null source"; return FPM_E_INVALID_ARG; }
+    int rc = check_sizes(ctx, w, h);
+    if (rc != FPM_OK) return rc;
+    HIP_TRY(hipSetDevice(ctx->device));
+    rc = upload_sources(ctx, grays, count, w, h, stride);
+    if (rc != FPM_OK) return rc;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return FPM_OK;
+}
+
+int fpm_match_staged(fpm_ctx* ctx, fpm_result* out, int32_t cap, int32_t* n_results) {
+    if (!ctx || !n_results) return FPM_E_INVALID_ARG;
+    if (!ctx->learned) { ctx->err = "template not learned"; return FPM_E_NOT_LEARNED; }
+    if (ctx->S <= 0) { ctx->err = "no staged sources"; return FPM_E_INVALID_ARG; }
+    HIP_TRY(hipSetDevice(ctx->device));
+    std::vector<std::vector<fpm_result>> res;
+    int rc = run_staged(ctx, res);
+    if (rc != FPM_OK) return rc;
+    int status = FPM_OK;
+    for (int s = 0; s < ctx->S; ++s) {
+        n_results[s] = (int32_t)res[s].size();
+        for (int i = 0; i < (int)res[s].size(); ++i) {
+            if (i < cap && out) out[(size_t)s * cap + i] = res[s][i];
+            else status = FPM_E_CAPACITY;
+        }
+    }
+    return status;
+}
+
+// TemplateMatcher::match (TemplateMatcher.cpp:97-437)
+int fpm_match(fpm_ctx* ctx, const uint8_t* gray, int32_t w, int32_t h, size_t stride, fpm_result* out, int32_t cap,
+              int32_t* n_results, double* seconds) {
+    if (!ctx || !n_results) return FPM_E_INVALID_ARG;
+    *n_results = 0;
+    if (!gray || w <= 0 || h <= 0 || stride < (size_t)w) { ctx->err = "empty source"; return FPM_E_INVALID_ARG; }
+    int rc = check_sizes(ctx, w, h);
+    if (rc != FPM_OK) return rc;
+    HIP_TRY(hipSetDevice(ctx->device));
+    const auto t0 = std::chrono::high_resolution_clock::now();
+    rc = upload_sources(ctx, &gray, 1, w, h, stride);
+    if (rc != FPM_OK) return rc;
+    std::vector<std::vector<fpm_result>> res;
+    rc = run_staged(ctx, res);
+    if (rc != FPM_OK) return rc;
+    const auto t1 = std::chrono::high_resolution_clock::now();
+    const std::vector<fpm_result>& r = res[0];
+    *n_results = (int32_t)r.size();
+    if (!r.empty() && seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
+    for (int i = 0; i < (int)r.size() && i < cap && out; ++i) out[i] = r[i];
+    return (int)r.size() > cap ? FPM_E_CAPACITY : FPM_OK;
+}
+
+int fpm_search_stats(const fpm_ctx* ctx, int64_t* stats, int32_t cap) {
+    if (!ctx || !stats) return FPM_E_INVALID_ARG;
+    int n = 0;
+    for (int64_t v : ctx->stats)
+        if (n < cap) stats[n++] = v;
+    return n;
+}
+
+int fpm_template_info(const fpm_ctx* ctx, int32_t* levels, int32_t* border_color) {
+    if (!ctx || !levels || !border_color) return FPM_E_INVALID_ARG;
+    if (!ctx->learned) return FPM_E_NOT_LEARNED;
+    *levels = (int32_t)ctx->tmpl.size();
+    *border_color = ctx->border;
+    return FPM_OK;
+}
+
+int fpm_template_level(const fpm_ctx* ctx, int32_t level, int32_t* w, int32_t* h, double* mean, double* norm,
+                       double* inv_area, int32_t* result_equal1, uint8_t* pixels, size_t stride) {
+    if (!ctx || !w || !h || !mean || !norm || !inv_area || !result_equal1) return FPM_E_INVALID_ARG;
+    if (!ctx->learned) return FPM_E_NOT_LEARNED;
+    if (level < 0 || level >= (int)ctx->tmpl.size()) return FPM_E_INVALID_ARG;
+    const TmplLevel& t = ctx->tmpl[level];
+    *w = t.w; *h = t.h; *mean = t.mean; *norm = t.norm; *inv_area = t.inv_area; *result_equal1 = t.equal1 ? 1 : 0;
+    if (pixels)
+        for (int y = 0; y < t.h; ++y) std::memcpy(pixels + (size_t)y * stride, t.px.data() + (size_t)y * t.w, (size_t)t.w);
+    return FPM_OK;
+}
+
+// ---- pixel operators ----------------------------------------------------------------------------------
+int fpm_op_pyr_down(fpm_ctx* ctx, const uint8_t* src, int32_t w, int32_t h, size_t ss, uint8_t* dst, size_t ds) {
+    if (!ctx) return FPM_E_INVALID_ARG;
+    if (!src || !dst || w <= 0 || h <= 0 || ss < (size_t)w) { ctx->err = "bad image"; return FPM_E_INVALID_ARG; }
+    const int dw = (w + 1) / 2, dh = (h + 1) / 2;
+    if (ds < (size_t)dw) { ctx->err = "bad dst stride"; return FPM_E_INVALID_ARG; }
+    HIP_TRY(hipSetDevice(ctx->device));
+    const int sp = round_up(w + 4, 64), dp = round_up(dw + 4, 64);
+    HIP_TRY(ctx->d_op_a.ensure((size_t)sp * (h + 1)));
+    HIP_TRY(ctx->d_op_b.ensure((size_t)dp * (dh + 1)));
+    HIP_TRY(hipMemcpy2DAsync(ctx->d_op_a.p, sp, src, ss, w, h, hipMemcpyHostToDevice, ctx->stream));
+    launch_pyr_down(ctx->d_op_a.as<uint8_t>(), w, h, sp, 0, ctx->d_op_b.as<uint8_t>(), dw, dh, dp, 0, 1, ctx->stream);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy2DAsync(dst, ds, ctx->d_op_b.p, dp, dw, dh, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return FPM_OK;
+}
+
+int fpm_op_warp_affine(fpm_ctx* ctx, const uint8_t* src, int32_t w, int32_t h, size_t ss, const double m[6],
+                       uint8_t* dst, int32_t dw, int32_t dh, size_t ds, int32_t border) {
+    if (!ctx) return FPM_E_INVALID_ARG;
+    if (!src || !dst || !m || w <= 0 || h <= 0 || dw <= 0 || dh <= 0 || ss < (size_t)w || ds < (size_t)dw) {
+        ctx->err = "bad warp arguments";
+        return FPM_E_INVALID_ARG;
+    }
+    HIP_TRY(hipSetDevice(ctx->device));
+    const int sp = round_up(w + 4, 64), dp = round_up(dw + 4, 64);
+    HIP_TRY(ctx->d_op_a.ensure((size_t)sp * (h + 1)));
+    HIP_TRY(ctx->d_op_b.ensure((size_t)dp * (dh + 1)));
+    HIP_TRY(ctx->d_op_job.ensure(sizeof(WarpJob)));
+    WarpJob j{};
+    j.src = ctx->d_op_a.as<uint8_t>(); j.sw = w; j.sh = h; j.sp = sp;
+    j.dst = ctx->d_op_b.as<uint8_t>(); j.dw = dw; j.dh = dh; j.dp = dp;
+    j.border = border;
+    std::copy(m, m + 6, j.M);
+    invert_affine(j.M);
+    HIP_TRY(hipMemcpyAsync(ctx->d_op_job.p, &j, sizeof(j), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpy2DAsync(ctx->d_op_a.p, sp, src, ss, w, h, hipMemcpyHostToDevice, ctx->stream));
+    launch_warp(ctx->d_op_job.as<WarpJob>(), 1, dw * dh, ctx->stream);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy2DAsync(dst, ds, ctx->d_op_b.p, dp, dw, dh, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return FPM_OK;
+}
+
+int fpm_op_ncc_map(fpm_ctx* ctx, const uint8_t* src, int32_t w, int32_t h, size_t ss, int32_t layer, int32_t fold,
+                   float* out) {
+    if (!ctx) return FPM_E_INVALID_ARG;
+    if (!ctx->learned) { ctx->err = "template not learned"; return FPM_E_NOT_LEARNED; }
+    if (!src || !out || w <= 0 || h <= 0 || ss < (size_t)w || layer < 0 || layer >= (int)ctx->tmpl.size()) {
+        ctx->err = "bad ncc arguments";
+        return FPM_E_INVALID_ARG;
+    }
+    const TmplLevel& t = ctx->tmpl[layer];
+    if (w < t.w || h < t.h) { ctx->err = "image smaller than template level"; return FPM_E_SIZE; }
+    HIP_TRY(hipSetDevice(ctx->device));
+    const int ow = w - t.w + 1, oh = h - t.h + 1;
+    const int sp = round_up(w + 4, 64);
+    HIP_TRY(ctx->d_op_a.ensure((size_t)sp * (h + 1)));
+    HIP_TRY(ctx->d_op_b.ensure(sizeof(float) * (size_t)ow * oh));
+    HIP_TRY(ctx->d_op_job.ensure(sizeof(NccJob)));
+    NccJob j{};
+    j.img = ctx->d_op_a.as<uint8_t>(); j.iw = w; j.ih = h; j.ip = sp;
+    j.tmpl = ctx->d_tmpl.as<uint8_t>() + t.off; j.tw = t.w; j.th = t.h; j.tp = t.pitch;
+    j.out = ctx->d_op_b.as<float>(); j.ow = ow; j.oh = oh;
+    j.fold = fold ? 1 : 0;
+    j.equal1 = t.equal1 ? 1 : 0;
+    j.mean = t.mean; j.norm = t.norm; j.inv_area = t.inv_area;
+    HIP_TRY(hipMemcpyAsync(ctx->d_op_job.p, &j, sizeof(j), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpy2DAsync(ctx->d_op_a.p, sp, src, ss, w, h, hipMemcpyHostToDevice, ctx->stream));
+    launch_ncc_map(ctx->d_op_job.as<NccJob>(), 1, ow * oh, t.w * t.h, ctx->stream);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out, ctx->d_op_b.p, sizeof(float) * (size_t)ow * oh, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return FPM_OK;
+}
+
+// ---- profiling ----------------------------------------------------------------------------------------
+int fpm_profile_enable(fpm_ctx* ctx, int32_t enable) {
+    if (!ctx) return FPM_E_INVALID_ARG;
+    ctx->prof = enable != 0;
+    return FPM_OK;
+}
+
+int fpm_profile_reset(fpm_ctx* ctx) {
+    if (!ctx) return FPM_E_INVALID_ARG;
+    for (auto& k : ctx->kp) { k.ms = 0; k.launches = 0; k.bytes = 0; k.used = 0; }
+    return FPM_OK;
+}
+
+int fpm_profile_get(const fpm_ctx* ctx, int32_t kernel, double* total_ms, int64_t* launches, int64_t* bytes) {
+    if (!ctx || kernel < 0 || kernel >= FPM_K_COUNT || !total_ms || !launches || !bytes) return FPM_E_INVALID_ARG;
+    *total_ms = ctx->kp[kernel].ms;
+    *launches = ctx->kp[kernel].launches;
+    *bytes = ctx->kp[kernel].bytes;
+    return FPM_OK;
+}
+
+}  // extern "C"

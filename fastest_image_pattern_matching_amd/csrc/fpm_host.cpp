@@ -1,0 +1,281 @@
+// fpm_host.cpp — host stages of the search: final score filter, rotated-rectangle overlap suppression and the
+// optional sub-pixel quadric fit.  These are O(n^2)/O(1) control code over a few hundred results, run once
+// per search after the single device->host copy; they follow the reference line by line so that the surviving
+// set and order are identical (TemplateMatcher.cpp:373-395, 984-1194) and the OpenCV geometry primitives
+// they call (OpenCV 4.5.x semantics).  Compile with -ffp-contract=off.
+#include "fpm_host.h"
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+
+namespace fpm {
+
+bool score_big2small(const HostMatch& a, const HostMatch& b) { return a.score > b.score; }
+
+static inline double len2(float x, float y) { return std::sqrt((double)x * x + (double)y * y); }
+
+RRect rrect_from3(F2 p1, F2 p2, F2 p3) {
+    RRect r;
+    r.c = f2(0.5f * (p1.x + p3.x), 0.5f * (p1.y + p3.y));
+    const F2 e0 = f2(p1.x - p2.x, p1.y - p2.y);
+    const F2 e1 = f2(p2.x - p3.x, p2.y - p3.y);
+    // width = the edge whose slope lies in [-1, 1]; preference to e1 as in OpenCV
+    const bool w_is_e1 = std::fabs(e1.y) < std::fabs(e1.x);
+    const F2 we = w_is_e1 ? e1 : e0, he = w_is_e1 ? e0 : e1;
+    r.angle = std::atan(we.y / we.x) * 180.0f / (float)kPi;
+    r.w = (float)len2(we.x, we.y);
+    r.h = (float)len2(he.x, he.y);
+    return r;
+}
+
+static void rrect_corners(const RRect& r, F2 pt[4]) {
+    const double rad = r.angle * kPi / 180.;
+    const float b = (float)std::cos(rad) * 0.5f;
+    const float a = (float)std::sin(rad) * 0.5f;
+    pt[0] = f2(r.c.x - a * r.h - b * r.w, r.c.y + b * r.h - a * r.w);
+    pt[1] = f2(r.c.x + a * r.h - b * r.w, r.c.y - b * r.h - a * r.w);
+    pt[2] = f2(2 * r.c.x - pt[0].x, 2 * r.c.y - pt[0].y);
+    pt[3] = f2(2 * r.c.x - pt[1].x, 2 * r.c.y - pt[1].y);
+}
+
+// returns 0 = INTERSECT_NONE, 1 = INTERSECT_PARTIAL, 2 = INTERSECT_FULL
+int rrect_intersection(const RRect& ra, const RRect& rb, std::vector<F2>& pts) {
+    pts.clear();
+    F2 A[4], B[4], eA[4], eB[4];
+    rrect_corners(ra, A);
+    rrect_corners(rb, B);
+    float eps = 1e-6f * std::max(ra.w * ra.h, rb.w * rb.h);
+    bool coincident = true;
+    for (int i = 0; i < 4 && coincident; ++i)
+        coincident = !(std::fabs(A[i].x - B[i].x) > eps || std::fabs(A[i].y - B[i].y) > eps);
+    if (coincident) {
+        pts.assign(A, A + 4);
+        return 2;
+    }
+    for (int i = 0; i < 4; ++i) {
+        const int n = (i + 1) & 3;
+        eA[i] = f2(A[n].x - A[i].x, A[n].y - A[i].y);
+        eB[i] = f2(B[n].x - B[i].x, B[n].y - B[i].y);
+    }
+    for (int i = 0; i < 4; ++i) {
+        eps = std::min(eps, std::sqrt(eA[i].x * eA[i].x + eA[i].y * eA[i].y));
+        eps = std::min(eps, std::sqrt(eB[i].x * eB[i].x + eB[i].y * eB[i].y));
+    }
+    eps = std::max(1e-16f, eps);
+    int kind = 2;
+    // edge-edge crossings
+    for (int i = 0; i < 4; ++i) {
+        for (int j = 0; j < 4; ++j) {
+            const float dx = B[j].x - A[i].x, dy = B[j].y - A[i].y;
+            const float det = eB[j].x * eA[i].y - eA[i].x * eB[j].y;
+            if (std::fabs(det) < 1e-12) continue;
+            const float ta = (eB[j].x * dy - eB[j].y * dx) / det;
+            const float tb = (eA[i].x * dy - eA[i].y * dx) / det;
+            if (!std::isfinite(ta) || !std::isfinite(tb)) continue;
+            if (ta >= 0.0f && ta <= 1.0f && tb >= 0.0f && tb <= 1.0f)
+                pts.push_back(f2(A[i].x + eA[i].x * ta, A[i].y + eA[i].y * ta));
+        }
+    }
+    if (!pts.empty()) kind = 1;
+    // corners of one rectangle inside the other (sign test against the 4 edge lines)
+    auto inside = [](const F2& p, const F2* Q, const F2* eQ) {
+        int pos = 0, neg = 0;
+        for (int j = 0; j < 4; ++j) {
+            const float a = -eQ[j].y, b = eQ[j].x;
+            const float c = -(a * Q[j].x + b * Q[j].y);
+            const float s = a * p.x + b * p.y + c;
+            if (s >= 0) ++pos; else ++neg;
+        }
+        return pos == 4 || neg == 4;
+    };
+    for (int i = 0; i < 4; ++i)
+        if (inside(A[i], B, eB)) pts.push_back(A[i]);
+    for (int i = 0; i < 4; ++i)
+        if (inside(B[i], A, eA)) pts.push_back(B[i]);
+    int n = (int)pts.size();
+    if (n == 0) return 0;
+    // drop near-duplicates (swap-with-last), remembering pairwise distances for the > 8 pass
+    const int stride = n;
+    std::vector<float> dist((size_t)n * n, 0.f);
+    std::vector<int> slot(n);
+    for (int i = 0; i < n; ++i) {
+        slot[i] = i;
+        const F2 p = pts[i];
+        int j = i + 1;
+        while (j < n) {
+            const float ddx = pts[j].x - p.x, ddy = pts[j].y - p.y;
+            const float d2 = ddx * ddx + ddy * ddy;
+            if (d2 <= eps) {
+                if (j < n - 1) pts[j] = pts[n - 1];
+                --n;
+                continue;
+            }
+            dist[(size_t)i * stride + j] = d2;
+            ++j;
+        }
+    }
+    while (n > 8) {
+        int bj = 1;
+        float bd = dist[1];
+        for (int i = 0; i < n - 1; ++i) {
+            const float* row = dist.data() + (size_t)stride * slot[i];
+            for (int j = i + 1; j < n; ++j)
+                if (row[slot[j]] < bd) { bd = row[slot[j]]; bj = j; }
+        }
+        if (bj < n - 1) { pts[bj] = pts[n - 1]; slot[bj] = slot[n - 1]; }
+        --n;
+    }
+    pts.resize(n);
+    return kind;
+}
+
+void sort_pt_with_center(std::vector<F2>& pts) {
+    const int n = (int)pts.size();
+    F2 ctr = f2(0.f, 0.f);
+    for (const F2& p : pts) { ctr.x += p.x; ctr.y += p.y; }
+    ctr.x = ctr.x / n;
+    ctr.y = ctr.y / n;
+    std::vector<std::pair<F2, double>> keyed(n);
+    for (int i = 0; i < n; ++i) {
+        const F2 d = f2(pts[i].x - ctr.x, pts[i].y - ctr.y);
+        const float nn = d.x * d.x + d.y * d.y;   // (squared norm: reference behaviour)
+        double key;
+        if (d.y < 0) key = std::acos(d.x / nn) * kR2D;
+        else if (d.y > 0) key = 360 - std::acos(d.x / nn) * kR2D;
+        else key = (d.x - ctr.x > 0) ? 0 : 180;
+        keyed[i] = std::make_pair(pts[i], key);
+    }
+    std::sort(keyed.begin(), keyed.end(),
+              [](const std::pair<F2, double> l, const std::pair<F2, double> r) { return l.second < r.second; });
+    for (int i = 0; i < n; ++i) pts[i] = keyed[i].first;
+}
+
+double contour_area(const std::vector<F2>& pts) {
+    const int n = (int)pts.size();
+    if (n == 0) return 0.;
+    double acc = 0;
+    F2 prev = pts[n - 1];
+    for (const F2& p : pts) {
+        acc += (double)prev.x * p.y - (double)prev.y * p.x;
+        prev = p;
+    }
+    return std::fabs(acc * 0.5);
+}
+
+void filter_with_score(std::vector<HostMatch>& v, double score) {
+    std::sort(v.begin(), v.end(), score_big2small);
+    for (size_t i = 0; i < v.size(); ++i)
+        if (v[i].score < score) { v.erase(v.begin() + (long)i, v.end()); return; }
+}
+
+void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
+    if (v.empty()) return;
+    const int n = (int)v.size();
+    std::vector<F2> pts;
+    for (int i = 0; i + 1 < n; ++i) {
+        if (v[i].del) continue;
+        for (int j = i + 1; j < n; ++j) {
+            if (v[j].del) continue;
+            const int kind = rrect_intersection(v[i].rect, v[j].rect, pts);
+            if (kind == 0) continue;
+            bool drop = kind == 2;
+            if (kind == 1) {
+                if (pts.size() < 3) continue;
+                sort_pt_with_center(pts);
+                const double ratio = contour_area(pts) / (v[i].rect.w * v[i].rect.h);
+                drop = ratio > max_overlap;
+            }
+            if (drop) v[(v[i].score >= v[j].score) ? j : i].del = true;
+        }
+    }
+    v.erase(std::remove_if(v.begin(), v.end(), [](const HostMatch& m) { return m.del; }), v.end());
+}
+
+// (A^T A)^-1 by LU with partial pivoting (cv::invert, DECOMP_LU -> hal::LU64f), n x n, row-major.
+static bool invert_lu(std::vector<double> a, int n, std::vector<double>& inv) {
+    inv.assign((size_t)n * n, 0.0);
+    for (int i = 0; i < n; ++i) inv[(size_t)i * n + i] = 1.0;
+    for (int i = 0; i < n; ++i) {
+        int piv = i;
+        for (int r = i + 1; r < n; ++r)
+            if (std::fabs(a[(size_t)r * n + i]) > std::fabs(a[(size_t)piv * n + i])) piv = r;
+        if (std::fabs(a[(size_t)piv * n + i]) < DBL_EPSILON * 100) return false;
+        if (piv != i) {
+            for (int c = i; c < n; ++c) std::swap(a[(size_t)i * n + c], a[(size_t)piv * n + c]);
+            for (int c = 0; c < n; ++c) std::swap(inv[(size_t)i * n + c], inv[(size_t)piv * n + c]);
+        }
+        const double d = -1 / a[(size_t)i * n + i];
+        for (int r = i + 1; r < n; ++r) {
+            const double alpha = a[(size_t)r * n + i] * d;
+            for (int c = i + 1; c < n; ++c) a[(size_t)r * n + c] += alpha * a[(size_t)i * n + c];
+            for (int c = 0; c < n; ++c) inv[(size_t)r * n + c] += alpha * inv[(size_t)i * n + c];
+        }
+    }
+    for (int i = n - 1; i >= 0; --i)
+        for (int c = 0; c < n; ++c) {
+            double s = inv[(size_t)i * n + c];
+            for (int k = i + 1; k < n; ++k) s -= a[(size_t)i * n + k] * inv[(size_t)k * n + c];
+            inv[(size_t)i * n + c] = s / a[(size_t)i * n + i];
+        }
+    return true;
+}
+
+void subpix_estimation(const std::vector<HostMatch>& v, double* dx, double* dy, double* dangle, double angle_step,
+                       int imax) {
+    double A[27][10], S[27];
+    const double x0 = v[imax].ptx, y0 = v[imax].pty, t0 = v[imax].angle;
+    int row = 0;
+    for (int th = 0; th <= 2; ++th)
+        for (int y = -1; y <= 1; ++y)
+            for (int x = -1; x <= 1; ++x, ++row) {
+                const double X = x0 + x, Y = y0 + y, T = (t0 + (th - 1) * angle_step) * kD2R;
+                const double r[10] = {X * X, Y * Y, T * T, X * Y, X * T, Y * T, X, Y, T, 1.0};
+                for (int k = 0; k < 10; ++k) A[row][k] = r[k];
+                S[row] = v[imax + (th - 1)].vec[x + 1][y + 1];
+            }
+    std::vector<double> ata(100), inv;
+    for (int i = 0; i < 10; ++i)
+        for (int j = 0; j < 10; ++j) {
+            double s = 0;
+            for (int r = 0; r < 27; ++r) s += A[r][i] * A[r][j];
+            ata[(size_t)i * 10 + j] = s;
+        }
+    if (!invert_lu(ata, 10, inv)) inv.assign(100, 0.0);
+    double Z[10];
+    std::vector<double> ia(10 * 27);
+    for (int i = 0; i < 10; ++i)
+        for (int r = 0; r < 27; ++r) {
+            double s = 0;
+            for (int k = 0; k < 10; ++k) s += inv[(size_t)i * 10 + k] * A[r][k];
+            ia[(size_t)i * 27 + r] = s;
+        }
+    for (int i = 0; i < 10; ++i) {
+        double s = 0;
+        for (int r = 0; r < 27; ++r) s += ia[(size_t)i * 27 + r] * S[r];
+        Z[i] = s;
+    }
+    const double K[3][3] = {{2 * Z[0], Z[3], Z[4]}, {Z[3], 2 * Z[1], Z[5]}, {Z[4], Z[5], 2 * Z[2]}};
+    const double rhs[3] = {-Z[6], -Z[7], -Z[8]};
+    // closed-form 3x3 inverse (cv::invert for n == 3)
+    double det = K[0][0] * (K[1][1] * K[2][2] - K[1][2] * K[2][1]) - K[0][1] * (K[1][0] * K[2][2] - K[1][2] * K[2][0]) +
+                 K[0][2] * (K[1][0] * K[2][1] - K[1][1] * K[2][0]);
+    double t[9] = {0};
+    if (det != 0.) {
+        det = 1. / det;
+        t[0] = (K[1][1] * K[2][2] - K[1][2] * K[2][1]) * det;
+        t[1] = (K[0][2] * K[2][1] - K[0][1] * K[2][2]) * det;
+        t[2] = (K[0][1] * K[1][2] - K[0][2] * K[1][1]) * det;
+        t[3] = (K[1][2] * K[2][0] - K[1][0] * K[2][2]) * det;
+        t[4] = (K[0][0] * K[2][2] - K[0][2] * K[2][0]) * det;
+        t[5] = (K[0][2] * K[1][0] - K[0][0] * K[1][2]) * det;
+        t[6] = (K[1][0] * K[2][1] - K[1][1] * K[2][0]) * det;
+        t[7] = (K[0][1] * K[2][0] - K[0][0] * K[2][1]) * det;
+        t[8] = (K[0][0] * K[1][1] - K[0][1] * K[1][0]) * det;
+    }
+    *dx = t[0] * rhs[0] + t[1] * rhs[1] + t[2] * rhs[2];
+    *dy = t[3] * rhs[0] + t[4] * rhs[1] + t[5] * rhs[2];
+    *dangle = (t[6] * rhs[0] + t[7] * rhs[1] + t[8] * rhs[2]) * kR2D;
+}
+
+}  // namespace fpm

@@ -1,0 +1,35 @@
+// fpm_host.h — host-side stages of the search that are not data-parallel.
+#pragma once
+#include <vector>
+
+#include "fpm_geom.h"
+
+namespace fpm {
+
+// cv::RotatedRect (center, size, angle in degrees)
+struct RRect {
+    F2 c;
+    float w, h, angle;
+};
+
+// s_MatchParameter subset carried through the host stages (DataStructures.h:58-94)
+struct HostMatch {
+    double ptx, pty;
+    double score, angle;
+    RRect rect;
+    bool del;
+    bool on_border;
+    double vec[3][3];
+};
+
+RRect rrect_from3(F2 p1, F2 p2, F2 p3);                              // cv::RotatedRect(p1, p2, p3)
+int rrect_intersection(const RRect& a, const RRect& b, std::vector<F2>& pts);  // rotatedRectangleIntersection
+void sort_pt_with_center(std::vector<F2>& pts);                      // TemplateMatcher.cpp:1093-1131
+double contour_area(const std::vector<F2>& pts);                     // cv::contourArea
+void filter_with_score(std::vector<HostMatch>& v, double score);     // TemplateMatcher.cpp:984-1000
+void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap);  // :1133-1194
+void subpix_estimation(const std::vector<HostMatch>& v, double* dx, double* dy, double* dangle,
+                       double angle_step, int imax);                 // :1002-1072
+bool score_big2small(const HostMatch& a, const HostMatch& b);        // compareScoreBig2Small (:14-17)
+
+}  // namespace fpm

@@ -1,0 +1,131 @@
+// fpm_kernels.h — device job descriptors and kernel launchers (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fpm_geom.h"
+
+namespace fpm {
+
+// K2 / fpm_op_warp_affine: one inverse-mapped bilinear warp (cv::warpAffine INTER_LINEAR, BORDER_CONSTANT).
+struct WarpJob {
+    const uint8_t* src;
+    uint8_t* dst;
+    int32_t sw, sh, sp;      // source size, row pitch (bytes)
+    int32_t dw, dh, dp;      // destination size, row pitch
+    int32_t border;
+    int32_t pad;
+    double M[6];             // INVERTED matrix (dst -> src)
+};
+
+// K3+K4 / fpm_op_ncc_map: full NCC map of an image against one template level.
+struct NccJob {
+    const uint8_t* img;
+    const uint8_t* tmpl;
+    float* out;              // dense (ow x oh)
+    int32_t iw, ih, ip;
+    int32_t tw, th, tp;
+    int32_t ow, oh;
+    int32_t fold;            // 1: IM_Conv_SIMD per-row float fold; 0: TM_CCORR exact sum -> f32
+    int32_t equal1;          // s_TemplData::vecResultEqual1 -> map of ones
+    double mean, norm, inv_area;
+};
+
+// K5: peak extraction on one top-layer map (plain getNextMaxLoc or s_BlockMax).
+struct NmsJob {
+    float* map;
+    float* bmax;             // s_BlockMax scratch (block mode), nb entries
+    int32_t* bloc;
+    int32_t mw, mh;
+};
+
+struct Peak {
+    int32_t x, y;
+    float score;
+    int32_t pad;
+};
+
+struct NmsArgs {
+    const NmsJob* jobs;
+    Peak* peaks;             // [job][cap]
+    int32_t* counts;         // [job]
+    int32_t tw, th;          // top template size
+    int32_t cap;             // max_pos + MATCH_CANDIDATE_NUM
+    int32_t by_block;
+    double thr;              // vecLayerScore[top]
+    double overlap;
+};
+
+// Angle-tree node: the reference's refinement angle for one path, with glibc trig of angle*D2R.
+struct AngleNode {
+    double angle;
+    double c, s;             // cos, sin of (angle * D2R)
+    double cn, sn;           // cos, sin of -(angle * D2R)
+};
+
+// Top-layer per-angle constants (host-computed, TemplateMatcher.cpp:163-173).
+struct TopAngle {
+    float tx, ty;            // fTranslationX/Y
+    int32_t bw, bh;          // sizeBest
+};
+
+struct CandInitArgs {
+    const Peak* peaks;
+    const int32_t* counts;
+    const TopAngle* angles;  // [nang]
+    const AngleNode* top_nodes;  // [nang] angle, cos/sin of +-angle*D2R
+    CandState* state;        // [cap_total]
+    int32_t* live;           // output live list (layer top-1)
+    int32_t* live_count;
+    int32_t nang, cap;       // per source
+    int32_t total;           // sources * nang * cap
+    F2 center;               // top-layer ptCenter
+    int32_t refine;          // top layer > 0
+};
+
+struct RoiArgs {
+    const uint8_t* level;    // source pyramid level base (source 0); + src * level_stride
+    size_t level_stride;
+    int32_t W, H, P;         // level size and pitch
+    const uint8_t* tmpl;     // template level
+    int32_t tw, th, tp;
+    int32_t n3;              // refinement angles per candidate (1 or 3)
+    int32_t rc;              // template rows per chunk
+    int32_t fold;            // use_simd
+    int32_t equal1;
+    int32_t per_source;      // candidates per source (nang * cap)
+    double mean, norm, inv_area;
+    const int32_t* live;
+    const int32_t* live_count;
+    const CandState* state;
+    const AngleNode* nodes;  // level nodes; child = parent * n3 + j
+    RoiRecord* rec;          // [cand * n3 + j]
+};
+
+struct StepArgs {
+    const int32_t* live_in;
+    const int32_t* live_in_count;
+    int32_t* live_out;
+    int32_t* live_out_count;
+    CandState* state;
+    const RoiRecord* rec;
+    const AngleNode* nodes;
+    int32_t n3;
+    int32_t W, H;            // level size (ptSrcCenter)
+    int32_t mark_reached0;   // next layer is 0
+    double thr;              // vecLayerScore[layer]
+};
+
+// launchers (stream-ordered, no synchronisation)
+void launch_pyr_down(const uint8_t* src, int sw, int sh, int sp, size_t s_img, uint8_t* dst, int dw, int dh,
+                     int dp, size_t d_img, int nimg, hipStream_t st);
+void launch_warp(const WarpJob* jobs, int njobs, int max_pixels, hipStream_t st);
+void launch_ncc_map(const NccJob* jobs, int njobs, int max_out, int tmpl_bytes, hipStream_t st);
+void launch_nms(const NmsArgs& a, int njobs, int max_map, hipStream_t st);
+void launch_cand_init(const CandInitArgs& a, hipStream_t st);
+void launch_roi_corr(const RoiArgs& a, int max_items, hipStream_t st);
+void launch_cand_step(const StepArgs& a, int max_items, hipStream_t st);
+size_t roi_lds_bytes(int tw, int th, int rc);
+int roi_pick_rc(int tw, int th);
+
+}  // namespace fpm

@@ -1,0 +1,254 @@
+"""Python mirror of the reference's ``TemplateMatcher`` (include/TemplateMatcher.h:9-90) over the C ABI.
+
+Same method names, argument meaning and error behaviour as the C++ class: ``learnPattern`` returns False on an
+empty image (TemplateMatcher.cpp:47-49); ``match`` returns an empty list on an empty source, an unlearned
+template or a size mismatch (:99-114); ``getLastExecutionTime`` keeps its previous value when a search finds
+nothing (:398-404).  All pixel work runs in libfpm_hip.so on a gfx950 device.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib as L
+
+
+@dataclass
+class SingleTargetMatch:
+    """s_SingleTargetMatch (DataStructures.h:97-115)."""
+
+    ptLT: Tuple[float, float]
+    ptRT: Tuple[float, float]
+    ptRB: Tuple[float, float]
+    ptLB: Tuple[float, float]
+    ptCenter: Tuple[float, float]
+    dMatchedAngle: float
+    dMatchScore: float
+
+    @staticmethod
+    def from_c(r: "L.Result") -> "SingleTargetMatch":
+        return SingleTargetMatch((r.lt_x, r.lt_y), (r.rt_x, r.rt_y), (r.rb_x, r.rb_y), (r.lb_x, r.lb_y),
+                                 (r.cx, r.cy), r.angle, r.score)
+
+    def getCenterQPoint(self):
+        return self.ptCenter
+
+    def getBoundingRect(self):
+        xs = [self.ptLT[0], self.ptRT[0], self.ptRB[0], self.ptLB[0]]
+        ys = [self.ptLT[1], self.ptRT[1], self.ptRB[1], self.ptLB[1]]
+        return (min(xs), min(ys), max(xs) - min(xs), max(ys) - min(ys))
+
+    def as_tuple(self):
+        return (*self.ptLT, *self.ptRT, *self.ptRB, *self.ptLB, *self.ptCenter, self.dMatchedAngle,
+                self.dMatchScore)
+
+
+def _gray(img) -> np.ndarray:
+    a = np.asarray(img)
+    if a.ndim != 2 or a.dtype != np.uint8:
+        raise TypeError("expected a 2-D uint8 (CV_8UC1) image")
+    return np.ascontiguousarray(a)
+
+
+class TemplateMatcher:
+    """Drop-in for the reference TemplateMatcher, one context (one HIP stream) per instance."""
+
+    def __init__(self, device: int = 0):
+        self._lib = L.load()
+        self._ctx = C.c_void_p()
+        rc = self._lib.fpm_create(device, C.byref(self._ctx))
+        if rc != L.FPM_OK:
+            raise RuntimeError(f"fpm_create(device={device}) failed with {rc}: no gfx950 device / HIP runtime")
+        self._params = L.Params()
+        self._lib.fpm_params_default(C.byref(self._params))
+        self._last_time = 0.0
+        self._user_rect = None
+        self._cap = 4096
+
+    def __del__(self):
+        ctx = getattr(self, "_ctx", None)
+        if ctx is not None and ctx.value:
+            self._lib.fpm_destroy(ctx)
+            self._ctx = None
+
+    # -- error plumbing ---------------------------------------------------------------------------------
+    def last_error(self) -> str:
+        s = self._lib.fpm_last_error(self._ctx)
+        return s.decode() if s else ""
+
+    def _check(self, rc: int, what: str):
+        if rc == L.FPM_E_DEVICE or rc == L.FPM_E_INTERNAL:
+            raise RuntimeError(f"{what}: device error {rc}: {self.last_error()}")
+        return rc
+
+    def _push(self):
+        self._lib.fpm_set_params(self._ctx, C.byref(self._params))
+
+    # -- template -----------------------------------------------------------------------------------------
+    def learnPattern(self, templateImage) -> bool:
+        a = np.asarray(templateImage)
+        if a.size == 0:
+            return False
+        g = _gray(a)
+        self._push()
+        rc = self._check(self._lib.fpm_learn(self._ctx, L.u8ptr(g), g.shape[1], g.shape[0], g.strides[0]),
+                         "learnPattern")
+        return rc == L.FPM_OK
+
+    def isPatternLearned(self) -> bool:
+        return bool(self._lib.fpm_is_learned(self._ctx))
+
+    def clearPattern(self):
+        self._lib.fpm_clear_pattern(self._ctx)
+
+    # -- search ---------------------------------------------------------------------------------------------
+    def match(self, sourceImage) -> List[SingleTargetMatch]:
+        a = np.asarray(sourceImage)
+        if a.size == 0 or not self.isPatternLearned():
+            return []
+        g = _gray(a)
+        self._push()
+        while True:
+            out = (L.Result * self._cap)()
+            n = C.c_int32()
+            sec = C.c_double(self._last_time)
+            rc = self._check(self._lib.fpm_match(self._ctx, L.u8ptr(g), g.shape[1], g.shape[0], g.strides[0], out,
+                                                 self._cap, C.byref(n), C.byref(sec)), "match")
+            if rc == L.FPM_E_CAPACITY:
+                self._cap = max(self._cap * 2, n.value)
+                continue
+            if rc != L.FPM_OK:
+                return []
+            self._last_time = sec.value
+            return [SingleTargetMatch.from_c(out[i]) for i in range(n.value)]
+
+    def match_batch(self, sources: Sequence[np.ndarray]) -> List[List[SingleTargetMatch]]:
+        """Extension: all sources (same size) searched in one device pass (fpm_stage_sources + fpm_match_staged)."""
+        self.stage(sources)
+        return self.match_staged()
+
+    def stage(self, sources: Sequence[np.ndarray]):
+        gs = [_gray(s) for s in sources]
+        h, w = gs[0].shape
+        if any(g.shape != (h, w) for g in gs):
+            raise ValueError("all staged sources must have the same size")
+        self._push()
+        ptrs = (L._U8P * len(gs))(*[L.u8ptr(g) for g in gs])
+        rc = self._check(self._lib.fpm_stage_sources(self._ctx, ptrs, len(gs), w, h, gs[0].strides[0]), "stage")
+        if rc != L.FPM_OK:
+            raise ValueError(f"fpm_stage_sources failed with {rc}: {self.last_error()}")
+        self._staged = len(gs)
+
+    def match_staged(self) -> List[List[SingleTargetMatch]]:
+        n_src = self._staged
+        self._push()
+        while True:
+            out = (L.Result * (self._cap * n_src))()
+            n = (C.c_int32 * n_src)()
+            rc = self._check(self._lib.fpm_match_staged(self._ctx, out, self._cap, n), "match_staged")
+            if rc == L.FPM_E_CAPACITY:
+                self._cap = max(self._cap * 2, max(n))
+                continue
+            if rc != L.FPM_OK:
+                raise RuntimeError(f"fpm_match_staged failed with {rc}: {self.last_error()}")
+            return [[SingleTargetMatch.from_c(out[s * self._cap + i]) for i in range(n[s])] for s in range(n_src)]
+
+    def search_stats(self) -> List[int]:
+        buf = (C.c_int64 * 64)()
+        k = self._lib.fpm_search_stats(self._ctx, buf, 64)
+        return list(buf[:k])
+
+    # -- setters / getters (TemplateMatcher.h:22-37) --------------------------------------------------------
+    def resetParams(self):
+        """Back to the reference constructor defaults (TemplateMatcher.cpp:28-39)."""
+        self._lib.fpm_params_default(C.byref(self._params))
+
+    def setMaxPositions(self, v: int): self._params.max_pos = int(v)
+    def setMaxOverlap(self, v: float): self._params.max_overlap = float(v)
+    def setScore(self, v: float): self._params.score = float(v)
+    def setToleranceAngle(self, v: float): self._params.tolerance_angle = float(v)
+    def setMinReduceArea(self, v: int): self._params.min_reduce_area = int(v)
+    def setUseSIMD(self, v: bool): self._params.use_simd = 1 if v else 0
+    def setSubPixelEstimation(self, v: bool): self._params.subpixel = 1 if v else 0
+    def getMaxPositions(self) -> int: return self._params.max_pos
+    def getMaxOverlap(self) -> float: return self._params.max_overlap
+    def getScore(self) -> float: return self._params.score
+    def getToleranceAngle(self) -> float: return self._params.tolerance_angle
+    def getMinReduceArea(self) -> int: return self._params.min_reduce_area
+    def getUseSIMD(self) -> bool: return bool(self._params.use_simd)
+    def getSubPixelEstimation(self) -> bool: return bool(self._params.subpixel)
+    def getLastExecutionTime(self) -> float: return self._last_time
+
+    # -- user rectangle: stored only, unused by matching (TemplateMatcher.cpp:1224-1238) ---------------------
+    def setUserDefinedRect(self, rect): self._user_rect = tuple(rect)
+    def getUserDefinedRect(self): return self._user_rect if self._user_rect is not None else (0, 0, 0, 0)
+    def hasUserDefinedRect(self) -> bool: return self._user_rect is not None
+
+    # -- pixel operators (fpm_op_*) ---------------------------------------------------------------------------
+    def pyr_down(self, img) -> np.ndarray:
+        g = _gray(img)
+        h, w = g.shape
+        out = np.zeros(((h + 1) // 2, (w + 1) // 2), np.uint8)
+        rc = self._check(self._lib.fpm_op_pyr_down(self._ctx, L.u8ptr(g), w, h, g.strides[0], L.u8ptr(out),
+                                                   out.strides[0]), "pyr_down")
+        if rc != L.FPM_OK:
+            raise ValueError(self.last_error())
+        return out
+
+    def warp_affine(self, img, m, dsize, border: int = 0) -> np.ndarray:
+        g = _gray(img)
+        h, w = g.shape
+        dw, dh = dsize
+        out = np.zeros((dh, dw), np.uint8)
+        mm = (C.c_double * 6)(*np.asarray(m, np.float64).ravel().tolist())
+        rc = self._check(self._lib.fpm_op_warp_affine(self._ctx, L.u8ptr(g), w, h, g.strides[0], mm, L.u8ptr(out),
+                                                      dw, dh, out.strides[0], int(border)), "warp_affine")
+        if rc != L.FPM_OK:
+            raise ValueError(self.last_error())
+        return out
+
+    def ncc_map(self, img, layer: int, fold: bool) -> np.ndarray:
+        g = _gray(img)
+        h, w = g.shape
+        tw, th = self.template_level(layer)[0].shape[::-1]
+        out = np.zeros((h - th + 1, w - tw + 1), np.float32)
+        rc = self._check(self._lib.fpm_op_ncc_map(self._ctx, L.u8ptr(g), w, h, g.strides[0], int(layer),
+                                                  1 if fold else 0,
+                                                  out.ctypes.data_as(C.POINTER(C.c_float))), "ncc_map")
+        if rc != L.FPM_OK:
+            raise ValueError(self.last_error())
+        return out
+
+    def template_info(self):
+        lv, border = C.c_int32(), C.c_int32()
+        rc = self._lib.fpm_template_info(self._ctx, C.byref(lv), C.byref(border))
+        if rc != L.FPM_OK:
+            raise ValueError("template not learned")
+        return lv.value, border.value
+
+    def template_level(self, level: int):
+        w, h, eq = C.c_int32(), C.c_int32(), C.c_int32()
+        mean, norm, inv = C.c_double(), C.c_double(), C.c_double()
+        rc = self._lib.fpm_template_level(self._ctx, level, C.byref(w), C.byref(h), C.byref(mean), C.byref(norm),
+                                          C.byref(inv), C.byref(eq), None, 0)
+        if rc != L.FPM_OK:
+            raise ValueError("bad level")
+        px = np.zeros((h.value, w.value), np.uint8)
+        self._lib.fpm_template_level(self._ctx, level, C.byref(w), C.byref(h), C.byref(mean), C.byref(norm),
+                                     C.byref(inv), C.byref(eq), L.u8ptr(px), px.strides[0])
+        return px, mean.value, norm.value, inv.value, bool(eq.value)
+
+    # -- kernel timing ------------------------------------------------------------------------------------------
+    def profile(self, enable: bool):
+        self._lib.fpm_profile_enable(self._ctx, 1 if enable else 0)
+
+    def profile_reset(self):
+        self._lib.fpm_profile_reset(self._ctx)
+
+    def profile_get(self, kernel: int):
+        ms, n, b = C.c_double(), C.c_int64(), C.c_int64()
+        self._lib.fpm_profile_get(self._ctx, kernel, C.byref(ms), C.byref(n), C.byref(b))
+        return ms.value, n.value, b.value

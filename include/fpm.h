@@ -1,0 +1,151 @@
+/*
+ * fpm.h — C ABI of the MI355X-native NCC template matcher (libfpm_hip.so).
+ *
+ * Drop-in boundary for the reference's `TemplateMatcher` (lrm2017/Fastest_Image_Pattern_Matching,
+ * include/TemplateMatcher.h:9-90, src/TemplateMatcher.cpp:1-1239).  Every entry point below names the
+ * reference interface it replaces.  Plain pointers and sizes only: no torch / OpenCV / Qt types.
+ *
+ * Conventions
+ *   - Images are 8-bit single-channel (CV_8UC1) row-major with an explicit row stride in bytes, exactly
+ *     what `cv::imread(..., IMREAD_GRAYSCALE)` yields (src/MatchToolDialog.cpp:314, 341).
+ *   - Host image pointers are copied to device memory inside the call; the library never retains them.
+ *   - Every function returns an `int` status: FPM_OK (0) or a negative FPM_E_* code.  "No match" is
+ *     FPM_OK with *n_results == 0, mirroring the reference's empty vector (TemplateMatcher.cpp:99-114, 398).
+ *   - One context per host thread; a context is bound to one HIP device and owns one HIP stream.
+ *   - fpm_last_error() returns a human-readable message for the last failing call on a context.
+ */
+#ifndef FPM_H_
+#define FPM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FPM_ABI_VERSION 1
+
+/* status codes */
+#define FPM_OK 0
+#define FPM_E_INVALID_ARG (-1)   /* null pointer, non-positive size, bad stride            */
+#define FPM_E_NOT_LEARNED (-2)   /* match() before learnPattern() (TemplateMatcher.cpp:99)   */
+#define FPM_E_SIZE (-3)          /* source smaller than template (TemplateMatcher.cpp:107-114)*/
+#define FPM_E_DEVICE (-4)        /* HIP runtime error / no gfx950 device                     */
+#define FPM_E_CAPACITY (-5)      /* caller-provided result buffer too small                 */
+#define FPM_E_INTERNAL (-6)
+
+/* Search parameters: the 7 public setters of TemplateMatcher (TemplateMatcher.h:22-28) plus the hidden
+ * fixed members m_bToleranceRange / m_dTolerance1..4 (TemplateMatcher.h:88-89, TemplateMatcher.cpp:38).
+ * Defaults (fpm_params_default) equal the reference constructor (TemplateMatcher.cpp:28-39). */
+typedef struct fpm_params {
+    int32_t max_pos;          /* setMaxPositions      (default 70)   */
+    int32_t min_reduce_area;  /* setMinReduceArea     (default 256)  */
+    double max_overlap;       /* setMaxOverlap        (default 0.0)  */
+    double score;             /* setScore             (default 0.7)  */
+    double tolerance_angle;   /* setToleranceAngle    (default 0.0)  */
+    int32_t use_simd;         /* setUseSIMD           (default 1): lower layers use the per-row int32 ->
+                                 float fold of IM_Conv_SIMD (TemplateMatcher.cpp:487-512); 0 = TM_CCORR */
+    int32_t subpixel;         /* setSubPixelEstimation(default 0)    */
+    int32_t tolerance_range;  /* m_bToleranceRange    (fixed false in the reference)          */
+    int32_t reserved0;
+    double tolerance[4];      /* m_dTolerance1..4     (unused by the reference search)         */
+} fpm_params;
+
+/* One result; POD-identical to s_SingleTargetMatch (DataStructures.h:97-115): five cv::Point2d then two
+ * doubles, 12 f64 in total, same order. */
+typedef struct fpm_result {
+    double lt_x, lt_y;        /* ptLT     */
+    double rt_x, rt_y;        /* ptRT     */
+    double rb_x, rb_y;        /* ptRB     */
+    double lb_x, lb_y;        /* ptLB     */
+    double cx, cy;            /* ptCenter */
+    double angle;             /* dMatchedAngle (Qt sign convention, TemplateMatcher.cpp:428) */
+    double score;             /* dMatchScore */
+} fpm_result;
+
+typedef struct fpm_ctx fpm_ctx;
+
+/* --- lifecycle -------------------------------------------------------------------------------------- */
+void fpm_params_default(fpm_params* p);                 /* TemplateMatcher::TemplateMatcher (:28-39) */
+int fpm_create(int device, fpm_ctx** out);               /* TemplateMatcher::TemplateMatcher          */
+int fpm_destroy(fpm_ctx* ctx);                           /* TemplateMatcher::~TemplateMatcher (:41)   */
+const char* fpm_last_error(const fpm_ctx* ctx);
+int fpm_abi_version(void);
+
+/* --- parameters ------------------------------------------------------------------------------------- */
+int fpm_set_params(fpm_ctx* ctx, const fpm_params* p);   /* the 7 setters (TemplateMatcher.h:22-28)   */
+int fpm_get_params(const fpm_ctx* ctx, fpm_params* p);   /* the 7 getters (TemplateMatcher.h:31-37)   */
+
+/* --- template ----------------------------------------------------------------------------------------*/
+/* TemplateMatcher::learnPattern (TemplateMatcher.cpp:45-95).  Returns FPM_E_INVALID_ARG on an empty image
+ * (the reference returns false, :47-49). */
+int fpm_learn(fpm_ctx* ctx, const uint8_t* gray, int32_t width, int32_t height, size_t stride);
+int fpm_clear_pattern(fpm_ctx* ctx);                     /* clearPattern (:439-443)                   */
+int fpm_is_learned(const fpm_ctx* ctx);                  /* isPatternLearned (TemplateMatcher.h:43)   */
+
+/* --- search ------------------------------------------------------------------------------------------*/
+/* TemplateMatcher::match (TemplateMatcher.cpp:97-437).  Writes at most `cap` results (sorted by
+ * descending score, exactly the reference's vector order) and the count to *n_results.
+ * *seconds receives getLastExecutionTime() semantics: the pyramid->filter wall time; left unchanged when
+ * there is no result (the reference returns before updating it, :398-404).  seconds may be NULL. */
+int fpm_match(fpm_ctx* ctx, const uint8_t* gray, int32_t width, int32_t height, size_t stride,
+              fpm_result* out, int32_t cap, int32_t* n_results, double* seconds);
+
+/* Batched / device-resident search (no reference equivalent: the UI calls match() once per image).
+ * Sources are staged into context-owned HBM once (fpm_stage_sources), then fpm_match_staged runs the
+ * whole search for all staged sources layer-synchronously with one device->host copy at the end.
+ * out is [count][cap_per_source]; n_results is [count]. */
+int fpm_stage_sources(fpm_ctx* ctx, const uint8_t* const* grays, int32_t count, int32_t width,
+                      int32_t height, size_t stride);
+int fpm_match_staged(fpm_ctx* ctx, fpm_result* out, int32_t cap_per_source, int32_t* n_results);
+
+/* --- pixel operators (L1 kernels exposed for parity tests and standalone use) ----------------------- */
+/* cv::pyrDown (8U, 5x5 Gaussian, reflect-101), as called by cv::buildPyramid (TemplateMatcher.cpp:55,124).
+ * dst is ((w+1)/2) x ((h+1)/2) with row stride dst_stride. */
+int fpm_op_pyr_down(fpm_ctx* ctx, const uint8_t* src, int32_t w, int32_t h, size_t src_stride,
+                    uint8_t* dst, size_t dst_stride);
+/* cv::warpAffine(INTER_LINEAR, BORDER_CONSTANT=border) with forward 2x3 matrix m (row-major), as called at
+ * TemplateMatcher.cpp:175 (top layer) and :1089 (getRotatedROI, border 0). */
+int fpm_op_warp_affine(fpm_ctx* ctx, const uint8_t* src, int32_t w, int32_t h, size_t src_stride,
+                       const double m[6], uint8_t* dst, int32_t dw, int32_t dh, size_t dst_stride,
+                       int32_t border);
+/* TemplateMatcher::MatchTemplate + CCOEFF_Denominator (TemplateMatcher.cpp:485-598) of `src` against
+ * pyramid level `layer` of the learned template.  fold=1 selects the IM_Conv_SIMD per-row float fold
+ * (:496-510), fold=0 the TM_CCORR path (:514).  out is (w-tw+1) x (h-th+1) f32, dense. */
+int fpm_op_ncc_map(fpm_ctx* ctx, const uint8_t* src, int32_t w, int32_t h, size_t src_stride,
+                   int32_t layer, int32_t fold, float* out);
+/* Learned-template introspection: number of pyramid levels, per-level size and statistics
+ * (s_TemplData, DataStructures.h:16-55). */
+int fpm_template_info(const fpm_ctx* ctx, int32_t* levels, int32_t* border_color);
+int fpm_template_level(const fpm_ctx* ctx, int32_t level, int32_t* w, int32_t* h, double* mean,
+                       double* norm, double* inv_area, int32_t* result_equal1, uint8_t* pixels,
+                       size_t stride);
+
+/* --- instrumentation -------------------------------------------------------------------------------- */
+/* Per-search counters of the last fpm_match / fpm_match_staged call (source 0 for staged batches):
+ *   [0] top-layer angles  [1] top-layer candidates  [2..2+L) live candidates entering layer L-1..0
+ * Returns the number of entries written. */
+int fpm_search_stats(const fpm_ctx* ctx, int64_t* stats, int32_t cap);
+
+/* Kernel timing: when enabled, HIP events bracket every launch of each kernel family on the context's
+ * stream; fpm_profile_get returns total milliseconds, launch count and algorithmic bytes moved (inputs +
+ * outputs, u8 = 1 B, f32 = 4 B) accumulated since the last reset. */
+#define FPM_K_PYR 0        /* K1 pyrDown                                */
+#define FPM_K_TOP_WARP 1   /* K2 top-layer rotation                     */
+#define FPM_K_TOP_NCC 2    /* K3+K4 top-layer CCORR + normalisation     */
+#define FPM_K_TOP_NMS 3    /* K5 peak extraction                        */
+#define FPM_K_ROI_WARP 4   /* K6 refinement ROI rotation                */
+#define FPM_K_ROI_CORR 5   /* K7 refinement ROI correlation             */
+#define FPM_K_ROI_EVAL 6   /* K8 fold + normalise + argmax + decision   */
+#define FPM_K_COUNT 7
+int fpm_profile_enable(fpm_ctx* ctx, int32_t enable);
+int fpm_profile_reset(fpm_ctx* ctx);
+int fpm_profile_get(const fpm_ctx* ctx, int32_t kernel, double* total_ms, int64_t* launches,
+                    int64_t* bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FPM_H_ */

@@ -1,0 +1,170 @@
+"""ctypes binding of the CPU parity oracle (oracle/build/liboracle_fpm.so) — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this module, and only as the checker
+(or the timed CPU baseline); the product path (fastest_image_pattern_matching_amd) never imports it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from fastest_image_pattern_matching_amd._lib import Params, Result
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(REPO, "oracle")
+ORACLE_LIB = os.path.join(ORACLE_DIR, "build", "liboracle_fpm.so")
+_U8P = C.POINTER(C.c_uint8)
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(ORACLE_LIB):
+        subprocess.check_call(["make", "-C", ORACLE_DIR])
+    lib = C.CDLL(ORACLE_LIB)
+    lib.orc_create.restype = C.c_void_p
+    lib.orc_destroy.argtypes = [C.c_void_p]
+    lib.orc_set_params.argtypes = [C.c_void_p, C.POINTER(Params)]
+    lib.orc_get_params.argtypes = [C.c_void_p, C.POINTER(Params)]
+    lib.orc_learn.argtypes = [C.c_void_p, _U8P, C.c_int, C.c_int, C.c_size_t]
+    lib.orc_match.argtypes = [C.c_void_p, _U8P, C.c_int, C.c_int, C.c_size_t, C.POINTER(Result), C.c_int,
+                              C.POINTER(C.c_int), C.POINTER(C.c_double)]
+    lib.orc_search_stats.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.c_int]
+    lib.orc_top_candidates.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_int]
+    lib.orc_template_info.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    lib.orc_template_level.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                       C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                       C.POINTER(C.c_int), _U8P, C.c_size_t]
+    lib.orc_pyr_down.argtypes = [_U8P, C.c_int, C.c_int, C.c_size_t, _U8P, C.c_size_t]
+    lib.orc_warp_affine.argtypes = [_U8P, C.c_int, C.c_int, C.c_size_t, C.POINTER(C.c_double), _U8P, C.c_int,
+                                    C.c_int, C.c_size_t, C.c_int]
+    lib.orc_rotation_matrix.argtypes = [C.c_float, C.c_float, C.c_double, C.POINTER(C.c_double)]
+    lib.orc_ncc_map.argtypes = [C.c_void_p, _U8P, C.c_int, C.c_int, C.c_size_t, C.c_int, C.c_int,
+                                C.POINTER(C.c_float)]
+    lib.orc_rotrect_overlap.argtypes = [C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_double),
+                                        C.POINTER(C.c_int)]
+    lib.fpm_params_default.argtypes = [C.POINTER(Params)]
+    _lib = lib
+    return lib
+
+
+def _u8(a):
+    return a.ctypes.data_as(_U8P)
+
+
+def pyr_down(img: np.ndarray) -> np.ndarray:
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    out = np.zeros(((h + 1) // 2, (w + 1) // 2), np.uint8)
+    load().orc_pyr_down(_u8(img), w, h, img.strides[0], _u8(out), out.strides[0])
+    return out
+
+
+def warp_affine(img: np.ndarray, m, dsize, border: int = 0) -> np.ndarray:
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    dw, dh = dsize
+    out = np.zeros((dh, dw), np.uint8)
+    mm = (C.c_double * 6)(*np.asarray(m, np.float64).ravel().tolist())
+    load().orc_warp_affine(_u8(img), w, h, img.strides[0], mm, _u8(out), dw, dh, out.strides[0], int(border))
+    return out
+
+
+def rotation_matrix(cx: float, cy: float, angle: float) -> np.ndarray:
+    m = (C.c_double * 6)()
+    load().orc_rotation_matrix(cx, cy, angle, m)
+    return np.array(m[:], np.float64).reshape(2, 3)
+
+
+def rotrect_overlap(a, b):
+    """(type, area, npts) of two rotated rects given as (ptLT, ptRT, ptRB)."""
+    fa = (C.c_float * 6)(*[float(v) for v in np.ravel(a)])
+    fb = (C.c_float * 6)(*[float(v) for v in np.ravel(b)])
+    area, n = C.c_double(), C.c_int()
+    t = load().orc_rotrect_overlap(fa, fb, C.byref(area), C.byref(n))
+    return t, area.value, n.value
+
+
+class OracleMatcher:
+    """Same surface as fastest_image_pattern_matching_amd.TemplateMatcher (setters, learnPattern, match)."""
+
+    def __init__(self):
+        self._lib = load()
+        self._h = C.c_void_p(self._lib.orc_create())
+        self._p = Params()
+        self._lib.fpm_params_default(C.byref(self._p))
+        self.last_time = 0.0
+
+    def __del__(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.orc_destroy(self._h)
+            self._h = None
+
+    @property
+    def params(self) -> Params:
+        return self._p
+
+    def set(self, **kw):
+        for k, v in kw.items():
+            setattr(self._p, k, v)
+        return self
+
+    def learnPattern(self, t: np.ndarray) -> bool:
+        t = np.ascontiguousarray(t, np.uint8)
+        self._lib.orc_set_params(self._h, C.byref(self._p))
+        return self._lib.orc_learn(self._h, _u8(t), t.shape[1], t.shape[0], t.strides[0]) == 0
+
+    def match_raw(self, s: np.ndarray):
+        s = np.ascontiguousarray(s, np.uint8)
+        self._lib.orc_set_params(self._h, C.byref(self._p))
+        cap = 4096
+        out = (Result * cap)()
+        n = C.c_int()
+        sec = C.c_double(self.last_time)
+        rc = self._lib.orc_match(self._h, _u8(s), s.shape[1], s.shape[0], s.strides[0], out, cap, C.byref(n),
+                                 C.byref(sec))
+        self.last_time = sec.value
+        return rc, [tuple(getattr(out[i], f) for f, _ in Result._fields_) for i in range(min(n.value, cap))]
+
+    def match(self, s: np.ndarray):
+        return self.match_raw(s)[1]
+
+    def stats(self):
+        buf = (C.c_int64 * 64)()
+        k = self._lib.orc_search_stats(self._h, buf, 64)
+        return list(buf[:k])
+
+    def top_candidates(self):
+        n = self._lib.orc_top_candidates(self._h, None, 0)
+        buf = (C.c_double * (4 * max(n, 1)))()
+        self._lib.orc_top_candidates(self._h, buf, n)
+        return np.array(buf[:4 * n], np.float64).reshape(n, 4)
+
+    def template_levels(self):
+        lv, border = C.c_int(), C.c_int()
+        self._lib.orc_template_info(self._h, C.byref(lv), C.byref(border))
+        out = []
+        for i in range(lv.value):
+            w, h, eq = C.c_int(), C.c_int(), C.c_int()
+            mean, norm, inv = C.c_double(), C.c_double(), C.c_double()
+            self._lib.orc_template_level(self._h, i, C.byref(w), C.byref(h), C.byref(mean), C.byref(norm),
+                                         C.byref(inv), C.byref(eq), None, 0)
+            px = np.zeros((h.value, w.value), np.uint8)
+            self._lib.orc_template_level(self._h, i, C.byref(w), C.byref(h), C.byref(mean), C.byref(norm),
+                                         C.byref(inv), C.byref(eq), _u8(px), px.strides[0])
+            out.append((px, mean.value, norm.value, inv.value, bool(eq.value)))
+        return out, border.value
+
+    def ncc_map(self, img: np.ndarray, layer: int, fold: bool) -> np.ndarray:
+        img = np.ascontiguousarray(img, np.uint8)
+        levels, _ = self.template_levels()
+        th, tw = levels[layer][0].shape
+        out = np.zeros((img.shape[0] - th + 1, img.shape[1] - tw + 1), np.float32)
+        self._lib.orc_ncc_map(self._h, _u8(img), img.shape[1], img.shape[0], img.strides[0], layer,
+                              1 if fold else 0, out.ctypes.data_as(C.POINTER(C.c_float)))
+        return out

@@ -1,0 +1,59 @@
+"""The C-ABI library builds, loads and exports every entry point include/fpm.h declares (no GPU needed)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from fastest_image_pattern_matching_amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    src = open(os.path.join(REPO, "include", "fpm.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(fpm_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_the_boundary():
+    syms = declared_symbols()
+    for must in ("fpm_create", "fpm_destroy", "fpm_set_params", "fpm_learn", "fpm_match", "fpm_last_error"):
+        assert must in syms
+
+
+def test_library_exports_every_declared_symbol(fpm_lib):
+    missing = [s for s in declared_symbols() if not hasattr(fpm_lib, s)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_header(fpm_lib):
+    assert set(declared_symbols()) == set(_lib.SIGNATURES)
+
+
+def test_result_struct_is_s_single_target_match_layout():
+    # five cv::Point2d + dMatchedAngle + dMatchScore = 12 doubles (DataStructures.h:97-115)
+    assert C.sizeof(_lib.Result) == 12 * 8
+
+
+def test_defaults_equal_reference_constructor(fpm_lib):
+    p = _lib.Params()
+    fpm_lib.fpm_params_default(C.byref(p))
+    assert (p.max_pos, p.max_overlap, p.score, p.tolerance_angle, p.min_reduce_area, p.use_simd, p.subpixel) == \
+        (70, 0.0, 0.7, 0.0, 256, 1, 0)
+
+
+def test_abi_version(fpm_lib):
+    assert fpm_lib.fpm_abi_version() == 1
+
+
+def test_null_arguments_are_rejected_without_a_device(fpm_lib):
+    assert fpm_lib.fpm_create(0, None) == _lib.FPM_E_INVALID_ARG
+    assert fpm_lib.fpm_destroy(None) == _lib.FPM_E_INVALID_ARG
+    assert fpm_lib.fpm_set_params(None, None) == _lib.FPM_E_INVALID_ARG
+
+
+def test_library_is_gfx950_code_object():
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+    assert b"gfx942" not in blob and b"gfx90a" not in blob

@@ -1,0 +1,213 @@
+"""HIP path vs the CPU oracle on the same seeded inputs, through the C ABI (gfx950 required).
+
+Bar: bit-exact pixels / maps / positions / angles; scores within 1e-5 (BASELINE.json north_star) — the design
+makes them bit-identical, and the tests assert the exact equality they claim.
+"""
+import numpy as np
+import pytest
+
+from fastest_image_pattern_matching_amd import synth
+from tests import oracle
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("lt_x", "lt_y", "rt_x", "rt_y", "rb_x", "rb_y", "lb_x", "lb_y", "cx", "cy", "angle", "score")
+
+
+@pytest.fixture(scope="module")
+def hip(gpu_matcher_factory):
+    return gpu_matcher_factory()
+
+
+def assert_same_results(gpu, orc, label=""):
+    g = [r.as_tuple() for r in gpu]
+    assert len(g) == len(orc), f"{label}: {len(g)} GPU results vs {len(orc)} oracle results\n{g}\n{orc}"
+    for i, (a, b) in enumerate(zip(g, orc)):
+        for f, x, y in zip(FIELDS, a, b):
+            if f == "score":
+                assert abs(x - y) <= 1e-5, (label, i, f, x, y)
+            assert x == y, f"{label}: result {i} field {f}: gpu {x!r} oracle {y!r}"
+
+
+# ---------------------------------------------------------------------------------------------------- K1
+@pytest.mark.parametrize("shape", [(2, 2), (3, 5), (7, 130), (68, 136), (69, 137), (100, 333), (521, 762),
+                                   (1518, 2012), (3036, 4024)])
+def test_pyr_down(hip, shape):
+    rng = np.random.default_rng(shape[0] * 7 + shape[1])
+    img = rng.integers(0, 256, shape, dtype=np.uint8)
+    assert np.array_equal(hip.pyr_down(img), oracle.pyr_down(img))
+
+
+def test_pyr_down_strided_input(hip):
+    img = np.random.default_rng(9).integers(0, 256, (300, 500), dtype=np.uint8)[10:250, 3:411]
+    assert np.array_equal(hip.pyr_down(img), oracle.pyr_down(np.ascontiguousarray(img)))
+
+
+# ---------------------------------------------------------------------------------------------------- K2
+@pytest.mark.parametrize("seed", range(8))
+def test_warp_affine(hip, seed):
+    rng = np.random.default_rng(100 + seed)
+    h, w = int(rng.integers(5, 200)), int(rng.integers(5, 200))
+    img = rng.integers(0, 256, (h, w), dtype=np.uint8)
+    ang = float(rng.uniform(-200, 200))
+    m = oracle.rotation_matrix(float(rng.uniform(0, w)), float(rng.uniform(0, h)), ang)
+    m[:, 2] += rng.uniform(-20, 20, 2)
+    dw, dh = int(rng.integers(1, 260)), int(rng.integers(1, 260))
+    border = int(rng.integers(0, 256))
+    assert np.array_equal(hip.warp_affine(img, m, (dw, dh), border), oracle.warp_affine(img, m, (dw, dh), border))
+
+
+# ---------------------------------------------------------------------------------------------------- learn
+@pytest.mark.parametrize("name,mra", [("Dst1", 256), ("Dst7", 256), ("Dst10", 256), ("Dst4", 64), ("Dst6", 1024)])
+def test_learn_pattern(hip, templates, name, mra):
+    t = templates[name]
+    hip.setMinReduceArea(mra)
+    assert hip.learnPattern(t)
+    o = oracle.OracleMatcher().set(min_reduce_area=mra)
+    o.learnPattern(t)
+    levels, border = o.template_levels()
+    assert hip.template_info() == (len(levels), border)
+    for i, (px, mean, norm, inv, eq) in enumerate(levels):
+        gp, gm, gn, gi, ge = hip.template_level(i)
+        assert np.array_equal(gp, px) and (gm, gn, gi, ge) == (mean, norm, inv, eq)
+    hip.setMinReduceArea(256)
+
+
+# ---------------------------------------------------------------------------------------------------- K3+K4
+@pytest.mark.parametrize("fold", [False, True])
+def test_ncc_map_all_layers(hip, templates, fold):
+    t = templates["Dst1"]
+    hip.setMinReduceArea(256)
+    hip.learnPattern(t)
+    o = oracle.OracleMatcher()
+    o.learnPattern(t)
+    rng = np.random.default_rng(42)
+    levels, _ = o.template_levels()
+    for layer, (px, *_rest) in enumerate(levels):
+        th, tw = px.shape
+        img = rng.integers(0, 256, (th + 13, tw + 9), dtype=np.uint8)
+        img[5:5 + th, 3:3 + tw] = px
+        assert np.array_equal(hip.ncc_map(img, layer, fold), o.ncc_map(img, layer, fold)), layer
+
+
+# ---------------------------------------------------------------------------------------------------- search
+def _scene_rotated(templates, name, poses, size, seed, bg=(128, 10)):
+    t = templates[name]
+    s = synth.noise(size[0], size[1], bg[0], bg[1], seed)
+    for cx, cy, ang in poses:
+        synth.paste_rotated(s, t, cx, cy, ang)
+    return s, t
+
+
+def _run_both(hip, s, t, **prm):
+    o = oracle.OracleMatcher()
+    hip.resetParams()
+    for k, v in prm.items():
+        setattr(o.params, k, v)
+        setattr(hip._params, k, v)
+    assert o.learnPattern(t) and hip.learnPattern(t)
+    orc = o.match(s)
+    gpu = hip.match(s)
+    return gpu, orc, o.stats(), hip.search_stats()
+
+
+CASES = {
+    "plumbing_tol0": (lambda T: synth.plumbing_scene(T["Dst1"]), dict(max_pos=1)),
+    "dst1_rot30": (lambda T: _scene_rotated(T, "Dst1", [(640, 512, 30.0)], (1280, 1024), 1),
+                   dict(max_pos=1, tolerance_angle=180.0)),
+    "dst10_multi": (lambda T: _scene_rotated(T, "Dst10", [(100, 90, 37.0), (300, 250, -100.0), (420, 120, 170.0)],
+                                             (560, 400), 2), dict(max_pos=5, tolerance_angle=180.0)),
+    "dst10_nosimd": (lambda T: _scene_rotated(T, "Dst10", [(100, 90, 37.0), (300, 250, -100.0)], (560, 400), 3),
+                     dict(max_pos=5, tolerance_angle=180.0, use_simd=0)),
+    "dst5_subpixel": (lambda T: _scene_rotated(T, "Dst5", [(200, 180, 44.3)], (420, 380), 4, (60, 10)),
+                      dict(max_pos=1, tolerance_angle=180.0, subpixel=1)),
+    "dst4_block": (lambda T: _grid_scene(T["Dst4"], 900, 900, 60, 5), dict(max_pos=40, tolerance_angle=0.0)),
+    "dst4_overlap": (lambda T: _grid_scene(T["Dst4"], 400, 300, 20, 6),
+                     dict(max_pos=30, tolerance_angle=10.0, max_overlap=0.5, score=0.6)),
+    "dst3_range": (lambda T: _scene_rotated(T, "Dst3", [(150, 150, 12.0), (400, 260, -33.0)], (560, 420), 7),
+                   dict(max_pos=4, tolerance_angle=40.0, tolerance_range=1)),
+    "top_is_layer0": (lambda T: _scene_rotated(T, "Dst4", [(60, 50, 0.0), (150, 80, 0.0)], (220, 160), 8),
+                      dict(max_pos=3, min_reduce_area=1024)),
+    "score_low_many": (lambda T: _scene_rotated(T, "Dst9", [(200, 200, 5.0), (500, 300, 95.0)], (700, 520), 9),
+                       dict(max_pos=10, tolerance_angle=180.0, score=0.5)),
+}
+
+
+def _grid_scene(t, w, h, pitch, seed):
+    s = synth.box_blur(synth.noise(w, h, 128, 25, seed), 3)
+    th, tw = t.shape
+    for y in range(10, h - th - 10, pitch):
+        for x in range(10, w - tw - 10, pitch + 7):
+            synth.paste(s, t, x, y)
+    return s, t
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_match_parity(hip, templates, case):
+    make, prm = CASES[case]
+    s, t = make(templates)
+    gpu, orc, ostats, gstats = _run_both(hip, s, t, **prm)
+    assert gstats == ostats, (gstats, ostats)
+    assert_same_results(gpu, orc, case)
+    assert len(orc) >= 1
+
+
+def test_src7_full_search(hip, templates):
+    """BASELINE configs[1] at full size: 4024x3036 / 762x521, +-180 deg, TargetNum 3."""
+    s, t = synth.src7_scene(templates["Dst7"])
+    gpu, orc, ostats, gstats = _run_both(hip, s, t, max_pos=3, tolerance_angle=180.0, score=0.7)
+    assert gstats == ostats
+    assert_same_results(gpu, orc, "src7")
+    assert len(gpu) == 3
+
+
+def test_constant_template(hip):
+    t = np.full((40, 40), 90, np.uint8)
+    s = synth.noise(200, 150, 90, 20, 12)
+    gpu, orc, ostats, gstats = _run_both(hip, s, t, max_pos=2)
+    assert gstats == ostats
+    assert_same_results(gpu, orc, "equal1")
+
+
+def test_batch_equals_single(hip, templates):
+    t = templates["Dst10"]
+    srcs = []
+    for k in range(5):
+        s = synth.noise(360, 300, 128, 10, 50 + k)
+        synth.paste_rotated(s, t, 100 + 30 * k, 120 + 10 * k, 20.0 * k - 50)
+        srcs.append(s)
+    o = oracle.OracleMatcher().set(max_pos=2, tolerance_angle=180.0)
+    o.learnPattern(t)
+    hip.resetParams()
+    hip.setMaxPositions(2)
+    hip.setToleranceAngle(180.0)
+    hip.learnPattern(t)
+    batch = hip.match_batch(srcs)
+    for k, s in enumerate(srcs):
+        assert_same_results(batch[k], o.match(s), f"batch{k}")
+
+
+def test_error_behaviour(hip, templates):
+    hip.clearPattern()
+    assert hip.match(np.zeros((50, 50), np.uint8)) == []        # not learned (TemplateMatcher.cpp:99)
+    assert hip.learnPattern(np.zeros((0, 0), np.uint8)) is False
+    hip.learnPattern(templates["Dst10"])
+    assert hip.match(np.zeros((20, 200), np.uint8)) == []       # orientation mismatch (:107-110)
+    assert hip.match(np.zeros((0, 0), np.uint8)) == []
+    prev = hip.getLastExecutionTime()
+    assert hip.match(np.full((80, 80), 7, np.uint8)) == []       # nothing found: time unchanged (:398-404)
+    assert hip.getLastExecutionTime() == prev
+
+
+def test_src6_real_image(hip, templates):
+    """README Test6 (README.md:70; Result Images/Result6.jpg): Src6/Dst6, TargetNum 15, Score 0.8, Tol 180,
+    MRA 256 -> 15 pocket detections, identical to the oracle."""
+    import os
+
+    from fastest_image_pattern_matching_amd.images import imread_gray
+
+    src = imread_gray(os.path.join(os.path.dirname(__file__), "golden", "Src6.jpg"))
+    gpu, orc, ostats, gstats = _run_both(hip, src, templates["Dst6"], max_pos=15, score=0.8, tolerance_angle=180.0)
+    assert gstats == ostats
+    assert_same_results(gpu, orc, "src6")
+    assert len(gpu) == 15
