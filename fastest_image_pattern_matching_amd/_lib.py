@@ -22,8 +22,8 @@ FPM_E_DEVICE = -4
 FPM_E_CAPACITY = -5
 FPM_E_INTERNAL = -6
 
-K_PYR, K_TOP_WARP, K_TOP_NCC, K_TOP_NMS, K_ROI_WARP, K_ROI_CORR, K_ROI_EVAL = range(7)
-KERNEL_NAMES = ["pyr_down", "top_warp", "top_ncc", "top_nms", "roi_warp", "roi_corr", "cand_step"]
+K_PYR, K_TOP_WARP, K_TOP_NCC, K_TOP_NMS, K_ROI_WARP, K_ROI_CORR, K_ROI_EVAL, K_CAND = range(8)
+KERNEL_NAMES = ["pyr_down", "top_warp", "top_ncc", "top_nms", "roi_warp", "roi_corr", "roi_eval", "cand"]
 
 
 class Params(C.Structure):

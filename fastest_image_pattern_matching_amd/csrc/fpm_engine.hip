@@ -96,13 +96,16 @@ struct Plan {
     int max_canvas = 0, max_map = 0;
     // device buffers owned by the plan
     DevBuf d_canvas, d_map, d_bmax, d_bloc, d_jobs, d_nodes, d_top, d_topn, d_peaks, d_counts, d_state,
-        d_live, d_livecnt, d_rec;
+        d_live, d_livecnt, d_rec, d_rowsum, d_wsum, d_wsq, d_tab, d_roi;
+    int tabw = 0, tabh = 0, roi_pitch = 0;
+    size_t roi_stride = 0;
+    int slot_cap = 0;                          // ROIs per refinement round (bounded scratch)
     size_t off_warp = 0, off_ncc = 0, off_nms = 0;
     PinBuf h_out;
     size_t h_counts = 0, h_peaks = 0, h_state = 0, h_rec = 0, h_live = 0, h_total = 0;
     void release() {
         for (DevBuf* b : {&d_canvas, &d_map, &d_bmax, &d_bloc, &d_jobs, &d_nodes, &d_top, &d_topn, &d_peaks,
-                          &d_counts, &d_state, &d_live, &d_livecnt, &d_rec})
+                          &d_counts, &d_state, &d_live, &d_livecnt, &d_rec, &d_rowsum, &d_wsum, &d_wsq, &d_tab, &d_roi})
             b->release();
         h_out.release();
         valid = false;
@@ -381,6 +384,30 @@ int build_plan(fpm_ctx* ctx) {
     HIP_TRY(P.d_live.ensure(sizeof(int32_t) * (size_t)P.C * 2));
     HIP_TRY(P.d_livecnt.ensure(sizeof(int32_t) * (L + 2)));
     HIP_TRY(P.d_rec.ensure(sizeof(RoiRecord) * (size_t)P.C * P.n3));
+    {   // refinement scratch per ROI (tables, sampled ROI, row sums, window partials); bounded, rounds cover the rest
+        size_t max_rows = 1, max_chunks = 1;
+        int max_w = 1;
+        for (int l = 0; l < L; ++l) {
+            const int rc = roi_pick_rc(ctx->tmpl[l].w, ctx->tmpl[l].h);
+            max_rows = std::max(max_rows, (size_t)ctx->tmpl[l].h);
+            max_chunks = std::max(max_chunks, (size_t)(ctx->tmpl[l].h + rc - 1) / rc);
+            max_w = std::max(max_w, ctx->tmpl[l].w);
+        }
+        P.roi_pitch = roi_pitch_for(max_w);
+        P.tabw = P.roi_pitch;
+        P.tabh = round_up((int)max_rows + 6, 4);
+        P.roi_stride = round_up((size_t)P.roi_pitch * (max_rows + 6 + 1), (size_t)256);
+        const size_t per_roi = sizeof(int32_t) * 2 * (P.tabw + P.tabh) + P.roi_stride + max_rows * 49 * 4 +
+                               max_chunks * 49 * 12;
+        const size_t budget = (size_t)16 << 30;   // of 288 GB HBM; rounds only beyond this
+        const size_t want = (size_t)P.C * P.n3;
+        P.slot_cap = (int)std::max<size_t>(1, std::min(want, budget / per_roi));
+        HIP_TRY(P.d_tab.ensure((size_t)P.slot_cap * 2 * (P.tabw + P.tabh) * sizeof(int32_t)));
+        HIP_TRY(P.d_roi.ensure((size_t)P.slot_cap * P.roi_stride));
+        HIP_TRY(P.d_rowsum.ensure((size_t)P.slot_cap * max_rows * 49 * 4));
+        HIP_TRY(P.d_wsum.ensure((size_t)P.slot_cap * max_chunks * 49 * 4));
+        HIP_TRY(P.d_wsq.ensure((size_t)P.slot_cap * max_chunks * 49 * 8));
+    }
     // job tables
     std::vector<WarpJob> wj(J);
     std::vector<NccJob> nj(J);
@@ -531,27 +558,47 @@ int enqueue_search(fpm_ctx* ctx) {
         const int d = L - 1 - l;
         const SrcLevel& lv = ctx->src[l];
         const TmplLevel& tl = ctx->tmpl[l];
-        {
-            ProfScope ps(ctx, FPM_K_ROI_CORR, 0);
-            RoiArgs ra;
-            ra.level = dsrc + lv.off; ra.level_stride = lv.img_bytes;
-            ra.W = lv.w; ra.H = lv.h; ra.P = lv.pitch;
-            ra.tmpl = ctx->d_tmpl.as<uint8_t>() + tl.off; ra.tw = tl.w; ra.th = tl.h; ra.tp = tl.pitch;
-            ra.n3 = P.n3;
-            ra.rc = roi_pick_rc(tl.w, tl.h);
-            ra.fold = ctx->prm.use_simd ? 1 : 0;
-            ra.equal1 = tl.equal1 ? 1 : 0;
-            ra.per_source = P.nang * P.cap;
-            ra.mean = tl.mean; ra.norm = tl.norm; ra.inv_area = tl.inv_area;
-            ra.live = live[d & 1];
-            ra.live_count = livecnt + d;
-            ra.state = P.d_state.as<CandState>();
-            ra.nodes = P.d_nodes.as<AngleNode>() + P.node_off[d];
-            ra.rec = P.d_rec.as<RoiRecord>();
-            launch_roi_corr(ra, P.C * P.n3, st);
+        RoiArgs ra;
+        ra.level = dsrc + lv.off; ra.level_stride = lv.img_bytes;
+        ra.W = lv.w; ra.H = lv.h; ra.P = lv.pitch;
+        ra.tmpl = ctx->d_tmpl.as<uint8_t>() + tl.off; ra.tw = tl.w; ra.th = tl.h; ra.tp = tl.pitch;
+        ra.n3 = P.n3;
+        ra.rc = roi_pick_rc(tl.w, tl.h);
+        ra.nchunk = (tl.h + ra.rc - 1) / ra.rc;
+        ra.fold = ctx->prm.use_simd ? 1 : 0;
+        ra.equal1 = tl.equal1 ? 1 : 0;
+        ra.per_source = P.nang * P.cap;
+        ra.mean = tl.mean; ra.norm = tl.norm; ra.inv_area = tl.inv_area;
+        ra.live = live[d & 1];
+        ra.live_count = livecnt + d;
+        ra.state = P.d_state.as<CandState>();
+        ra.nodes = P.d_nodes.as<AngleNode>() + P.node_off[d];
+        ra.tab = P.d_tab.as<int32_t>(); ra.tabw = P.tabw; ra.tabh = P.tabh;
+        ra.roi = P.d_roi.as<uint8_t>(); ra.roi_pitch = P.roi_pitch; ra.roi_stride = P.roi_stride;
+        ra.rowsum = P.d_rowsum.as<uint32_t>();
+        ra.wsum = P.d_wsum.as<uint32_t>();
+        ra.wsq = P.d_wsq.as<uint64_t>();
+        ra.rec = P.d_rec.as<RoiRecord>();
+        const int total_rois = P.C * P.n3;
+        for (int base = 0; base < total_rois; base += P.slot_cap) {
+            ra.slot_base = base;
+            ra.slot_cap = std::min(P.slot_cap, total_rois - base);
+            {
+                ProfScope ps(ctx, FPM_K_ROI_WARP, 0);
+                launch_roi_tables(ra, st);
+                launch_roi_warp(ra, st);
+            }
+            {
+                ProfScope ps(ctx, FPM_K_ROI_CORR, 0);
+                launch_roi_corr(ra, st);
+            }
+            {
+                ProfScope ps(ctx, FPM_K_ROI_EVAL, 0);
+                launch_roi_eval(ra, st);
+            }
         }
         if (l > 0) {
-            ProfScope ps(ctx, FPM_K_ROI_EVAL, 0);
+            ProfScope ps(ctx, FPM_K_CAND, 0);
             StepArgs sa;
             sa.live_in = live[d & 1];
             sa.live_in_count = livecnt + d;
@@ -714,7 +761,15 @@ int run_staged(fpm_ctx* ctx, std::vector<std::vector<fpm_result>>& results) {
             const int l = P.L - 1 - d;
             const TmplLevel& t = ctx->tmpl[l];
             const int64_t rois = (int64_t)lc[d] * P.n3;
-            ctx->kp[FPM_K_ROI_CORR].bytes += rois * ((int64_t)(t.w + 6) * (t.h + 6) + (int64_t)t.w * t.h + 49 * 4);
+            const int rc = roi_pick_rc(t.w, t.h);
+            const int64_t nch = (t.h + rc - 1) / rc;
+            // warp: ROI bytes written (its source taps are a gather, not counted); corr: ROI + template read,
+            // row sums + window partials written
+            ctx->kp[FPM_K_ROI_WARP].bytes += rois * (int64_t)(t.w + 6) * (t.h + 6);
+            ctx->kp[FPM_K_ROI_CORR].bytes +=
+                rois * ((int64_t)(t.w + 6) * (t.h + 6) + (int64_t)t.w * t.h + (int64_t)t.h * 49 * 4 + nch * 49 * 12);
+            // eval kernel: row sums + partials read, one record written
+            ctx->kp[FPM_K_ROI_EVAL].bytes += rois * ((int64_t)t.h * 49 * 4 + nch * 49 * 12 + (int64_t)sizeof(RoiRecord));
         }
     }
     return FPM_OK;

@@ -90,15 +90,26 @@ struct RoiArgs {
     const uint8_t* tmpl;     // template level
     int32_t tw, th, tp;
     int32_t n3;              // refinement angles per candidate (1 or 3)
-    int32_t rc;              // template rows per chunk
+    int32_t rc;              // template rows per correlation chunk
+    int32_t nchunk;          // ceil(th / rc)
     int32_t fold;            // use_simd
     int32_t equal1;
     int32_t per_source;      // candidates per source (nang * cap)
+    int32_t slot_base;       // this round covers live ROIs [slot_base, slot_base + slot_cap)
+    int32_t slot_cap;
     double mean, norm, inv_area;
     const int32_t* live;
     const int32_t* live_count;
     const CandState* state;
     const AngleNode* nodes;  // level nodes; child = parent * n3 + j
+    int32_t* tab;            // [slot] fixed-point warp tables: ad[tabw], bd[tabw], x0[tabh], y0[tabh]
+    int32_t tabw, tabh;
+    uint8_t* roi;            // [slot] sampled ROI, (th+6) rows x roi_pitch bytes
+    int32_t roi_pitch;
+    size_t roi_stride;
+    uint32_t* rowsum;        // [slot][th][49] exact int32 per-row dot products
+    uint32_t* wsum;          // [slot][nchunk][49] window-sum partials of I
+    uint64_t* wsq;           // [slot][nchunk][49] window-sum partials of I^2
     RoiRecord* rec;          // [cand * n3 + j]
 };
 
@@ -123,9 +134,13 @@ void launch_warp(const WarpJob* jobs, int njobs, int max_pixels, hipStream_t st)
 void launch_ncc_map(const NccJob* jobs, int njobs, int max_out, int tmpl_bytes, hipStream_t st);
 void launch_nms(const NmsArgs& a, int njobs, int max_map, hipStream_t st);
 void launch_cand_init(const CandInitArgs& a, hipStream_t st);
-void launch_roi_corr(const RoiArgs& a, int max_items, hipStream_t st);
+void launch_roi_tables(const RoiArgs& a, hipStream_t st);
+void launch_roi_warp(const RoiArgs& a, hipStream_t st);
+void launch_roi_corr(const RoiArgs& a, hipStream_t st);
+void launch_roi_eval(const RoiArgs& a, hipStream_t st);
 void launch_cand_step(const StepArgs& a, int max_items, hipStream_t st);
-size_t roi_lds_bytes(int tw, int th, int rc);
 int roi_pick_rc(int tw, int th);
+int roi_pitch_for(int tw);
+size_t roi_corr_lds(int roi_pitch, int tw, int rc);
 
 }  // namespace fpm

@@ -81,58 +81,122 @@ __device__ __forceinline__ float ccoeff(double num, double wsum, double wsq, dou
 }
 
 // ============================================================================================== K1
-// Output tile 64 x 32 per 256-thread workgroup; input tile (132 + 4) x 68 bytes in LDS.  Interior tiles
-// load aligned dwords; border tiles apply reflect-101 per byte.  Exact integer arithmetic.
-constexpr int PYR_OW = 64, PYR_OH = 32, PYR_IW = 2 * PYR_OW + 8, PYR_IH = 2 * PYR_OH + 4;
+// pyrDown, LDS-tiled: a 256-thread workgroup produces a 128 x 32 output tile.  Its 288 x 68 input tile (source
+// columns 2*ox0-16 .. +287, rows 2*oy0-2 .. +67, rows reflected at load time) is fetched with 16-byte loads that
+// are all issued before the first use; columns outside the image are then patched in LDS with reflect-101.
+// Horizontal [1 4 6 4 1]: h = dot4(0x04060401, 4 bytes) + 5th byte with v_dot4_u32_u8; vertical sum of 5 rows,
+// (v + 128) >> 8, four output bytes per dword store.  Exact integer arithmetic.
+constexpr int PD_OW = 128, PD_OH = 32;
+constexpr int PD_IW = 2 * PD_OW + 32, PD_IH = 2 * PD_OH + 4;   // 288 x 68 bytes
+constexpr uint32_t PD_K = 0x04060401u;                         // bytes {1, 4, 6, 4}
 
+// ABL (profiling builds only): 1 = stop after the loads, 2 = after the LDS tile, 3 = after the horizontal pass
+template <int ABL>
 __global__ __launch_bounds__(256) void k_pyr_down(const uint8_t* __restrict__ src, int sw, int sh, int sp,
                                                   size_t s_img, uint8_t* __restrict__ dst, int dw, int dh,
                                                   int dp, size_t d_img) {
-    __shared__ __attribute__((aligned(16))) uint8_t tin[PYR_IH][PYR_IW];
-    __shared__ uint16_t hs[PYR_IH][PYR_OW];
+    __shared__ __attribute__((aligned(16))) uint8_t tin[PD_IH][PD_IW];
+    __shared__ __attribute__((aligned(16))) uint16_t hs[PD_IH][PD_OW];
     src += (size_t)blockIdx.z * s_img;
     dst += (size_t)blockIdx.z * d_img;
     const int tid = threadIdx.x;
-    const int ox0 = blockIdx.x * PYR_OW, oy0 = blockIdx.y * PYR_OH;
-    const int ix0 = 2 * ox0 - 4;  // tin column 0 <-> source column ix0 (4-byte aligned)
-    const int iy0 = 2 * oy0 - 2;  // tin row 0    <-> source row iy0
-    const bool interior = ix0 >= 0 && ix0 + PYR_IW <= sw && iy0 >= 0 && iy0 + PYR_IH <= sh;
-    if (interior) {
-        constexpr int WPR = PYR_IW / 4;  // 34 dwords per row
-        for (int i = tid; i < PYR_IH * WPR; i += 256) {
-            const int r = i / WPR, c = i - r * WPR;
-            *(uint32_t*)&tin[r][4 * c] = *(const uint32_t*)(src + (size_t)(iy0 + r) * sp + ix0 + 4 * c);
+    const int ox0 = blockIdx.x * PD_OW, oy0 = blockIdx.y * PD_OH;
+    const int ix0 = 2 * ox0 - 16;   // tin column 0 <-> source column ix0 (16-byte aligned)
+    const int iy0 = 2 * oy0 - 2;    // tin row 0    <-> source row iy0 (reflected)
+    constexpr int Q = PD_IW / 16;   // 18 uint4 per row
+    constexpr int NLD = (PD_IH * Q + 255) / 256;
+    // rows: one reflection covers every row an output needs (-2 .. sh+1); rows past that are clamped (unused)
+    auto srow = [&](int r) {
+        int y = iy0 + r;
+        y = y < 0 ? -y : y;
+        y = y >= sh ? 2 * sh - 2 - y : y;
+        return y < 0 ? 0 : (y >= sh ? sh - 1 : y);
+    };
+    uint4 v[NLD];
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+        const int i = tid + 256 * k;
+        const int r = i / Q, c = i - r * Q;
+        const int x = ix0 + 16 * c;
+        v[k] = make_uint4(0, 0, 0, 0);
+        if (i < PD_IH * Q && x >= 0 && x + 16 <= sp) v[k] = *(const uint4*)(src + (size_t)srow(r) * sp + x);
+    }
+    if (ABL == 1) {
+        uint32_t x = 0;
+        for (int k = 0; k < NLD; ++k) x ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+        if (x == 0x9e3779b9u) dst[tid] = (uint8_t)x;
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+        const int i = tid + 256 * k;
+        if (i < PD_IH * Q) {
+            const int r = i / Q, c = i - r * Q;
+            *(uint4*)&tin[r][16 * c] = v[k];
         }
-    } else {
-        for (int i = tid; i < PYR_IH * (PYR_IW - 4); i += 256) {
-            const int r = i / (PYR_IW - 4), c = 2 + (i - r * (PYR_IW - 4));
-            tin[r][c] = src[(size_t)reflect101(iy0 + r, sh) * sp + reflect101(ix0 + c, sw)];
+    }
+    // columns outside [0, sw) that an output of this tile reads (at most 2 on each side): reflect-101
+    const int xlo = 2 * ox0 - 2, xhi = min(2 * (ox0 + PD_OW - 1) + 2, 2 * (dw - 1) + 2);
+    if (xlo < 0 || xhi >= sw) {          // uniform per workgroup
+        __syncthreads();                 // the 16-byte tile stores above cover the patched bytes
+        for (int i = tid; i < PD_IH * 4; i += 256) {
+            const int r = i >> 2, k = i & 3;
+            const int x = k < 2 ? xlo + k : xhi - (k - 2);   // xlo, xlo+1, xhi, xhi-1
+            if ((x < 0 && k < 2) || (x >= sw && k >= 2))
+                tin[r][x - ix0] = src[(size_t)srow(r) * sp + reflect101(x, sw)];
         }
     }
     __syncthreads();
-    // horizontal [1 4 6 4 1]: output column oc uses tin columns 2*oc + 2 .. 2*oc + 6
-    for (int i = tid; i < PYR_IH * PYR_OW; i += 256) {
-        const int r = i >> 6, oc = i & 63;
-        const uint8_t* p = &tin[r][2 * oc + 2];
-        hs[r][oc] = (uint16_t)(p[0] + 4 * p[1] + 6 * p[2] + 4 * p[3] + p[4]);
+    if (ABL == 2) { if (tin[tid & 63][tid >> 2] == 0x5a && tid == 999) dst[0] = 1; return; }
+    // horizontal: 4 consecutive outputs per item, tin columns 2*oc + 14 .. 2*oc + 24
+    constexpr int NH = PD_IH * (PD_OW / 4);
+#pragma unroll
+    for (int k = 0; k < (NH + 255) / 256; ++k) {
+        const int i = tid + 256 * k;
+        if (i >= NH) break;
+        const int r = i / (PD_OW / 4), g = i - r * (PD_OW / 4);
+        const uint32_t* w = (const uint32_t*)&tin[r][8 * g + 12];   // bytes 8g+12 .. 8g+27
+        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
+        // output 4g+j uses tin bytes 8g + 2j + 14 .. +18  (= w-relative 2j + 2 .. 2j + 6)
+        const uint32_t h0 = __builtin_amdgcn_udot4(PD_K, __builtin_amdgcn_alignbyte(w1, w0, 2), 0, false) + ((w1 >> 16) & 0xff);
+        const uint32_t h1 = __builtin_amdgcn_udot4(PD_K, w1, 0, false) + (w2 & 0xff);
+        const uint32_t h2 = __builtin_amdgcn_udot4(PD_K, __builtin_amdgcn_alignbyte(w2, w1, 2), 0, false) + ((w2 >> 16) & 0xff);
+        const uint32_t h3 = __builtin_amdgcn_udot4(PD_K, w2, 0, false) + (w3 & 0xff);
+        uint2 o;
+        o.x = h0 | (h1 << 16);
+        o.y = h2 | (h3 << 16);
+        *(uint2*)&hs[r][4 * g] = o;
     }
     __syncthreads();
-    const int oc = tid & 63;
-    const int ox = ox0 + oc;
-    for (int orow = tid >> 6; orow < PYR_OH; orow += 4) {
-        const int oy = oy0 + orow;
-        if (ox < dw && oy < dh) {
-            const int v = hs[2 * orow][oc] + 4 * hs[2 * orow + 1][oc] + 6 * hs[2 * orow + 2][oc] +
-                          4 * hs[2 * orow + 3][oc] + hs[2 * orow + 4][oc];
-            dst[(size_t)oy * dp + ox] = (uint8_t)((v + 128) >> 8);
+    if (ABL == 3) { if (hs[tid & 63][tid >> 1] == 0x5a5a && tid == 999) dst[0] = 1; return; }
+    // vertical: 4 consecutive outputs of one row per item
+#pragma unroll
+    for (int k = 0; k < PD_OH * (PD_OW / 4) / 256; ++k) {
+        const int i = tid + 256 * k;
+        const int orow = i / (PD_OW / 4), g = i - orow * (PD_OW / 4);
+        const int oy = oy0 + orow, ox = ox0 + 4 * g;
+        if (oy >= dh || ox >= dw) continue;
+        uint32_t acc[4] = {128, 128, 128, 128};
+        const int kw[5] = {1, 4, 6, 4, 1};
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+            const uint2 q = *(const uint2*)&hs[2 * orow + t][4 * g];
+            acc[0] += kw[t] * (q.x & 0xffff); acc[1] += kw[t] * (q.x >> 16);
+            acc[2] += kw[t] * (q.y & 0xffff); acc[3] += kw[t] * (q.y >> 16);
+        }
+        uint8_t* d = dst + (size_t)oy * dp + ox;
+        if (ox + 4 <= dw) {
+            *(uint32_t*)d = (acc[0] >> 8) | ((acc[1] >> 8) << 8) | ((acc[2] >> 8) << 16) | ((acc[3] >> 8) << 24);
+        } else {
+            for (int j = 0; j < dw - ox; ++j) d[j] = (uint8_t)(acc[j] >> 8);
         }
     }
 }
 
 void launch_pyr_down(const uint8_t* src, int sw, int sh, int sp, size_t s_img, uint8_t* dst, int dw, int dh,
                      int dp, size_t d_img, int nimg, hipStream_t st) {
-    dim3 grid((dw + PYR_OW - 1) / PYR_OW, (dh + PYR_OH - 1) / PYR_OH, nimg);
-    hipLaunchKernelGGL(k_pyr_down, grid, dim3(256), 0, st, src, sw, sh, sp, s_img, dst, dw, dh, dp, d_img);
+    dim3 grid((dw + PD_OW - 1) / PD_OW, (dh + PD_OH - 1) / PD_OH, nimg);
+    hipLaunchKernelGGL(k_pyr_down<0>, grid, dim3(256), 0, st, src, sw, sh, sp, s_img, dst, dw, dh, dp, d_img);
 }
 
 // ============================================================================================== K2
@@ -363,74 +427,350 @@ void launch_cand_init(const CandInitArgs& a, hipStream_t st) {
 }
 
 // ============================================================================================== K6+K7+K8
-// One workgroup per refinement ROI (candidate, angle j).  Per chunk of RC template rows:
-//   sample ROI rows [t0, t0+rc+6) of the rotated (w+6)x(h+6) ROI straight from the pyramid level into LDS,
-//   stage template rows [t0, t0+rc) into LDS, per-row int32 dot products for all 49 (dy,dx) offsets with
-//   v_dot4_u32_u8 (thread = (template row, dy), 7 dx accumulators via v_alignbyte), then 49 threads fold
-//   the chunk's rows into f32 in row order and add exact window sums.  Finally CCOEFF normalisation in f64,
-//   first-occurrence argmax over the 7x7 map, border flag and 3x3 neighbourhood.
-constexpr int ROI_MAXRC = 32;
+// Refinement ROIs (getRotatedROI + MatchTemplate(bUseSIMD) + minMaxLoc, TemplateMatcher.cpp:309-328), as four
+// short kernels over the device-compacted list of live (candidate, angle) ROIs:
+//   k_roi_tables  per ROI: the fixed-point warp tables (adelta/bdelta per column, X0/Y0 per row)
+//   k_roi_warp    per 32x32 ROI tile and wave: LDS-staged footprint + bilinear gathers -> ROI bytes in HBM
+//   k_roi_corr    per (ROI, 16 template rows): exact int32 row dot products for all 49 offsets + window sums
+//   k_roi_eval    per ROI: ordered f32 fold (:505-508), f64 CCOEFF normalisation, argmax, border, 3x3
+// ---- geometry of the refinement scratch ----------------------------------------------------------------------
+constexpr int ROI_RC = 16;           // template rows per correlation chunk
+constexpr int ROI_T = 32;            // warp tile: 32 x 32 ROI pixels per wave task
+constexpr int ROI_FT = 4096;         // per-wave LDS footprint buffer (bytes) >= worst-case rotated tile bbox
 
-struct RoiLayout {
-    int RW, RH, ntw, SBp, TBp;
-    size_t o_ad, o_bd, o_x0, o_y0, o_ra, o_rq, o_rs, o_sc, o_sb, o_tb, total;
-    __host__ __device__ void make(int tw, int th, int rc) {
-        RW = tw + 6; RH = th + 6;
-        ntw = (tw + 3) / 4;
-        SBp = 4 * ntw + 12; if (SBp < RW) SBp = (RW + 3) & ~3;
-        if (((SBp >> 2) & 1) == 0) SBp += 4;
-        TBp = 4 * ntw; if (((TBp >> 2) & 1) == 0) TBp += 4;
-        size_t o = 0;
-        auto take = [&](size_t bytes) { size_t r = o; o += (bytes + 15) & ~(size_t)15; return r; };
-        o_ad = take(sizeof(int) * RW);
-        o_bd = take(sizeof(int) * RW);
-        o_x0 = take(sizeof(int) * (rc + 6));
-        o_y0 = take(sizeof(int) * (rc + 6));
-        o_ra = take(sizeof(int) * (rc + 6));
-        o_rq = take(sizeof(int) * (rc + 6));
-        o_rs = take(sizeof(uint32_t) * rc * 49);
-        o_sc = take(sizeof(float) * 64);
-        o_sb = take((size_t)(rc + 6) * SBp);
-        o_tb = take((size_t)rc * TBp);
-        total = o;
+int roi_pick_rc(int /*tw*/, int th) { return th < ROI_RC ? th : ROI_RC; }
+
+// ROI row pitch: >= RW + 16 (look-ahead words of the correlation), pitch/4 = 4 * odd (conflict-free b128 reads)
+__host__ __device__ inline int roi_pitch_calc(int tw) {
+    int q = ((tw + 6 + 16) + 15) / 16;  // in 16-byte units
+    if ((q & 1) == 0) ++q;
+    return q * 16;
+}
+int roi_pitch_for(int tw) { return roi_pitch_calc(tw); }
+
+__host__ __device__ inline int tmpl_pitch_calc(int tw) {   // template LDS rows: >= 4*ceil(tw/4) + 16, same rule
+    int q = ((((tw + 3) / 4) * 4 + 16) + 15) / 16;
+    if ((q & 1) == 0) ++q;
+    return q * 16;
+}
+
+size_t roi_corr_lds(int roi_pitch, int tw, int rc) {
+    return (size_t)(rc + 6) * roi_pitch + (size_t)(rc + 12) * tmpl_pitch_calc(tw) +
+           sizeof(uint32_t) * (rc * 49 + 2 * (rc + 6) + 2 * 7 * (rc + 6)) + 64;
+}
+
+// bilinear tap from global memory (fallback when a footprint does not fit the LDS buffer);
+// (sum_i w_i v_i + 2^14) >> 15 evaluated as t = 32*h0 + fy*(h1 - h0), h = 32*va + fx*(vb - va) ->
+// (t + 512) >> 10: the same integer with fewer multiplies
+__device__ __forceinline__ int roi_tap(const uint8_t* __restrict__ src, int sw, int sh, int sp, int X, int Y) {
+    const int sx = sat_s16(X >> kInterBits), sy = sat_s16(Y >> kInterBits);
+    const int fx = X & (kInterTab - 1), fy = Y & (kInterTab - 1);
+    int v0, v1, v2, v3;
+    if ((unsigned)sx < (unsigned)(sw - 1) && (unsigned)sy < (unsigned)(sh - 1)) {
+        const uint8_t* p = src + (size_t)sy * sp + sx;
+        v0 = p[0]; v1 = p[1]; v2 = p[sp]; v3 = p[sp + 1];
+    } else if (sx >= sw || sx + 1 < 0 || sy >= sh || sy + 1 < 0) {
+        return 0;
+    } else {
+        const bool x0 = sx >= 0 && sx < sw, x1 = sx + 1 >= 0 && sx + 1 < sw;
+        const bool y0 = sy >= 0 && sy < sh, y1 = sy + 1 >= 0 && sy + 1 < sh;
+        const uint8_t* r0 = src + (size_t)sy * sp;
+        const uint8_t* r1 = r0 + sp;
+        v0 = x0 && y0 ? r0[sx] : 0;
+        v1 = x1 && y0 ? r0[sx + 1] : 0;
+        v2 = x0 && y1 ? r1[sx] : 0;
+        v3 = x1 && y1 ? r1[sx + 1] : 0;
     }
-};
-
-size_t roi_lds_bytes(int tw, int th, int rc) {
-    RoiLayout l;
-    l.make(tw, th, rc);
-    return l.total;
+    const int h0 = 32 * v0 + fx * (v1 - v0), h1 = 32 * v2 + fx * (v3 - v2);
+    return (32 * h0 + fy * (h1 - h0) + 512) >> 10;
 }
 
-int roi_pick_rc(int tw, int th) {
-    int rc = th < ROI_MAXRC ? th : ROI_MAXRC;
-    while (rc > 1 && roi_lds_bytes(tw, th, rc) > 150 * 1024) --rc;
-    return rc;
+__device__ __forceinline__ void roi_slot(const RoiArgs& a, int slot, int& id, int& jj) {
+    const int ri = a.slot_base + slot;
+    const int li = ri / a.n3;
+    jj = ri - li * a.n3;
+    id = a.live[li];
 }
 
-__global__ __launch_bounds__(256) void k_roi_corr(RoiArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    RoiLayout L;
-    L.make(a.tw, a.th, a.rc);
-    int* ad = (int*)(smem + L.o_ad);
-    int* bd = (int*)(smem + L.o_bd);
-    int* x0r = (int*)(smem + L.o_x0);
-    int* y0r = (int*)(smem + L.o_y0);
-    int* rall = (int*)(smem + L.o_ra);
-    int* rallq = (int*)(smem + L.o_rq);
-    uint32_t* rs = (uint32_t*)(smem + L.o_rs);
-    float* sc = (float*)(smem + L.o_sc);
-    uint8_t* SB = smem + L.o_sb;
-    uint8_t* TB = smem + L.o_tb;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int RW = L.RW, tw = a.tw, th = a.th;
-    const int items = *a.live_count * a.n3;
+__device__ __forceinline__ int roi_count(const RoiArgs& a) {
+    int rois = *a.live_count * a.n3 - a.slot_base;
+    return rois < 0 ? 0 : (rois > a.slot_cap ? a.slot_cap : rois);
+}
 
-    for (int item = blockIdx.x; item < items; item += gridDim.x) {
-        const int li = item / a.n3, jj = item - li * a.n3;
-        const int id = a.live[li];
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---- K6a: per-ROI fixed-point warp tables (getRotatedROI -> warpAffine's adelta/bdelta/X0/Y0) ----------------
+__global__ __launch_bounds__(256) void k_roi_tables(RoiArgs a) {
+    const int rois = roi_count(a);
+    for (int slot = blockIdx.x; slot < rois; slot += gridDim.x) {
+        int id, jj;
+        roi_slot(a, slot, id, jj);
         const CandState st = a.state[id];
         const AngleNode nd = a.nodes[st.node * a.n3 + jj];
+        double M[6];
+        roi_matrix(a.W, a.H, f2(st.lt.x * 2, st.lt.y * 2), nd.c, nd.s, M);
+        int32_t* t = a.tab + (size_t)slot * 2 * (a.tabw + a.tabh);
+        for (int x = threadIdx.x; x < a.tabw; x += 256) {
+            t[x] = rint_i(M[0] * x * kAbScale);
+            t[a.tabw + x] = rint_i(M[3] * x * kAbScale);
+        }
+        for (int y = threadIdx.x; y < a.tabh; y += 256) {
+            t[2 * a.tabw + y] = rint_i((M[1] * y + M[2]) * kAbScale) + kRoundDelta;
+            t[2 * a.tabw + a.tabh + y] = rint_i((M[4] * y + M[5]) * kAbScale) + kRoundDelta;
+        }
+    }
+}
+
+// ---- K6b: ROI sampling.  One wave = one 32x32 ROI tile: the tile's source footprint (bounding box of the
+// rotated tile, clipped to the image) is staged into wave-private LDS with aligned dword loads, then every lane
+// produces 4 rows x 4 pixels by gathering the bilinear taps from LDS and stores them as dwords.  No workgroup
+// barrier; full occupancy.  Border pixels follow remapBilinear's BORDER_CONSTANT(0) rules exactly.
+__global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t ft_all[4][ROI_FT];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint8_t* FT = ft_all[wv];
+    const int RW = a.tw + 6, RH = a.th + 6, W = a.W, H = a.H;
+    const int txn = (RW + ROI_T - 1) / ROI_T, tyn = (RH + ROI_T - 1) / ROI_T;
+    const int rois = roi_count(a);
+    const long tasks = (long)rois * tyn * txn;
+    const int lr = lane >> 3, lg = lane & 7;   // lane -> rows lr + 8i, columns 4*lg .. 4*lg+3
+    for (long task = (long)blockIdx.x * 4 + wv; task < tasks; task += (long)gridDim.x * 4) {
+        const int tx = (int)(task % txn);
+        const long q = task / txn;
+        const int ty = (int)(q % tyn);
+        const int slot = (int)(q / tyn);
+        int id, jj;
+        roi_slot(a, slot, id, jj);
+        const uint8_t* lvl = a.level + (size_t)(id / a.per_source) * a.level_stride;
+        const int32_t* t = a.tab + (size_t)slot * 2 * (a.tabw + a.tabh);
+        const int32_t* tad = t;
+        const int32_t* tbd = t + a.tabw;
+        const int32_t* tx0 = t + 2 * a.tabw;
+        const int32_t* ty0 = tx0 + a.tabh;
+        const int cx0 = tx * ROI_T, cx1 = min(cx0 + ROI_T, RW) - 1;
+        const int ry0 = ty * ROI_T, ry1 = min(ry0 + ROI_T, RH) - 1;
+        int bx0 = INT_MAX, bx1 = INT_MIN, by0 = INT_MAX, by1 = INT_MIN;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int c = (k & 1) ? cx1 : cx0, r = (k & 2) ? ry1 : ry0;
+            const int X = (tx0[r] + tad[c]) >> (kAbBits - kInterBits);
+            const int Y = (ty0[r] + tbd[c]) >> (kAbBits - kInterBits);
+            bx0 = min(bx0, X >> kInterBits); bx1 = max(bx1, X >> kInterBits);
+            by0 = min(by0, Y >> kInterBits); by1 = max(by1, Y >> kInterBits);
+        }
+        // +-1 px covers the per-pixel rounding of the fixed-point map, +1 the second tap; clip to the image
+        bx0 = max(bx0 - 1, 0); by0 = max(by0 - 1, 0);
+        bx1 = min(bx1 + 2, W - 1); by1 = min(by1 + 2, H - 1);
+        const bool any = bx0 <= bx1 && by0 <= by1;
+        const int bxa = bx0 & ~3;
+        int ftw = any ? ((bx1 - bxa + 4) & ~3) : 0;
+        if (((ftw >> 2) & 1) == 0) ftw += 4;    // odd dword pitch: spread gather banks
+        const int fth = any ? by1 - by0 + 1 : 0;
+        const bool in_lds = ftw * fth <= ROI_FT;
+        wave_sync();   // previous task's gathers are done with FT
+        if (any && in_lds) {
+            const int wpr = ftw >> 2;
+            for (int i = lane; i < wpr * fth; i += 64) {
+                const int r = i / wpr, c = i - r * wpr;
+                const int gx = bxa + 4 * c;
+                *(uint32_t*)(FT + r * ftw + 4 * c) =
+                    gx < a.P ? *(const uint32_t*)(lvl + (size_t)(by0 + r) * a.P + gx) : 0u;
+            }
+        }
+        wave_sync();
+        const int c0 = cx0 + 4 * lg;
+        if (c0 <= cx1) {
+            const int4 A = *(const int4*)(tad + c0);
+            const int4 B = *(const int4*)(tbd + c0);
+            const int adv[4] = {A.x, A.y, A.z, A.w}, bdv[4] = {B.x, B.y, B.z, B.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = ry0 + lr + 8 * i;
+                if (r > ry1) break;
+                const int X0 = tx0[r], Y0 = ty0[r];
+                uint32_t pk = 0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int X = (X0 + adv[u]) >> (kAbBits - kInterBits);
+                    const int Y = (Y0 + bdv[u]) >> (kAbBits - kInterBits);
+                    int v;
+                    if (in_lds) {
+                        const int sx = sat_s16(X >> kInterBits), sy = sat_s16(Y >> kInterBits);
+                        const int fx = X & (kInterTab - 1), fy = Y & (kInterTab - 1);
+                        const uint8_t* p = FT + (sy - by0) * ftw + (sx - bxa);
+                        int v0, v1, v2, v3;
+                        if ((unsigned)sx < (unsigned)(W - 1) && (unsigned)sy < (unsigned)(H - 1)) {
+                            v0 = p[0]; v1 = p[1]; v2 = p[ftw]; v3 = p[ftw + 1];
+                        } else if (sx >= W || sx + 1 < 0 || sy >= H || sy + 1 < 0) {
+                            v0 = v1 = v2 = v3 = 0;
+                        } else {
+                            const bool x0 = sx >= 0 && sx < W, x1 = sx + 1 >= 0 && sx + 1 < W;
+                            const bool y0 = sy >= 0 && sy < H, y1 = sy + 1 >= 0 && sy + 1 < H;
+                            v0 = x0 && y0 ? p[0] : 0;
+                            v1 = x1 && y0 ? p[1] : 0;
+                            v2 = x0 && y1 ? p[ftw] : 0;
+                            v3 = x1 && y1 ? p[ftw + 1] : 0;
+                        }
+                        const int h0 = 32 * v0 + fx * (v1 - v0), h1 = 32 * v2 + fx * (v3 - v2);
+                        v = (32 * h0 + fy * (h1 - h0) + 512) >> 10;
+                    } else {
+                        v = roi_tap(lvl, W, H, a.P, X, Y);
+                    }
+                    if (c0 + u >= RW) v = 0;
+                    pk |= (uint32_t)v << (8 * u);
+                }
+                *(uint32_t*)(a.roi + (size_t)slot * a.roi_stride + (size_t)r * a.roi_pitch + c0) = pk;
+            }
+        }
+    }
+}
+
+// ---- K7: per-row exact correlation.  grid = (ROI, chunk of RC template rows).  ROI rows [t0, t0+rc+6) and
+// template rows [t0, t0+rc) are staged into LDS (16-byte loads; template rows padded with 6 zero rows on both
+// sides).  Thread = (source row s, column group g): for every 16-byte slice of its group it forms the 7 byte
+// shifts of the source words with v_alignbyte and accumulates all 49 (dy, dx) dot products of template rows
+// s - dy with v_dot4_u32_u8 (49 accumulators).  Group partials are combined with exact LDS integer atomics.
+// Also exact window sums of I and I^2 per chunk.
+__global__ __launch_bounds__(256) void k_roi_corr(RoiArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int tw = a.tw, th = a.th, RW = tw + 6;
+    const int ntw = (tw + 3) / 4;
+    const int SBp = a.roi_pitch, TBp = tmpl_pitch_calc(tw);
+    const int RC = a.rc, NS = RC + 6;
+    uint8_t* SB = smem;                                   // NS rows x SBp
+    uint8_t* TB = SB + (size_t)NS * SBp;                  // (RC + 12) rows x TBp, rows 0..5 and 6+rc.. zero
+    uint32_t* rs = (uint32_t*)(TB + (size_t)(RC + 12) * TBp);   // RC x 49
+    int* rall = (int*)(rs + RC * 49);                     // NS
+    int* rallq = rall + NS;                               // NS
+    int* wi = rallq + NS;                                 // NS x 7
+    int* wq = wi + NS * 7;                                // NS x 7
+    const int tid = threadIdx.x;
+    const int rois = roi_count(a);
+    const int items = rois * a.nchunk;
+    // column groups: G groups of `seg` words (multiple of 4) per source row
+    for (int item = blockIdx.x; item < items; item += gridDim.x) {
+        const int slot = item / a.nchunk, chunk = item - slot * a.nchunk;
+        const int t0 = chunk * RC, rc = min(RC, th - t0), nsrc = rc + 6;
+        const int G = 256 / nsrc;
+        const int seg = (((ntw + G - 1) / G) + 3) & ~3;
+        __syncthreads();
+        {   // stage: ROI rows (whole pitch incl. zero look-ahead), template rows (zero padded)
+            const uint8_t* rsrc = a.roi + (size_t)slot * a.roi_stride + (size_t)t0 * a.roi_pitch;
+            const int q4 = SBp >> 4;
+            for (int i = tid; i < nsrc * q4; i += 256) {
+                const int r = i / q4, c = i - r * q4;
+                *(uint4*)(SB + (size_t)r * SBp + 16 * c) = *(const uint4*)(rsrc + (size_t)r * a.roi_pitch + 16 * c);
+            }
+            const int tq = TBp >> 2;
+            for (int i = tid; i < (RC + 12) * tq; i += 256) {
+                const int r = i / tq, c = i - r * tq;
+                const int tr = r - 6;
+                uint32_t wv = 0;
+                if (tr >= 0 && tr < rc && 4 * c < tw) {
+                    wv = *(const uint32_t*)(a.tmpl + (size_t)(t0 + tr) * a.tp + 4 * c);
+                    const int valid = tw - 4 * c;
+                    if (valid < 4) wv &= (1u << (8 * valid)) - 1u;
+                }
+                *(uint32_t*)(TB + (size_t)r * TBp + 4 * c) = wv;
+            }
+            for (int i = tid; i < rc * 49; i += 256) rs[i] = 0;
+            if (tid < nsrc) { rall[tid] = 0; rallq[tid] = 0; }
+        }
+        __syncthreads();
+        const int s = tid % nsrc, g = tid / nsrc;
+        if (g < G && !(seg * g >= ntw)) {
+            uint32_t acc[7][7];
+#pragma unroll
+            for (int d = 0; d < 7; ++d)
+#pragma unroll
+                for (int x = 0; x < 7; ++x) acc[d][x] = 0;
+            uint32_t s1 = 0, s2 = 0;
+            const uint32_t* srow = (const uint32_t*)(SB + (size_t)s * SBp);
+            const int k0 = g * seg, k1 = min(k0 + seg, ntw);
+            // TB row for dy is (s - dy + 6)
+            const uint32_t* trow0 = (const uint32_t*)(TB + (size_t)(s + 6) * TBp);
+            uint4 cur = *(const uint4*)(srow + k0);
+            for (int k = k0; k < k1; k += 4) {
+                const uint4 nxt = *(const uint4*)(srow + k + 4);
+                const uint32_t w[6] = {cur.x, cur.y, cur.z, cur.w, nxt.x, nxt.y};
+                uint4 tv[7];
+#pragma unroll
+                for (int d = 0; d < 7; ++d) tv[d] = *(const uint4*)(trow0 - (size_t)d * (TBp >> 2) + k);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (k + q >= k1) break;
+                    const uint32_t a0 = w[q], a1 = w[q + 1], a2 = w[q + 2];
+                    const uint32_t sh[7] = {a0, __builtin_amdgcn_alignbyte(a1, a0, 1), __builtin_amdgcn_alignbyte(a1, a0, 2),
+                                            __builtin_amdgcn_alignbyte(a1, a0, 3), a1,
+                                            __builtin_amdgcn_alignbyte(a2, a1, 1), __builtin_amdgcn_alignbyte(a2, a1, 2)};
+                    s1 = __builtin_amdgcn_udot4(a0, 0x01010101u, s1, false);
+                    s2 = __builtin_amdgcn_udot4(a0, a0, s2, false);
+#pragma unroll
+                    for (int d = 0; d < 7; ++d) {
+                        const uint32_t tt = q == 0 ? tv[d].x : q == 1 ? tv[d].y : q == 2 ? tv[d].z : tv[d].w;
+#pragma unroll
+                        for (int x = 0; x < 7; ++x) acc[d][x] = __builtin_amdgcn_udot4(tt, sh[x], acc[d][x], false);
+                    }
+                }
+                cur = nxt;
+            }
+            // words of the row beyond the last group (look-ahead region) belong to no group: the row sum of
+            // bytes [4*ntw, RW) is added by the group that owns word ntw-1
+            if (k1 == ntw) {
+                for (int k = ntw; k < (RW + 3) / 4; ++k) {
+                    const uint32_t wv = srow[k];
+                    s1 = __builtin_amdgcn_udot4(wv, 0x01010101u, s1, false);
+                    s2 = __builtin_amdgcn_udot4(wv, wv, s2, false);
+                }
+            }
+            atomicAdd(&rall[s], (int)s1);
+            atomicAdd(&rallq[s], (int)s2);
+#pragma unroll
+            for (int d = 0; d < 7; ++d) {
+                const int tl = s - d;
+                if (tl >= 0 && tl < rc)
+#pragma unroll
+                    for (int x = 0; x < 7; ++x) atomicAdd(&rs[tl * 49 + d * 7 + x], acc[d][x]);
+            }
+        }
+        __syncthreads();
+        // rows out + window-row sums (full-row sum minus <= 6 edge pixels)
+        for (int i = tid; i < rc * 49; i += 256) a.rowsum[((size_t)slot * th + t0) * 49 + i] = rs[i];
+        for (int i = tid; i < nsrc * 7; i += 256) {
+            const int r = i / 7, dx = i - r * 7;
+            const uint8_t* sbr = SB + (size_t)r * SBp;
+            int q1 = rall[r], q2 = rallq[r];
+            for (int c = 0; c < dx; ++c) { const int v = sbr[c]; q1 -= v; q2 -= v * v; }
+            for (int c = dx + tw; c < RW; ++c) { const int v = sbr[c]; q1 -= v; q2 -= v * v; }
+            wi[i] = q1;
+            wq[i] = q2;
+        }
+        __syncthreads();
+        if (tid < 49) {
+            const int pdy = tid / 7, pdx = tid - pdy * 7;
+            uint32_t s1 = 0;
+            uint64_t s2 = 0;
+            for (int tl = 0; tl < rc; ++tl) {
+                s1 += (uint32_t)wi[(tl + pdy) * 7 + pdx];
+                s2 += (uint32_t)wq[(tl + pdy) * 7 + pdx];
+            }
+            a.wsum[((size_t)slot * a.nchunk + chunk) * 49 + tid] = s1;
+            a.wsq[((size_t)slot * a.nchunk + chunk) * 49 + tid] = s2;
+        }
+    }
+}
+
+__global__ __launch_bounds__(64) void k_roi_eval(RoiArgs a) {
+    __shared__ float sc[64];
+    const int tid = threadIdx.x;
+    const int rois = roi_count(a);
+    for (int slot = blockIdx.x; slot < rois; slot += gridDim.x) {
+        int id, jj;
+        roi_slot(a, slot, id, jj);
         RoiRecord* out = a.rec + (size_t)id * a.n3 + jj;
         if (a.equal1) {   // CCOEFF_Denominator: matResult = 1 everywhere (:529-533)
             if (tid == 0) {
@@ -439,110 +779,30 @@ __global__ __launch_bounds__(256) void k_roi_corr(RoiArgs a) {
             }
             continue;
         }
-        const int src = id / a.per_source;
-        const uint8_t* lvl = a.level + (size_t)src * a.level_stride;
-        double M[6];
-        roi_matrix(a.W, a.H, f2(st.lt.x * 2, st.lt.y * 2), nd.c, nd.s, M);
-        for (int x = tid; x < RW; x += 256) {
-            ad[x] = rint_i(M[0] * x * kAbScale);
-            bd[x] = rint_i(M[3] * x * kAbScale);
-        }
-        float accF = 0.f;
-        uint64_t accI = 0;
-        int64_t sumI = 0, sumQ = 0;
-        const int pdy = tid / 7, pdx = tid - pdy * 7;
-
-        for (int t0 = 0; t0 < th; t0 += a.rc) {
-            const int rc = min(a.rc, th - t0), nsrc = rc + 6;
-            __syncthreads();
-            if (tid < nsrc) {
-                const int y = t0 + tid;
-                x0r[tid] = rint_i((M[1] * y + M[2]) * kAbScale) + kRoundDelta;
-                y0r[tid] = rint_i((M[4] * y + M[5]) * kAbScale) + kRoundDelta;
-            }
-            // template rows -> LDS (dword loads, bytes beyond tw zeroed)
-            const int twd = L.TBp >> 2;
-            for (int r = 0; r < rc; ++r) {
-                const uint8_t* trow = a.tmpl + (size_t)(t0 + r) * a.tp;
-                for (int c = tid; c < twd; c += 256) {
-                    uint32_t wv = 0;
-                    if (4 * c < tw) {
-                        wv = *(const uint32_t*)(trow + 4 * c);
-                        const int valid = tw - 4 * c;
-                        if (valid < 4) wv &= (1u << (8 * valid)) - 1u;
-                    }
-                    *(uint32_t*)(TB + (size_t)r * L.TBp + 4 * c) = wv;
-                }
-            }
-            __syncthreads();
-            // sample the ROI rows (getRotatedROI -> warpAffine, border 0)
-            for (int r = 0; r < nsrc; ++r) {
-                uint8_t* sbr = SB + (size_t)r * L.SBp;
-                const int X0 = x0r[r], Y0 = y0r[r];
-                for (int c = tid; c < L.SBp; c += 256) {
-                    int v = 0;
-                    if (c < RW) {
-                        const int X = (X0 + ad[c]) >> (kAbBits - kInterBits);
-                        const int Y = (Y0 + bd[c]) >> (kAbBits - kInterBits);
-                        v = warp_tap(lvl, a.W, a.H, a.P, X, Y, 0);
-                    }
-                    sbr[c] = (uint8_t)v;
-                }
-            }
-            __syncthreads();
-            // full-row sums of I and I^2 (one wave per row)
-            for (int r = wave; r < nsrc; r += 4) {
-                const uint8_t* sbr = SB + (size_t)r * L.SBp;
-                int s1 = 0, s2 = 0;
-                for (int c = lane; c < RW; c += 64) { const int v = sbr[c]; s1 += v; s2 += v * v; }
-                for (int off = 32; off > 0; off >>= 1) { s1 += __shfl_xor(s1, off); s2 += __shfl_xor(s2, off); }
-                if (lane == 0) { rall[r] = s1; rallq[r] = s2; }
-            }
-            // per-row dot products: thread = (template row tl, offset dy), 7 dx accumulators
-            {
-                const int tl = tid & 31, dy = tid >> 5;
-                if (dy < 7 && tl < rc) {
-                    const uint32_t* trw = (const uint32_t*)(TB + (size_t)tl * L.TBp);
-                    const uint32_t* srw = (const uint32_t*)(SB + (size_t)(tl + dy) * L.SBp);
-                    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0, c5 = 0, c6 = 0;
-                    uint32_t wa = srw[0], wb = srw[1];
-#pragma unroll 4
-                    for (int k = 0; k < L.ntw; ++k) {
-                        const uint32_t wc = srw[k + 2], t = trw[k];
-                        c0 = __builtin_amdgcn_udot4(t, wa, c0, false);
-                        c1 = __builtin_amdgcn_udot4(t, __builtin_amdgcn_alignbyte(wb, wa, 1), c1, false);
-                        c2 = __builtin_amdgcn_udot4(t, __builtin_amdgcn_alignbyte(wb, wa, 2), c2, false);
-                        c3 = __builtin_amdgcn_udot4(t, __builtin_amdgcn_alignbyte(wb, wa, 3), c3, false);
-                        c4 = __builtin_amdgcn_udot4(t, wb, c4, false);
-                        c5 = __builtin_amdgcn_udot4(t, __builtin_amdgcn_alignbyte(wc, wb, 1), c5, false);
-                        c6 = __builtin_amdgcn_udot4(t, __builtin_amdgcn_alignbyte(wc, wb, 2), c6, false);
-                        wa = wb;
-                        wb = wc;
-                    }
-                    uint32_t* o = rs + tl * 49 + dy * 7;
-                    o[0] = c0; o[1] = c1; o[2] = c2; o[3] = c3; o[4] = c4; o[5] = c5; o[6] = c6;
-                }
-            }
-            __syncthreads();
-            // fold in template-row order + exact window sums
-            if (tid < 49) {
-                for (int tl = 0; tl < rc; ++tl) {
-                    const uint32_t v = rs[tl * 49 + tid];
-                    if (a.fold) accF = accF + (float)(int)v;
-                    else accI += v;
-                    const int r = tl + pdy;
-                    const uint8_t* sbr = SB + (size_t)r * L.SBp;
-                    int s1 = rall[r], s2 = rallq[r];
-                    for (int c = 0; c < pdx; ++c) { const int q = sbr[c]; s1 -= q; s2 -= q * q; }
-                    for (int c = pdx + tw; c < RW; ++c) { const int q = sbr[c]; s1 -= q; s2 -= q * q; }
-                    sumI += s1;
-                    sumQ += s2;
-                }
-            }
-        }
         if (tid < 49) {
+            const uint32_t* rs = a.rowsum + (size_t)slot * a.th * 49 + tid;
+            float accF = 0.f;
+            uint64_t accI = 0;
+            int t = 0;
+            if (a.fold) {
+                for (; t + 8 <= a.th; t += 8) {
+                    uint32_t v[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) v[u] = rs[(size_t)(t + u) * 49];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) accF = accF + (float)(int)v[u];   // :507, row order
+                }
+                for (; t < a.th; ++t) accF = accF + (float)(int)rs[(size_t)t * 49];
+            } else {
+                for (; t < a.th; ++t) accI += rs[(size_t)t * 49];
+            }
+            uint64_t s1 = 0, s2 = 0;
+            for (int c = 0; c < a.nchunk; ++c) {
+                s1 += a.wsum[((size_t)slot * a.nchunk + c) * 49 + tid];
+                s2 += a.wsq[((size_t)slot * a.nchunk + c) * 49 + tid];
+            }
             const double num = a.fold ? (double)accF : (double)(float)(double)accI;
-            sc[tid] = ccoeff(num, (double)sumI, (double)sumQ, a.mean, a.norm, a.inv_area);
+            sc[tid] = ccoeff(num, (double)s1, (double)s2, a.mean, a.norm, a.inv_area);
         }
         __syncthreads();
         if (tid == 0) {
@@ -564,16 +824,37 @@ __global__ __launch_bounds__(256) void k_roi_corr(RoiArgs a) {
     }
 }
 
-void launch_roi_corr(const RoiArgs& a, int max_items, hipStream_t st) {
-    if (max_items <= 0) return;
-    const size_t lds = roi_lds_bytes(a.tw, a.th, a.rc);
+void launch_roi_tables(const RoiArgs& a, hipStream_t st) {
+    if (a.slot_cap <= 0 || a.equal1) return;
+    const int grid = a.slot_cap < 2048 ? a.slot_cap : 2048;
+    hipLaunchKernelGGL(k_roi_tables, dim3(grid), dim3(256), 0, st, a);
+}
+
+void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
+    if (a.slot_cap <= 0 || a.equal1) return;
+    const long tiles = (long)a.slot_cap * ((a.th + 6 + ROI_T - 1) / ROI_T) * ((a.tw + 6 + ROI_T - 1) / ROI_T);
+    const long want = (tiles + 3) / 4;
+    const int grid = (int)(want < 16384 ? want : 16384);
+    hipLaunchKernelGGL(k_roi_warp, dim3(grid), dim3(256), 0, st, a);
+}
+
+void launch_roi_corr(const RoiArgs& a, hipStream_t st) {
+    if (a.slot_cap <= 0 || a.equal1) return;
+    const size_t lds = roi_corr_lds(a.roi_pitch, a.tw, a.rc);
     static size_t lds_attr = 0;
     if (lds > 65536 && lds > lds_attr) {
         (void)hipFuncSetAttribute((const void*)k_roi_corr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         lds_attr = lds;
     }
-    int grid = max_items < 4096 ? max_items : 4096;
+    const long items = (long)a.slot_cap * a.nchunk;
+    const int grid = (int)(items < 8192 ? items : 8192);
     hipLaunchKernelGGL(k_roi_corr, dim3(grid), dim3(256), lds, st, a);
+}
+
+void launch_roi_eval(const RoiArgs& a, hipStream_t st) {
+    if (a.slot_cap <= 0) return;
+    const int grid = a.slot_cap < 4096 ? a.slot_cap : 4096;
+    hipLaunchKernelGGL(k_roi_eval, dim3(grid), dim3(64), 0, st, a);
 }
 
 // ============================================================================================== step

@@ -131,14 +131,15 @@ int fpm_search_stats(const fpm_ctx* ctx, int64_t* stats, int32_t cap);
 /* Kernel timing: when enabled, HIP events bracket every launch of each kernel family on the context's
  * stream; fpm_profile_get returns total milliseconds, launch count and algorithmic bytes moved (inputs +
  * outputs, u8 = 1 B, f32 = 4 B) accumulated since the last reset. */
-#define FPM_K_PYR 0        /* K1 pyrDown                                */
-#define FPM_K_TOP_WARP 1   /* K2 top-layer rotation                     */
-#define FPM_K_TOP_NCC 2    /* K3+K4 top-layer CCORR + normalisation     */
-#define FPM_K_TOP_NMS 3    /* K5 peak extraction                        */
-#define FPM_K_ROI_WARP 4   /* K6 refinement ROI rotation                */
-#define FPM_K_ROI_CORR 5   /* K7 refinement ROI correlation             */
-#define FPM_K_ROI_EVAL 6   /* K8 fold + normalise + argmax + decision   */
-#define FPM_K_COUNT 7
+#define FPM_K_PYR 0        /* K1 pyrDown                                                   */
+#define FPM_K_TOP_WARP 1   /* K2 top-layer rotation                                        */
+#define FPM_K_TOP_NCC 2    /* K3+K4 top-layer CCORR + normalisation                        */
+#define FPM_K_TOP_NMS 3    /* K5 peak extraction                                           */
+#define FPM_K_ROI_WARP 4   /* K6 refinement ROI tables + LDS-staged bilinear sampling      */
+#define FPM_K_ROI_CORR 5   /* K7 refinement per-row int32 correlation + window sums        */
+#define FPM_K_ROI_EVAL 6   /* K8 row fold + normalisation + argmax + 3x3                   */
+#define FPM_K_CAND 7       /* candidate init / best-of-3 / early break / back-mapping      */
+#define FPM_K_COUNT 8
 int fpm_profile_enable(fpm_ctx* ctx, int32_t enable);
 int fpm_profile_reset(fpm_ctx* ctx);
 int fpm_profile_get(const fpm_ctx* ctx, int32_t kernel, double* total_ms, int64_t* launches,
