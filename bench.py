@@ -32,6 +32,35 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# kernels of each profiled family (fpm_profile_* families, include/fpm.h FPM_K_*)
+FAMILY_KERNELS = {"pyr_down": ["k_pyr_down"], "top_warp": ["k_warp"], "top_ncc": ["k_ncc_map"], "top_nms": ["k_nms"],
+                  "roi_warp": ["k_roi_tables", "k_roi_warp"], "roi_corr": ["k_roi_corr"], "roi_eval": ["k_roi_eval"],
+                  "cand": ["k_cand_init", "k_cand_step"]}
+TRAFFIC_CSV = os.path.join(REPO, "profiles", "latest", "pmc_traffic.csv")
+
+
+def pmc_traffic(family):
+    """HBM bytes per launch of `family` from the committed PMC summary (scripts/pmc_bench.sh: separate FETCH_SIZE /
+    WRITE_SIZE passes over this same bench command, FETCH_SIZE doubled for gfx950); None if not collected."""
+    import csv
+
+    if not os.path.exists(TRAFFIC_CSV):
+        return None
+    per = {}
+    with open(TRAFFIC_CSV) as fh:
+        for row in csv.DictReader(fh):
+            if row["counter"].startswith(("FETCH_BYTES", "WRITE_BYTES")):
+                per.setdefault(row["kernel"], 0.0)
+                per[row["kernel"]] += float(row["mean_per_dispatch"])
+    tot, found = 0.0, False
+    for k in FAMILY_KERNELS.get(family, []):
+        for name, v in per.items():
+            if name.startswith(f"fpm::{k}(") or name.startswith(f"void fpm::{k}<"):
+                tot += v
+                found = True
+    return int(tot) if found else None
+
+
 def make_sources(templ, n, seed0):
     from fastest_image_pattern_matching_amd import synth
 
@@ -117,7 +146,15 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    n_matches = [len(r) for r in res]
+    # the report exchange of the sharded path (sharding.gather_results; outside the timed region)
+    if dist is not None:
+        from fastest_image_pattern_matching_amd import sharding
+
+        full = sharding.gather_results([[r.as_tuple() for r in rr] for rr in res], world * args.batch, cap=64,
+                                       device=torch.device("cuda", local))
+        n_matches = [len(r) for r in full]
+    else:
+        n_matches = [len(r) for r in res]
 
     # kernel-level pass with HIP events around every launch
     m.profile(True)
@@ -136,7 +173,7 @@ def main():
     bytes_per_launch = d["bytes"] / d["launches"]
     achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": dom,
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic(dom), "kernel": dom,
                 "avg_launch_us": round(avg_s * 1e6, 3), "algorithmic_bytes_per_launch": int(bytes_per_launch)}
 
     searches = world * args.batch * args.steps

@@ -1,0 +1,98 @@
+"""Multi-GPU layer: one process per GPU, sources sharded across ranks (batch config).
+
+Every source image is an independent ``TemplateMatcher::match`` call (TemplateMatcher.cpp:97-437), so the path
+partitions by source with no data-path collective: rank r searches the contiguous slice
+``shard_range(n, world, r)`` of the batch on its own GPU.  The only exchange is the final report — one
+``all_gather`` of fixed-capacity result blocks (12 f64 per s_SingleTargetMatch, DataStructures.h:97-115) so
+every rank (or just rank 0) can assemble the per-source result lists in the original source order.
+
+The exchange works with any torch.distributed backend: ``nccl`` (RCCL over xGMI, tensors on the rank's GPU)
+on the MI355X node and ``gloo`` (CPU tensors) in the CPU tests.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+FIELDS = 12   # lt, rt, rb, lb, center (x, y each), angle, score
+
+
+def shard_range(n: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous block split of n sources over `world` ranks; the first n % world ranks get one extra."""
+    if world <= 0 or not (0 <= rank < world) or n < 0:
+        raise ValueError(f"bad shard request n={n} world={world} rank={rank}")
+    q, r = divmod(n, world)
+    start = rank * q + min(rank, r)
+    return start, start + q + (1 if rank < r else 0)
+
+
+def shard_sizes(n: int, world: int) -> List[int]:
+    return [b - a for a, b in (shard_range(n, world, k) for k in range(world))]
+
+
+def pack_results(per_source: Sequence[Sequence[Sequence[float]]], slots: int, cap: int) -> np.ndarray:
+    """Pack up to `slots` per-source result lists (each result a 12-tuple) into a [slots, 1 + cap*12] f64
+    block: column 0 = result count, then `cap` zero-padded results.  Raises if a source has > cap results."""
+    block = np.zeros((slots, 1 + cap * FIELDS), dtype=np.float64)
+    if len(per_source) > slots:
+        raise ValueError(f"{len(per_source)} sources do not fit {slots} slots")
+    for i, res in enumerate(per_source):
+        if len(res) > cap:
+            raise ValueError(f"source {i}: {len(res)} results exceed capacity {cap}")
+        block[i, 0] = len(res)
+        for j, r in enumerate(res):
+            if len(r) != FIELDS:
+                raise ValueError(f"result must have {FIELDS} fields, got {len(r)}")
+            block[i, 1 + j * FIELDS:1 + (j + 1) * FIELDS] = r
+    return block
+
+
+def unpack_results(block: np.ndarray, count: int) -> List[List[Tuple[float, ...]]]:
+    out = []
+    cap = (block.shape[1] - 1) // FIELDS
+    for i in range(count):
+        k = int(block[i, 0])
+        if not 0 <= k <= cap:
+            raise ValueError(f"corrupt result block: count {k} > cap {cap}")
+        out.append([tuple(float(v) for v in block[i, 1 + j * FIELDS:1 + (j + 1) * FIELDS]) for j in range(k)])
+    return out
+
+
+def gather_results(local: Sequence[Sequence[Sequence[float]]], n_total: int, cap: int, group=None,
+                   device=None) -> List[List[Tuple[float, ...]]]:
+    """all_gather every rank's shard of results; returns the full per-source list (source order) on every rank.
+
+    `local` holds the results of this rank's shard_range(n_total, world, rank) sources, in order.  Blocks are
+    padded to the largest shard so one fixed-size collective suffices (KB-scale: latency-bound over xGMI)."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    sizes = shard_sizes(n_total, world)
+    if len(local) != sizes[rank]:
+        raise ValueError(f"rank {rank} holds {len(local)} results, its shard has {sizes[rank]} sources")
+    slots = max(max(sizes), 1)
+    mine = torch.from_numpy(pack_results(local, slots, cap))
+    if device is not None:
+        mine = mine.to(device)
+    parts = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(parts, mine, group=group)
+    full: List[List[Tuple[float, ...]]] = []
+    for k in range(world):
+        full.extend(unpack_results(parts[k].cpu().numpy(), sizes[k]))
+    return full
+
+
+def match_sharded(matcher, sources: Sequence[np.ndarray], cap: int = 256, group=None, device=None):
+    """Search this rank's slice of `sources` with `matcher` (a TemplateMatcher bound to this rank's GPU) and
+    return every source's results, in source order, on every rank."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    a, b = shard_range(len(sources), world, rank)
+    mine = matcher.match_batch(list(sources[a:b])) if b > a else []
+    local = [[r.as_tuple() for r in res] for res in mine]
+    return gather_results(local, len(sources), cap, group=group, device=device)
