@@ -65,6 +65,9 @@ struct PinBuf {
 struct TmplLevel {
     int w, h, pitch;
     size_t off;              // offset in the device template slab
+    size_t off8;             // offset in the i8 template slab (T ^ 0x80, zero padded; MFMA A operand)
+    int p8;                  // its row pitch: 64 * ceil(w / 64)
+    size_t tsum_off;         // offset (elements) of the per-row sums in d_tsum
     double mean, norm, inv_area;
     bool equal1;
     std::vector<uint8_t> px; // host copy (dense)
@@ -96,8 +99,8 @@ struct Plan {
     int max_canvas = 0, max_map = 0;
     // device buffers owned by the plan
     DevBuf d_canvas, d_map, d_bmax, d_bloc, d_jobs, d_nodes, d_top, d_topn, d_peaks, d_counts, d_state,
-        d_live, d_livecnt, d_rec, d_rowsum, d_wsum, d_wsq, d_tab, d_roi;
-    int tabw = 0, tabh = 0, roi_pitch = 0;
+        d_live, d_livecnt, d_rec, d_rowsum, d_wsum, d_wsq, d_tab, d_roi, d_tdesc;
+    int tabw = 0, tabh = 0, roi_pitch = 0, tdesc_stride = 1;
     size_t roi_stride = 0;
     int slot_cap = 0;                          // ROIs per refinement round (bounded scratch)
     size_t off_warp = 0, off_ncc = 0, off_nms = 0;
@@ -105,7 +108,7 @@ struct Plan {
     size_t h_counts = 0, h_peaks = 0, h_state = 0, h_rec = 0, h_live = 0, h_total = 0;
     void release() {
         for (DevBuf* b : {&d_canvas, &d_map, &d_bmax, &d_bloc, &d_jobs, &d_nodes, &d_top, &d_topn, &d_peaks,
-                          &d_counts, &d_state, &d_live, &d_livecnt, &d_rec, &d_rowsum, &d_wsum, &d_wsq, &d_tab, &d_roi})
+                          &d_counts, &d_state, &d_live, &d_livecnt, &d_rec, &d_rowsum, &d_wsum, &d_wsq, &d_tab, &d_roi, &d_tdesc})
             b->release();
         h_out.release();
         valid = false;
@@ -130,7 +133,7 @@ struct fpm_ctx {
     bool learned = false;
     int border = 0;
     std::vector<TmplLevel> tmpl;
-    DevBuf d_tmpl;
+    DevBuf d_tmpl, d_tmpl8, d_tsum;
     uint64_t tmpl_gen = 0;
     // staged sources
     int S = 0, sw = 0, sh = 0, src_L = -1;
@@ -387,7 +390,9 @@ int build_plan(fpm_ctx* ctx) {
     {   // refinement scratch per ROI (tables, sampled ROI, row sums, window partials); bounded, rounds cover the rest
         size_t max_rows = 1, max_chunks = 1;
         int max_w = 1;
+        P.tdesc_stride = 1;
         for (int l = 0; l < L; ++l) {
+            P.tdesc_stride = std::max(P.tdesc_stride, roi_tiles_for(ctx->tmpl[l].w, ctx->tmpl[l].h));
             const int rc = roi_pick_rc(ctx->tmpl[l].w, ctx->tmpl[l].h);
             max_rows = std::max(max_rows, (size_t)ctx->tmpl[l].h);
             max_chunks = std::max(max_chunks, (size_t)(ctx->tmpl[l].h + rc - 1) / rc);
@@ -397,14 +402,15 @@ int build_plan(fpm_ctx* ctx) {
         P.tabw = P.roi_pitch;
         P.tabh = round_up((int)max_rows + 6, 4);
         P.roi_stride = round_up((size_t)P.roi_pitch * (max_rows + 6 + 1), (size_t)256);
-        const size_t per_roi = sizeof(int32_t) * 2 * (P.tabw + P.tabh) + P.roi_stride + max_rows * 49 * 4 +
+        const size_t per_roi = sizeof(int32_t) * 2 * (P.tabw + P.tabh) + sizeof(int4) * P.tdesc_stride + P.roi_stride + max_rows * 49 * 4 +
                                max_chunks * 49 * 12;
         const size_t budget = (size_t)16 << 30;   // of 288 GB HBM; rounds only beyond this
         const size_t want = (size_t)P.C * P.n3;
         P.slot_cap = (int)std::max<size_t>(1, std::min(want, budget / per_roi));
         HIP_TRY(P.d_tab.ensure((size_t)P.slot_cap * 2 * (P.tabw + P.tabh) * sizeof(int32_t)));
+        HIP_TRY(P.d_tdesc.ensure((size_t)P.slot_cap * P.tdesc_stride * sizeof(int4)));
         HIP_TRY(P.d_roi.ensure((size_t)P.slot_cap * P.roi_stride));
-        HIP_TRY(P.d_rowsum.ensure((size_t)P.slot_cap * max_rows * 49 * 4));
+        HIP_TRY(P.d_rowsum.ensure((size_t)P.slot_cap * round_up(max_rows * 49, (size_t)4) * 4));
         HIP_TRY(P.d_wsum.ensure((size_t)P.slot_cap * max_chunks * 49 * 4));
         HIP_TRY(P.d_wsq.ensure((size_t)P.slot_cap * max_chunks * 49 * 8));
     }
@@ -562,6 +568,8 @@ int enqueue_search(fpm_ctx* ctx) {
         ra.level = dsrc + lv.off; ra.level_stride = lv.img_bytes;
         ra.W = lv.w; ra.H = lv.h; ra.P = lv.pitch;
         ra.tmpl = ctx->d_tmpl.as<uint8_t>() + tl.off; ra.tw = tl.w; ra.th = tl.h; ra.tp = tl.pitch;
+        ra.tmpl8 = ctx->d_tmpl8.as<int8_t>() + tl.off8; ra.tp8 = tl.p8; ra.nk = (tl.w + 63) / 64;
+        ra.tsum = ctx->d_tsum.as<int32_t>() + tl.tsum_off;
         ra.n3 = P.n3;
         ra.rc = roi_pick_rc(tl.w, tl.h);
         ra.nchunk = (tl.h + ra.rc - 1) / ra.rc;
@@ -574,6 +582,7 @@ int enqueue_search(fpm_ctx* ctx) {
         ra.state = P.d_state.as<CandState>();
         ra.nodes = P.d_nodes.as<AngleNode>() + P.node_off[d];
         ra.tab = P.d_tab.as<int32_t>(); ra.tabw = P.tabw; ra.tabh = P.tabh;
+        ra.tdesc = P.d_tdesc.as<int4>(); ra.tdesc_stride = P.tdesc_stride;
         ra.roi = P.d_roi.as<uint8_t>(); ra.roi_pitch = P.roi_pitch; ra.roi_stride = P.roi_stride;
         ra.rowsum = P.d_rowsum.as<uint32_t>();
         ra.wsum = P.d_wsum.as<uint32_t>();
@@ -832,7 +841,7 @@ int fpm_destroy(fpm_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     ctx->plan.release();
-    ctx->d_tmpl.release(); ctx->d_src.release();
+    ctx->d_tmpl.release(); ctx->d_tmpl8.release(); ctx->d_tsum.release(); ctx->d_src.release();
     ctx->d_op_a.release(); ctx->d_op_b.release(); ctx->d_op_job.release();
     for (auto& k : ctx->kp)
         for (auto& e : k.ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
@@ -900,6 +909,33 @@ int fpm_learn(fpm_ctx* ctx, const uint8_t* gray, int32_t w, int32_t h, size_t st
         norm = std::sqrt(norm);
         norm /= std::sqrt(inv_area);
         lv[l].mean = mean; lv[l].norm = norm; lv[l].inv_area = inv_area;
+    }
+    {   // MFMA operand copies: T ^ 0x80 (= T - 128 as i8), zero beyond the template; per-row sums of T
+        size_t o8 = 0, os = 0;
+        for (int l = 0; l <= L; ++l) {
+            lv[l].p8 = 64 * ((lv[l].w + 63) / 64);
+            lv[l].off8 = o8;
+            o8 += (size_t)lv[l].p8 * round_up(lv[l].h, kMmaRows);
+            lv[l].tsum_off = os;
+            os += round_up(lv[l].h, kMmaRows);
+        }
+        o8 += 64;   // slack: k_roi_corr prefetches one 64-byte block past a row's last
+        std::vector<int8_t> h8(o8, 0);
+        std::vector<int32_t> hs(os, 0);
+        for (int l = 0; l <= L; ++l)
+            for (int y = 0; y < lv[l].h; ++y) {
+                int32_t sum = 0;
+                for (int x = 0; x < lv[l].w; ++x) {
+                    const uint8_t v = lv[l].px[(size_t)y * lv[l].w + x];
+                    h8[lv[l].off8 + (size_t)y * lv[l].p8 + x] = (int8_t)(v ^ 0x80);
+                    sum += v;
+                }
+                hs[lv[l].tsum_off + y] = sum;
+            }
+        HIP_TRY(ctx->d_tmpl8.ensure(o8));
+        HIP_TRY(ctx->d_tsum.ensure(os * sizeof(int32_t)));
+        HIP_TRY(hipMemcpy(ctx->d_tmpl8.p, h8.data(), o8, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(ctx->d_tsum.p, hs.data(), os * sizeof(int32_t), hipMemcpyHostToDevice));
     }
     ctx->tmpl = std::move(lv);
     ctx->learned = true;

@@ -89,6 +89,10 @@ struct RoiArgs {
     int32_t W, H, P;         // level size and pitch
     const uint8_t* tmpl;     // template level
     int32_t tw, th, tp;
+    const int8_t* tmpl8;     // template level as i8 (T ^ 0x80), zero beyond tw / th: [round_up(th,16)][tp8]
+    int32_t tp8;             // its row pitch (multiple of 64)
+    int32_t nk;              // ceil(tw / 64): MFMA k-steps per row
+    const int32_t* tsum;     // per template row: sum of T (u8)
     int32_t n3;              // refinement angles per candidate (1 or 3)
     int32_t rc;              // template rows per correlation chunk
     int32_t nchunk;          // ceil(th / rc)
@@ -104,6 +108,8 @@ struct RoiArgs {
     const AngleNode* nodes;  // level nodes; child = parent * n3 + j
     int32_t* tab;            // [slot] fixed-point warp tables: ad[tabw], bd[tabw], x0[tabh], y0[tabh]
     int32_t tabw, tabh;
+    int4* tdesc;             // [slot][tdesc_stride] per 32x32 ROI tile: source footprint box + flags
+    int32_t tdesc_stride;
     uint8_t* roi;            // [slot] sampled ROI, (th+6) rows x roi_pitch bytes
     int32_t roi_pitch;
     size_t roi_stride;
@@ -141,6 +147,8 @@ void launch_roi_eval(const RoiArgs& a, hipStream_t st);
 void launch_cand_step(const StepArgs& a, int max_items, hipStream_t st);
 int roi_pick_rc(int tw, int th);
 int roi_pitch_for(int tw);
+int roi_tiles_for(int tw, int th);   // 32x32 warp tiles of a (tw+6) x (th+6) ROI
 size_t roi_corr_lds(int roi_pitch, int tw, int rc);
+constexpr int kMmaRows = 16;   // template rows per MFMA correlation chunk (M of v_mfma_i32_16x16x64_i8)
 
 }  // namespace fpm

@@ -434,29 +434,34 @@ void launch_cand_init(const CandInitArgs& a, hipStream_t st) {
 //   k_roi_corr    per (ROI, 16 template rows): exact int32 row dot products for all 49 offsets + window sums
 //   k_roi_eval    per ROI: ordered f32 fold (:505-508), f64 CCOEFF normalisation, argmax, border, 3x3
 // ---- geometry of the refinement scratch ----------------------------------------------------------------------
-constexpr int ROI_RC = 16;           // template rows per correlation chunk
+constexpr int ROI_RC = kMmaRows;     // template rows per correlation chunk
 constexpr int ROI_T = 32;            // warp tile: 32 x 32 ROI pixels per wave task
 constexpr int ROI_FT = 4096;         // per-wave LDS footprint buffer (bytes) >= worst-case rotated tile bbox
 
 int roi_pick_rc(int /*tw*/, int th) { return th < ROI_RC ? th : ROI_RC; }
 
-// ROI row pitch: >= RW + 16 (look-ahead words of the correlation), pitch/4 = 4 * odd (conflict-free b128 reads)
+// ROI row pitch: >= RW + 16 (look-ahead of the 16-byte B reads at shift <= 6) and >= 64*ceil(tw/64) + 22 (the
+// MFMA k range), pitch/16 odd (spreads the LDS banks of row-strided 16-byte reads)
 __host__ __device__ inline int roi_pitch_calc(int tw) {
-    int q = ((tw + 6 + 16) + 15) / 16;  // in 16-byte units
+    const int need_a = tw + 6 + 16, need_b = 64 * ((tw + 63) / 64) + 22;
+    int q = ((need_a > need_b ? need_a : need_b) + 15) / 16;   // in 16-byte units
     if ((q & 1) == 0) ++q;
     return q * 16;
 }
 int roi_pitch_for(int tw) { return roi_pitch_calc(tw); }
 
-__host__ __device__ inline int tmpl_pitch_calc(int tw) {   // template LDS rows: >= 4*ceil(tw/4) + 16, same rule
-    int q = ((((tw + 3) / 4) * 4 + 16) + 15) / 16;
+// LDS row pitch of the staged i8 template rows: >= tp8, pitch/16 odd (conflict-free row-strided b128 reads)
+__host__ __device__ inline int tmpl_lds_pitch(int tp8) {
+    int q = tp8 / 16;
     if ((q & 1) == 0) ++q;
     return q * 16;
 }
 
-size_t roi_corr_lds(int roi_pitch, int tw, int rc) {
-    return (size_t)(rc + 6) * roi_pitch + (size_t)(rc + 12) * tmpl_pitch_calc(tw) +
-           sizeof(uint32_t) * (rc * 49 + 2 * (rc + 6) + 2 * 7 * (rc + 6)) + 64;
+size_t roi_corr_lds(int roi_pitch, int tw, int /*rc*/) {
+    constexpr int src_rows = 2 * kMmaRows + 6;
+    const int tp8 = 64 * ((tw + 63) / 64);
+    return (size_t)src_rows * roi_pitch + (size_t)2 * kMmaRows * tmpl_lds_pitch(tp8) +
+           sizeof(uint32_t) * (2 * src_rows + 2 * 7 * src_rows) + 64;
 }
 
 // bilinear tap from global memory (fallback when a footprint does not fit the LDS buffer);
@@ -503,9 +508,22 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// ---- K6a: per-ROI fixed-point warp tables (getRotatedROI -> warpAffine's adelta/bdelta/X0/Y0) ----------------
+// ---- K6a: per-ROI fixed-point warp tables (getRotatedROI -> warpAffine's adelta/bdelta/X0/Y0) and, from them,
+// one descriptor per 32x32 ROI tile: the tile's source footprint box (corner samples +-1 px: the fixed-point map
+// is two roundings of a linear map, so every pixel's tap lies within the corners' range +-1) and flags
+// (bit0: footprint non-empty, bit1: fits the per-wave LDS buffer, bit2: every tap inside the image).
+constexpr int kTileAny = 1, kTileLds = 2, kTileInterior = 4;
+int roi_tiles_for(int tw, int th) { return ((tw + 6 + ROI_T - 1) / ROI_T) * ((th + 6 + ROI_T - 1) / ROI_T); }
+
 __global__ __launch_bounds__(256) void k_roi_tables(RoiArgs a) {
+    extern __shared__ int32_t tl[];   // ad[tabw] bd[tabw] x0[tabh] y0[tabh]
     const int rois = roi_count(a);
+    const int RW = a.tw + 6, RH = a.th + 6, W = a.W, H = a.H;
+    const int txn = (RW + ROI_T - 1) / ROI_T, tyn = (RH + ROI_T - 1) / ROI_T;
+    int32_t* lad = tl;
+    int32_t* lbd = lad + a.tabw;
+    int32_t* lx0 = lbd + a.tabw;
+    int32_t* ly0 = lx0 + a.tabh;
     for (int slot = blockIdx.x; slot < rois; slot += gridDim.x) {
         int id, jj;
         roi_slot(a, slot, id, jj);
@@ -514,260 +532,349 @@ __global__ __launch_bounds__(256) void k_roi_tables(RoiArgs a) {
         double M[6];
         roi_matrix(a.W, a.H, f2(st.lt.x * 2, st.lt.y * 2), nd.c, nd.s, M);
         int32_t* t = a.tab + (size_t)slot * 2 * (a.tabw + a.tabh);
+        __syncthreads();   // previous slot's descriptors are done with the LDS tables
         for (int x = threadIdx.x; x < a.tabw; x += 256) {
-            t[x] = rint_i(M[0] * x * kAbScale);
-            t[a.tabw + x] = rint_i(M[3] * x * kAbScale);
+            const int ad = rint_i(M[0] * x * kAbScale), bd = rint_i(M[3] * x * kAbScale);
+            t[x] = ad; t[a.tabw + x] = bd;
+            lad[x] = ad; lbd[x] = bd;
         }
         for (int y = threadIdx.x; y < a.tabh; y += 256) {
-            t[2 * a.tabw + y] = rint_i((M[1] * y + M[2]) * kAbScale) + kRoundDelta;
-            t[2 * a.tabw + a.tabh + y] = rint_i((M[4] * y + M[5]) * kAbScale) + kRoundDelta;
+            const int x0 = rint_i((M[1] * y + M[2]) * kAbScale) + kRoundDelta;
+            const int y0 = rint_i((M[4] * y + M[5]) * kAbScale) + kRoundDelta;
+            t[2 * a.tabw + y] = x0; t[2 * a.tabw + a.tabh + y] = y0;
+            lx0[y] = x0; ly0[y] = y0;
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < txn * tyn; i += 256) {
+            const int ty = i / txn, tx = i - ty * txn;
+            const int cx0 = tx * ROI_T, cx1 = min(cx0 + ROI_T, RW) - 1;
+            const int ry0 = ty * ROI_T, ry1 = min(ry0 + ROI_T, RH) - 1;
+            int bx0 = INT_MAX, bx1 = INT_MIN, by0 = INT_MAX, by1 = INT_MIN;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int c = (k & 1) ? cx1 : cx0, r = (k & 2) ? ry1 : ry0;
+                const int X = (lx0[r] + lad[c]) >> (kAbBits - kInterBits);
+                const int Y = (ly0[r] + lbd[c]) >> (kAbBits - kInterBits);
+                bx0 = min(bx0, X >> kInterBits); bx1 = max(bx1, X >> kInterBits);
+                by0 = min(by0, Y >> kInterBits); by1 = max(by1, Y >> kInterBits);
+            }
+            const bool interior = bx0 - 1 >= 0 && bx1 + 1 <= W - 2 && by0 - 1 >= 0 && by1 + 1 <= H - 2;
+            bx0 = max(bx0 - 1, 0); by0 = max(by0 - 1, 0);
+            bx1 = min(bx1 + 2, W - 1); by1 = min(by1 + 2, H - 1);
+            const bool any = bx0 <= bx1 && by0 <= by1;
+            const int bxa = bx0 & ~3;
+            int ftw = any ? ((bx1 - bxa + 4) & ~3) : 0;
+            if (((ftw >> 2) & 1) == 0) ftw += 4;    // odd dword pitch: spread gather banks
+            const int fth = any ? by1 - by0 + 1 : 0;
+            const bool in_lds = (ftw >> 2) <= 16 && ftw * fth <= ROI_FT;
+            a.tdesc[(size_t)slot * a.tdesc_stride + i] =
+                make_int4(bxa, by0, ftw | (fth << 16),
+                          (any ? kTileAny : 0) | (in_lds ? kTileLds : 0) | (interior ? kTileInterior : 0));
         }
     }
 }
 
-// ---- K6b: ROI sampling.  One wave = one 32x32 ROI tile: the tile's source footprint (bounding box of the
-// rotated tile, clipped to the image) is staged into wave-private LDS with aligned dword loads, then every lane
-// produces 4 rows x 4 pixels by gathering the bilinear taps from LDS and stores them as dwords.  No workgroup
-// barrier; full occupancy.  Border pixels follow remapBilinear's BORDER_CONSTANT(0) rules exactly.
+// ---- K6b: ROI sampling.  One wave = one 32x32 ROI tile: its descriptor and the lane's table entries are loaded
+// together; the tile's source footprint is staged into wave-private LDS with dword loads; every lane produces
+// 4 rows x 4 pixels by gathering the bilinear taps from LDS and stores them as dwords.  Interior tiles take a
+// branch-free path; others follow remapBilinear's BORDER_CONSTANT(0) rules per pixel.  No workgroup barrier.
 __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t ft_all[4][ROI_FT];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint8_t* FT = ft_all[wv];
     const int RW = a.tw + 6, RH = a.th + 6, W = a.W, H = a.H;
     const int txn = (RW + ROI_T - 1) / ROI_T, tyn = (RH + ROI_T - 1) / ROI_T;
-    const int rois = roi_count(a);
-    const long tasks = (long)rois * tyn * txn;
+    const int per_roi = txn * tyn;
+    const int tasks = roi_count(a) * per_roi;
     const int lr = lane >> 3, lg = lane & 7;   // lane -> rows lr + 8i, columns 4*lg .. 4*lg+3
-    for (long task = (long)blockIdx.x * 4 + wv; task < tasks; task += (long)gridDim.x * 4) {
-        const int tx = (int)(task % txn);
-        const long q = task / txn;
-        const int ty = (int)(q % tyn);
-        const int slot = (int)(q / tyn);
+    for (int task = blockIdx.x * 4 + wv; task < tasks; task += gridDim.x * 4) {
+        const int slot = task / per_roi;
+        const int rem = task - slot * per_roi;
+        const int ty = rem / txn, tx = rem - ty * txn;
+        const int4 dsc = a.tdesc[(size_t)slot * a.tdesc_stride + rem];
+        const int32_t* t = a.tab + (size_t)slot * 2 * (a.tabw + a.tabh);
+        const int cx0 = tx * ROI_T, cx1 = min(cx0 + ROI_T, RW) - 1;
+        const int ry0 = ty * ROI_T, ry1 = min(ry0 + ROI_T, RH) - 1;
+        const int c0 = cx0 + 4 * lg;
+        const int cc = min(c0, cx1 & ~3);   // tables are read in bounds even for idle lanes
+        const int4 A = *(const int4*)(t + cc);
+        const int4 B = *(const int4*)(t + a.tabw + cc);
+        int X0r[4], Y0r[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = min(ry0 + lr + 8 * i, ry1);
+            X0r[i] = t[2 * a.tabw + r];
+            Y0r[i] = t[2 * a.tabw + a.tabh + r];
+        }
         int id, jj;
         roi_slot(a, slot, id, jj);
         const uint8_t* lvl = a.level + (size_t)(id / a.per_source) * a.level_stride;
-        const int32_t* t = a.tab + (size_t)slot * 2 * (a.tabw + a.tabh);
-        const int32_t* tad = t;
-        const int32_t* tbd = t + a.tabw;
-        const int32_t* tx0 = t + 2 * a.tabw;
-        const int32_t* ty0 = tx0 + a.tabh;
-        const int cx0 = tx * ROI_T, cx1 = min(cx0 + ROI_T, RW) - 1;
-        const int ry0 = ty * ROI_T, ry1 = min(ry0 + ROI_T, RH) - 1;
-        int bx0 = INT_MAX, bx1 = INT_MIN, by0 = INT_MAX, by1 = INT_MIN;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int c = (k & 1) ? cx1 : cx0, r = (k & 2) ? ry1 : ry0;
-            const int X = (tx0[r] + tad[c]) >> (kAbBits - kInterBits);
-            const int Y = (ty0[r] + tbd[c]) >> (kAbBits - kInterBits);
-            bx0 = min(bx0, X >> kInterBits); bx1 = max(bx1, X >> kInterBits);
-            by0 = min(by0, Y >> kInterBits); by1 = max(by1, Y >> kInterBits);
-        }
-        // +-1 px covers the per-pixel rounding of the fixed-point map, +1 the second tap; clip to the image
-        bx0 = max(bx0 - 1, 0); by0 = max(by0 - 1, 0);
-        bx1 = min(bx1 + 2, W - 1); by1 = min(by1 + 2, H - 1);
-        const bool any = bx0 <= bx1 && by0 <= by1;
-        const int bxa = bx0 & ~3;
-        int ftw = any ? ((bx1 - bxa + 4) & ~3) : 0;
-        if (((ftw >> 2) & 1) == 0) ftw += 4;    // odd dword pitch: spread gather banks
-        const int fth = any ? by1 - by0 + 1 : 0;
-        const bool in_lds = ftw * fth <= ROI_FT;
+        const int bxa = dsc.x, by0 = dsc.y, ftw = dsc.z & 0xffff, fth = dsc.z >> 16, flags = dsc.w;
+        const bool in_lds = (flags & kTileLds) != 0;
+        const int wpr = ftw >> 2;
         wave_sync();   // previous task's gathers are done with FT
-        if (any && in_lds) {
-            const int wpr = ftw >> 2;
-            for (int i = lane; i < wpr * fth; i += 64) {
-                const int r = i / wpr, c = i - r * wpr;
+        if ((flags & kTileAny) && in_lds) {   // lane -> word column lane & 15, rows (lane >> 4) + 4i
+            const int c = lane & 15;
+            if (c < wpr) {
                 const int gx = bxa + 4 * c;
-                *(uint32_t*)(FT + r * ftw + 4 * c) =
-                    gx < a.P ? *(const uint32_t*)(lvl + (size_t)(by0 + r) * a.P + gx) : 0u;
+                const uint8_t* gsrc = lvl + (size_t)by0 * a.P + gx;
+                for (int r = lane >> 4; r < fth; r += 4)
+                    *(uint32_t*)(FT + r * ftw + 4 * c) = gx < a.P ? *(const uint32_t*)(gsrc + (size_t)r * a.P) : 0u;
             }
         }
         wave_sync();
-        const int c0 = cx0 + 4 * lg;
-        if (c0 <= cx1) {
-            const int4 A = *(const int4*)(tad + c0);
-            const int4 B = *(const int4*)(tbd + c0);
-            const int adv[4] = {A.x, A.y, A.z, A.w}, bdv[4] = {B.x, B.y, B.z, B.w};
+        if (c0 > cx1) continue;
+        const int adv[4] = {A.x, A.y, A.z, A.w}, bdv[4] = {B.x, B.y, B.z, B.w};
+        uint8_t* dst = a.roi + (size_t)slot * a.roi_stride + c0;
+        if ((flags & kTileInterior) && in_lds) {
+            const uint8_t* base = FT - by0 * ftw - bxa;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int r = ry0 + lr + 8 * i;
                 if (r > ry1) break;
-                const int X0 = tx0[r], Y0 = ty0[r];
                 uint32_t pk = 0;
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    const int X = (X0 + adv[u]) >> (kAbBits - kInterBits);
-                    const int Y = (Y0 + bdv[u]) >> (kAbBits - kInterBits);
-                    int v;
-                    if (in_lds) {
-                        const int sx = sat_s16(X >> kInterBits), sy = sat_s16(Y >> kInterBits);
-                        const int fx = X & (kInterTab - 1), fy = Y & (kInterTab - 1);
-                        const uint8_t* p = FT + (sy - by0) * ftw + (sx - bxa);
-                        int v0, v1, v2, v3;
-                        if ((unsigned)sx < (unsigned)(W - 1) && (unsigned)sy < (unsigned)(H - 1)) {
-                            v0 = p[0]; v1 = p[1]; v2 = p[ftw]; v3 = p[ftw + 1];
-                        } else if (sx >= W || sx + 1 < 0 || sy >= H || sy + 1 < 0) {
-                            v0 = v1 = v2 = v3 = 0;
-                        } else {
-                            const bool x0 = sx >= 0 && sx < W, x1 = sx + 1 >= 0 && sx + 1 < W;
-                            const bool y0 = sy >= 0 && sy < H, y1 = sy + 1 >= 0 && sy + 1 < H;
-                            v0 = x0 && y0 ? p[0] : 0;
-                            v1 = x1 && y0 ? p[1] : 0;
-                            v2 = x0 && y1 ? p[ftw] : 0;
-                            v3 = x1 && y1 ? p[ftw + 1] : 0;
-                        }
-                        const int h0 = 32 * v0 + fx * (v1 - v0), h1 = 32 * v2 + fx * (v3 - v2);
-                        v = (32 * h0 + fy * (h1 - h0) + 512) >> 10;
-                    } else {
-                        v = roi_tap(lvl, W, H, a.P, X, Y);
-                    }
+                    const int X = (X0r[i] + adv[u]) >> (kAbBits - kInterBits);
+                    const int Y = (Y0r[i] + bdv[u]) >> (kAbBits - kInterBits);
+                    const int fx = X & (kInterTab - 1), fy = Y & (kInterTab - 1);
+                    const uint8_t* p = base + __mul24(Y >> kInterBits, ftw) + (X >> kInterBits);
+                    const int v0 = p[0], v1 = p[1], v2 = p[ftw], v3 = p[ftw + 1];
+                    const int h0 = 32 * v0 + __mul24(fx, v1 - v0), h1 = 32 * v2 + __mul24(fx, v3 - v2);
+                    int v = (32 * h0 + __mul24(fy, h1 - h0) + 512) >> 10;
                     if (c0 + u >= RW) v = 0;
                     pk |= (uint32_t)v << (8 * u);
                 }
-                *(uint32_t*)(a.roi + (size_t)slot * a.roi_stride + (size_t)r * a.roi_pitch + c0) = pk;
+                *(uint32_t*)(dst + (size_t)r * a.roi_pitch) = pk;
             }
+            continue;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = ry0 + lr + 8 * i;
+            if (r > ry1) break;
+            uint32_t pk = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int X = (X0r[i] + adv[u]) >> (kAbBits - kInterBits);
+                const int Y = (Y0r[i] + bdv[u]) >> (kAbBits - kInterBits);
+                int v;
+                if (in_lds) {
+                    const int sx = sat_s16(X >> kInterBits), sy = sat_s16(Y >> kInterBits);
+                    const int fx = X & (kInterTab - 1), fy = Y & (kInterTab - 1);
+                    const uint8_t* p = FT + (sy - by0) * ftw + (sx - bxa);
+                    int v0, v1, v2, v3;
+                    if ((unsigned)sx < (unsigned)(W - 1) && (unsigned)sy < (unsigned)(H - 1)) {
+                        v0 = p[0]; v1 = p[1]; v2 = p[ftw]; v3 = p[ftw + 1];
+                    } else if (sx >= W || sx + 1 < 0 || sy >= H || sy + 1 < 0) {
+                        v0 = v1 = v2 = v3 = 0;
+                    } else {
+                        const bool x0 = sx >= 0 && sx < W, x1 = sx + 1 >= 0 && sx + 1 < W;
+                        const bool y0 = sy >= 0 && sy < H, y1 = sy + 1 >= 0 && sy + 1 < H;
+                        v0 = x0 && y0 ? p[0] : 0;
+                        v1 = x1 && y0 ? p[1] : 0;
+                        v2 = x0 && y1 ? p[ftw] : 0;
+                        v3 = x1 && y1 ? p[ftw + 1] : 0;
+                    }
+                    const int h0 = 32 * v0 + fx * (v1 - v0), h1 = 32 * v2 + fx * (v3 - v2);
+                    v = (32 * h0 + fy * (h1 - h0) + 512) >> 10;
+                } else {
+                    v = roi_tap(lvl, W, H, a.P, X, Y);
+                }
+                if (c0 + u >= RW) v = 0;
+                pk |= (uint32_t)v << (8 * u);
+            }
+            *(uint32_t*)(dst + (size_t)r * a.roi_pitch) = pk;
         }
     }
 }
 
-// ---- K7: per-row exact correlation.  grid = (ROI, chunk of RC template rows).  ROI rows [t0, t0+rc+6) and
-// template rows [t0, t0+rc) are staged into LDS (16-byte loads; template rows padded with 6 zero rows on both
-// sides).  Thread = (source row s, column group g): for every 16-byte slice of its group it forms the 7 byte
-// shifts of the source words with v_alignbyte and accumulates all 49 (dy, dx) dot products of template rows
-// s - dy with v_dot4_u32_u8 (49 accumulators).  Group partials are combined with exact LDS integer atomics.
-// Also exact window sums of I and I^2 per chunk.
+// ---- K7: per-row exact correlation on the matrix cores.  For one ROI, the 49 per-row dot products
+// R[t][dy][dx] = sum_c T[t][c] * I[t+dy][c+dx] (IM_Conv_SIMD's int32 row results, TemplateMatcher.cpp:487-512)
+// are, for each shift dx, a banded GEMM  D_dx[t][s] = sum_c T[t][c] * I[s][c+dx]  kept where 0 <= s - t < 7:
+// A = template rows (M = 16), B = source rows (N = 16), K = columns, 64 per v_mfma_i32_16x16x64_i8.
+// A work item is a band of 32 template rows (2 M tiles) and its 38 source rows (3 N tiles); wave w takes the
+// (M, N) tile pair (w & 1, (w & 1) + (w >> 1)) and all 7 shifts, so a shift is uniform per instruction: B
+// fragments are aligned 16 + 8 byte LDS reads funnel-shifted by a constant (v_alignbyte), A fragments aligned
+// 16-byte loads of the i8 template.  u8 operands enter the signed MFMA as x ^ 0x80 = x - 128; the exact value
+// is restored with integer corrections  sum T*I = sum T'I' + 128*(W[s][dx] + TS[t]) - 16384*tw  (W = window row
+// sum of I, TS = template row sum; mod 2^32, true value < 2^31).  The item also produces the rows' exact window
+// sums of I and I^2 and the per-16-row-chunk window-sum partials used by the normalisation.
+typedef int fpm_v4i __attribute__((ext_vector_type(4)));
+constexpr int kBandRows = 2 * kMmaRows;       // template rows per work item
+constexpr int kBandSrc = kBandRows + 6;       // source rows per work item
+constexpr int kStageRows = (kBandSrc + 3) / 4;   // staged rows per wave
+constexpr int kStageBatch = 5;                  // of which loaded together
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += (uint32_t)__shfl_xor((int)v, m, 64);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, int sh) {
+    return sh == 0 ? lo : __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+
+// MODE (profiling ablations in scripts/roi_microbench.hip; the product uses 0): 2 = no MFMA loop, 3 = no staging
+template <int MODE>
 __global__ __launch_bounds__(256) void k_roi_corr(RoiArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tw = a.tw, th = a.th, RW = tw + 6;
-    const int ntw = (tw + 3) / 4;
-    const int SBp = a.roi_pitch, TBp = tmpl_pitch_calc(tw);
-    const int RC = a.rc, NS = RC + 6;
-    uint8_t* SB = smem;                                   // NS rows x SBp
-    uint8_t* TB = SB + (size_t)NS * SBp;                  // (RC + 12) rows x TBp, rows 0..5 and 6+rc.. zero
-    uint32_t* rs = (uint32_t*)(TB + (size_t)(RC + 12) * TBp);   // RC x 49
-    int* rall = (int*)(rs + RC * 49);                     // NS
-    int* rallq = rall + NS;                               // NS
-    int* wi = rallq + NS;                                 // NS x 7
-    int* wq = wi + NS * 7;                                // NS x 7
-    const int tid = threadIdx.x;
-    const int rois = roi_count(a);
-    const int items = rois * a.nchunk;
-    // column groups: G groups of `seg` words (multiple of 4) per source row
+    const int SBp = a.roi_pitch;
+    const int TBp = tmpl_lds_pitch(a.tp8);
+    uint8_t* SB = smem;                                        // kBandSrc rows x SBp, bytes ^ 0x80
+    uint8_t* TB = SB + (size_t)kBandSrc * SBp;                 // kBandRows template rows (i8) x TBp
+    uint32_t* rall = (uint32_t*)(TB + (size_t)kBandRows * TBp); // full-row sums of I
+    uint32_t* rallq = rall + kBandSrc;                         // full-row sums of I^2
+    uint32_t* wi = rallq + kBandSrc;                           // [row][dx] window sums of I
+    uint32_t* wq = wi + kBandSrc * 7;                          // [row][dx] window sums of I^2
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int nband = (th + kBandRows - 1) / kBandRows;
+    const int items = roi_count(a) * nband;
+    const int q4 = SBp >> 4;                                   // 16-byte columns per row
+    const int nwr = (RW + 3) >> 2;                             // words holding ROI pixels
+    const int g = lane >> 4, n = lane & 15;
+    const int mt = wv & 1, nt = mt + (wv >> 1);                // this wave's (M, N) tile pair
     for (int item = blockIdx.x; item < items; item += gridDim.x) {
-        const int slot = item / a.nchunk, chunk = item - slot * a.nchunk;
-        const int t0 = chunk * RC, rc = min(RC, th - t0), nsrc = rc + 6;
-        const int G = 256 / nsrc;
-        const int seg = (((ntw + G - 1) / G) + 3) & ~3;
+        const int slot = item / nband, band = item - slot * nband;
+        const int T0 = band * kBandRows, rb = min(kBandRows, th - T0), nsrc = rb + 6;
+        __syncthreads();   // previous item done with SB / wi
+        if (tid < kBandSrc) { rall[tid] = 0; rallq[tid] = 0; }
         __syncthreads();
-        {   // stage: ROI rows (whole pitch incl. zero look-ahead), template rows (zero padded)
-            const uint8_t* rsrc = a.roi + (size_t)slot * a.roi_stride + (size_t)t0 * a.roi_pitch;
-            const int q4 = SBp >> 4;
-            for (int i = tid; i < nsrc * q4; i += 256) {
-                const int r = i / q4, c = i - r * q4;
-                *(uint4*)(SB + (size_t)r * SBp + 16 * c) = *(const uint4*)(rsrc + (size_t)r * a.roi_pitch + 16 * c);
-            }
-            const int tq = TBp >> 2;
-            for (int i = tid; i < (RC + 12) * tq; i += 256) {
-                const int r = i / tq, c = i - r * tq;
-                const int tr = r - 6;
-                uint32_t wv = 0;
-                if (tr >= 0 && tr < rc && 4 * c < tw) {
-                    wv = *(const uint32_t*)(a.tmpl + (size_t)(t0 + tr) * a.tp + 4 * c);
-                    const int valid = tw - 4 * c;
-                    if (valid < 4) wv &= (1u << (8 * valid)) - 1u;
-                }
-                *(uint32_t*)(TB + (size_t)r * TBp + 4 * c) = wv;
-            }
-            for (int i = tid; i < rc * 49; i += 256) rs[i] = 0;
-            if (tid < nsrc) { rall[tid] = 0; rallq[tid] = 0; }
-        }
-        __syncthreads();
-        const int s = tid % nsrc, g = tid / nsrc;
-        if (g < G && !(seg * g >= ntw)) {
-            uint32_t acc[7][7];
+        if (MODE != 3) {   // stage: wave wv stages rows wv + 4i; row sums by wave reduction
+            const uint8_t* rsrc = a.roi + (size_t)slot * a.roi_stride + (size_t)T0 * a.roi_pitch;
+            for (int c0 = 0; c0 < q4; c0 += 64) {
+                const int c = c0 + lane;
+                for (int i0 = 0; i0 < kStageRows; i0 += kStageBatch) {   // kStageBatch rows' loads in flight
+                    uint4 v[kStageBatch];
 #pragma unroll
-            for (int d = 0; d < 7; ++d)
+                    for (int i = 0; i < kStageBatch; ++i) {
+                        const int r = wv + 4 * (i0 + i);
+                        v[i] = (r < nsrc && c < q4) ? *(const uint4*)(rsrc + (size_t)r * a.roi_pitch + 16 * c)
+                                                    : make_uint4(0, 0, 0, 0);
+                    }
 #pragma unroll
-                for (int x = 0; x < 7; ++x) acc[d][x] = 0;
-            uint32_t s1 = 0, s2 = 0;
-            const uint32_t* srow = (const uint32_t*)(SB + (size_t)s * SBp);
-            const int k0 = g * seg, k1 = min(k0 + seg, ntw);
-            // TB row for dy is (s - dy + 6)
-            const uint32_t* trow0 = (const uint32_t*)(TB + (size_t)(s + 6) * TBp);
-            uint4 cur = *(const uint4*)(srow + k0);
-            for (int k = k0; k < k1; k += 4) {
-                const uint4 nxt = *(const uint4*)(srow + k + 4);
-                const uint32_t w[6] = {cur.x, cur.y, cur.z, cur.w, nxt.x, nxt.y};
-                uint4 tv[7];
+                    for (int i = 0; i < kStageBatch; ++i) {
+                        const int r = wv + 4 * (i0 + i);
+                        if (r >= nsrc) break;   // wave-uniform
+                        uint32_t s1 = 0, s2 = 0;
+                        const uint32_t w4[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
 #pragma unroll
-                for (int d = 0; d < 7; ++d) tv[d] = *(const uint4*)(trow0 - (size_t)d * (TBp >> 2) + k);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    if (k + q >= k1) break;
-                    const uint32_t a0 = w[q], a1 = w[q + 1], a2 = w[q + 2];
-                    const uint32_t sh[7] = {a0, __builtin_amdgcn_alignbyte(a1, a0, 1), __builtin_amdgcn_alignbyte(a1, a0, 2),
-                                            __builtin_amdgcn_alignbyte(a1, a0, 3), a1,
-                                            __builtin_amdgcn_alignbyte(a2, a1, 1), __builtin_amdgcn_alignbyte(a2, a1, 2)};
-                    s1 = __builtin_amdgcn_udot4(a0, 0x01010101u, s1, false);
-                    s2 = __builtin_amdgcn_udot4(a0, a0, s2, false);
-#pragma unroll
-                    for (int d = 0; d < 7; ++d) {
-                        const uint32_t tt = q == 0 ? tv[d].x : q == 1 ? tv[d].y : q == 2 ? tv[d].z : tv[d].w;
-#pragma unroll
-                        for (int x = 0; x < 7; ++x) acc[d][x] = __builtin_amdgcn_udot4(tt, sh[x], acc[d][x], false);
+                        for (int k = 0; k < 4; ++k) {
+                            const uint32_t x = 4 * c + k < nwr ? w4[k] : 0u;
+                            s1 = __builtin_amdgcn_udot4(x, 0x01010101u, s1, false);
+                            s2 = __builtin_amdgcn_udot4(x, x, s2, false);
+                        }
+                        if (c < q4) {
+                            uint4 x = v[i];
+                            x.x ^= 0x80808080u; x.y ^= 0x80808080u; x.z ^= 0x80808080u; x.w ^= 0x80808080u;
+                            *(uint4*)(SB + (size_t)r * SBp + 16 * c) = x;
+                        }
+                        s1 = wave_sum_u32(s1);
+                        s2 = wave_sum_u32(s2);
+                        if (lane == 0) { rall[r] += s1; rallq[r] += s2; }
                     }
                 }
-                cur = nxt;
             }
-            // words of the row beyond the last group (look-ahead region) belong to no group: the row sum of
-            // bytes [4*ntw, RW) is added by the group that owns word ntw-1
-            if (k1 == ntw) {
-                for (int k = ntw; k < (RW + 3) / 4; ++k) {
-                    const uint32_t wv = srow[k];
-                    s1 = __builtin_amdgcn_udot4(wv, 0x01010101u, s1, false);
-                    s2 = __builtin_amdgcn_udot4(wv, wv, s2, false);
-                }
-            }
-            atomicAdd(&rall[s], (int)s1);
-            atomicAdd(&rallq[s], (int)s2);
-#pragma unroll
-            for (int d = 0; d < 7; ++d) {
-                const int tl = s - d;
-                if (tl >= 0 && tl < rc)
-#pragma unroll
-                    for (int x = 0; x < 7; ++x) atomicAdd(&rs[tl * 49 + d * 7 + x], acc[d][x]);
+        }
+        {   // template rows T0 .. T0 + 16*ceil(rb/16) - 1 of the i8 slab
+            const int trows = (rb + kMmaRows - 1) / kMmaRows * kMmaRows, tq = a.tp8 >> 4;
+            const uint8_t* tsrc = (const uint8_t*)a.tmpl8 + (size_t)T0 * a.tp8;
+            for (int i = tid; i < trows * tq; i += 256) {
+                const int r = i / tq, c = i - r * tq;
+                *(uint4*)(TB + (size_t)r * TBp + 16 * c) = *(const uint4*)(tsrc + (size_t)r * a.tp8 + 16 * c);
             }
         }
         __syncthreads();
-        // rows out + window-row sums (full-row sum minus <= 6 edge pixels)
-        for (int i = tid; i < rc * 49; i += 256) a.rowsum[((size_t)slot * th + t0) * 49 + i] = rs[i];
-        for (int i = tid; i < nsrc * 7; i += 256) {
+        for (int i = tid; i < nsrc * 7; i += 256) {   // window [dx, dx + tw): full row minus <= 6 edge pixels
             const int r = i / 7, dx = i - r * 7;
             const uint8_t* sbr = SB + (size_t)r * SBp;
-            int q1 = rall[r], q2 = rallq[r];
-            for (int c = 0; c < dx; ++c) { const int v = sbr[c]; q1 -= v; q2 -= v * v; }
-            for (int c = dx + tw; c < RW; ++c) { const int v = sbr[c]; q1 -= v; q2 -= v * v; }
+            uint32_t q1 = rall[r], q2 = rallq[r];
+            for (int c = 0; c < dx; ++c) { const uint32_t v = sbr[c] ^ 0x80u; q1 -= v; q2 -= v * v; }
+            for (int c = dx + tw; c < RW; ++c) { const uint32_t v = sbr[c] ^ 0x80u; q1 -= v; q2 -= v * v; }
             wi[i] = q1;
             wq[i] = q2;
         }
         __syncthreads();
-        if (tid < 49) {
-            const int pdy = tid / 7, pdx = tid - pdy * 7;
-            uint32_t s1 = 0;
-            uint64_t s2 = 0;
-            for (int tl = 0; tl < rc; ++tl) {
-                s1 += (uint32_t)wi[(tl + pdy) * 7 + pdx];
-                s2 += (uint32_t)wq[(tl + pdy) * 7 + pdx];
+        const bool active = kMmaRows * mt < rb && kMmaRows * nt < nsrc;   // wave-uniform
+        if (MODE != 2 && active) {
+            const uint8_t* ap = TB + (size_t)(kMmaRows * mt + n) * TBp + 16 * g;
+            int sr = kMmaRows * nt + n;
+            if (sr >= nsrc) sr = 0;   // column outside the band: computed, never stored
+            const uint8_t* bp = SB + (size_t)sr * SBp + 16 * g;
+            fpm_v4i c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0, c4 = c0, c5 = c0, c6 = c0;
+            for (int k = 0; k < a.nk; ++k) {
+                const fpm_v4i av = *(const fpm_v4i*)__builtin_assume_aligned(ap + 64 * k, 16);
+                const uint8_t* bk = (const uint8_t*)__builtin_assume_aligned(bp + 64 * k, 16);
+                const uint4 lo = *(const uint4*)bk;
+                const uint2 hi = *(const uint2*)(bk + 16);
+                const uint32_t w0 = lo.x, w1 = lo.y, w2 = lo.z, w3 = lo.w, w4 = hi.x, w5 = hi.y;
+                // shift d: bytes [d, d + 16) of w0..w5 (o = d >> 2 words, then alignbyte by d & 3)
+                const uint32_t a10 = __builtin_amdgcn_alignbyte(w1, w0, 1), a21 = __builtin_amdgcn_alignbyte(w2, w1, 1),
+                               a32 = __builtin_amdgcn_alignbyte(w3, w2, 1), a43 = __builtin_amdgcn_alignbyte(w4, w3, 1),
+                               a54 = __builtin_amdgcn_alignbyte(w5, w4, 1);
+                const uint32_t b10 = __builtin_amdgcn_alignbyte(w1, w0, 2), b21 = __builtin_amdgcn_alignbyte(w2, w1, 2),
+                               b32 = __builtin_amdgcn_alignbyte(w3, w2, 2), b43 = __builtin_amdgcn_alignbyte(w4, w3, 2),
+                               b54 = __builtin_amdgcn_alignbyte(w5, w4, 2);
+                const uint32_t e10 = __builtin_amdgcn_alignbyte(w1, w0, 3), e21 = __builtin_amdgcn_alignbyte(w2, w1, 3),
+                               e32 = __builtin_amdgcn_alignbyte(w3, w2, 3), e43 = __builtin_amdgcn_alignbyte(w4, w3, 3);
+                c0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)w0, (int)w1, (int)w2, (int)w3}, c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)a10, (int)a21, (int)a32, (int)a43}, c1, 0, 0, 0);
+                c2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)b10, (int)b21, (int)b32, (int)b43}, c2, 0, 0, 0);
+                c3 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)e10, (int)e21, (int)e32, (int)e43}, c3, 0, 0, 0);
+                c4 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)w1, (int)w2, (int)w3, (int)w4}, c4, 0, 0, 0);
+                c5 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)a21, (int)a32, (int)a43, (int)a54}, c5, 0, 0, 0);
+                c6 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)b21, (int)b32, (int)b43, (int)b54}, c6, 0, 0, 0);
             }
-            a.wsum[((size_t)slot * a.nchunk + chunk) * 49 + tid] = s1;
-            a.wsq[((size_t)slot * a.nchunk + chunk) * 49 + tid] = s2;
+            const fpm_v4i acc[7] = {c0, c1, c2, c3, c4, c5, c6};
+            // D_dx: col = lane & 15 -> source row 16*nt + n, row = 4*(lane >> 4) + r -> template row 16*mt + 4g + r
+            uint32_t* rs_out = a.rowsum + (((size_t)th * 49 + 3) & ~(size_t)3) * slot + (size_t)T0 * 49;
+            const uint32_t kFix = 16384u * (uint32_t)tw;
+            const int s_ = kMmaRows * nt + n;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int t = kMmaRows * mt + 4 * g + r, dy = s_ - t;
+                if (t < rb && s_ < nsrc && dy >= 0 && dy < 7) {
+                    const uint32_t ts = (uint32_t)a.tsum[T0 + t];
+#pragma unroll
+                    for (int d = 0; d < 7; ++d)
+                        rs_out[(size_t)t * 49 + dy * 7 + d] = (uint32_t)acc[d][r] + 128u * (wi[s_ * 7 + d] + ts) - kFix;
+                }
+            }
+        }
+        if (tid < 2 * 49) {   // per-16-row-chunk partials of the window sums
+            const int h = tid / 49, k = tid - h * 49;
+            const int chunk = (T0 >> 4) + h;
+            const int tlo = kMmaRows * h, thi = min(tlo + kMmaRows, rb);
+            if (chunk < a.nchunk && tlo < thi) {
+                const int pdy = k / 7, ddx = k - pdy * 7;
+                uint32_t s1 = 0;
+                uint64_t s2 = 0;
+                for (int t = tlo; t < thi; ++t) {
+                    s1 += wi[(t + pdy) * 7 + ddx];
+                    s2 += wq[(t + pdy) * 7 + ddx];
+                }
+                a.wsum[((size_t)slot * a.nchunk + chunk) * 49 + k] = s1;
+                a.wsq[((size_t)slot * a.nchunk + chunk) * 49 + k] = s2;
+            }
         }
     }
 }
 
-__global__ __launch_bounds__(64) void k_roi_eval(RoiArgs a) {
+// ---- K8: per ROI: ordered f32 fold of the 49 row-sum series (:505-508), window sums, CCOEFF, argmax, 3x3.
+// The [th][49] row sums stream through LDS in blocks of kEvalRows rows; the next block's loads are in flight
+// (registers) while 49 lanes fold the current block in row order.
+constexpr int kEvalRows = 128;
+constexpr int kEvalVec = (kEvalRows * 49 / 4 + 255) / 256;   // uint4 per thread per block
+
+__global__ __launch_bounds__(256) void k_roi_eval(RoiArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t blk[kEvalRows * 49];
     __shared__ float sc[64];
     const int tid = threadIdx.x;
     const int rois = roi_count(a);
+    const int th = a.th;
+    const int nblk = (th + kEvalRows - 1) / kEvalRows;
     for (int slot = blockIdx.x; slot < rois; slot += gridDim.x) {
         int id, jj;
         roi_slot(a, slot, id, jj);
@@ -779,28 +886,43 @@ __global__ __launch_bounds__(64) void k_roi_eval(RoiArgs a) {
             }
             continue;
         }
-        if (tid < 49) {
-            const uint32_t* rs = a.rowsum + (size_t)slot * a.th * 49 + tid;
-            float accF = 0.f;
-            uint64_t accI = 0;
-            int t = 0;
-            if (a.fold) {
-                for (; t + 8 <= a.th; t += 8) {
-                    uint32_t v[8];
+        const size_t total4 = ((size_t)th * 49 + 3) >> 2;         // uint4 per ROI series (slot stride 4*total4)
+        const uint32_t* rs = a.rowsum + (size_t)slot * total4 * 4;
+        uint64_t s1 = 0, s2 = 0;
+        if (tid < 49) {   // window sums over the chunk partials (independent of the fold)
+            const uint32_t* ws = a.wsum + (size_t)slot * a.nchunk * 49 + tid;
+            const uint64_t* wq = a.wsq + (size_t)slot * a.nchunk * 49 + tid;
+            for (int c = 0; c < a.nchunk; ++c) { s1 += ws[(size_t)c * 49]; s2 += wq[(size_t)c * 49]; }
+        }
+        float accF = 0.f;
+        uint64_t accI = 0;
+        uint4 v[kEvalVec];
+        auto load_block = [&](int b) {
+            const size_t base4 = (size_t)b * (kEvalRows * 49 / 4);
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) v[u] = rs[(size_t)(t + u) * 49];
+            for (int i = 0; i < kEvalVec; ++i) {
+                const size_t q = base4 + tid + 256 * i;
+                v[i] = (tid + 256 * i < kEvalRows * 49 / 4 && q < total4) ? ((const uint4*)rs)[q] : make_uint4(0, 0, 0, 0);
+            }
+        };
+        load_block(0);
+        for (int b = 0; b < nblk; ++b) {
+            __syncthreads();   // previous block folded
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) accF = accF + (float)(int)v[u];   // :507, row order
+            for (int i = 0; i < kEvalVec; ++i)
+                if (tid + 256 * i < kEvalRows * 49 / 4) ((uint4*)blk)[tid + 256 * i] = v[i];
+            __syncthreads();
+            if (b + 1 < nblk) load_block(b + 1);
+            const int rows = min(kEvalRows, th - b * kEvalRows);
+            if (tid < 49) {
+                if (a.fold) {
+                    for (int t = 0; t < rows; ++t) accF = accF + (float)(int)blk[t * 49 + tid];   // :507, row order
+                } else {
+                    for (int t = 0; t < rows; ++t) accI += blk[t * 49 + tid];
                 }
-                for (; t < a.th; ++t) accF = accF + (float)(int)rs[(size_t)t * 49];
-            } else {
-                for (; t < a.th; ++t) accI += rs[(size_t)t * 49];
             }
-            uint64_t s1 = 0, s2 = 0;
-            for (int c = 0; c < a.nchunk; ++c) {
-                s1 += a.wsum[((size_t)slot * a.nchunk + c) * 49 + tid];
-                s2 += a.wsq[((size_t)slot * a.nchunk + c) * 49 + tid];
-            }
+        }
+        if (tid < 49) {
             const double num = a.fold ? (double)accF : (double)(float)(double)accI;
             sc[tid] = ccoeff(num, (double)s1, (double)s2, a.mean, a.norm, a.inv_area);
         }
@@ -820,19 +942,25 @@ __global__ __launch_bounds__(64) void k_roi_eval(RoiArgs a) {
                 for (int y = -1; y <= 1; ++y)
                     out->vec[(x + 1) * 3 + (y + 1)] = border ? 0.f : sc[(my + y) * 7 + (mx + x)];
         }
-        __syncthreads();
     }
 }
 
 void launch_roi_tables(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0 || a.equal1) return;
-    const int grid = a.slot_cap < 2048 ? a.slot_cap : 2048;
-    hipLaunchKernelGGL(k_roi_tables, dim3(grid), dim3(256), 0, st, a);
+    const int grid = a.slot_cap < 4096 ? a.slot_cap : 4096;
+    const size_t lds = sizeof(int32_t) * 2 * (a.tabw + a.tabh);
+    static size_t lds_attr = 0;
+    if (lds > 65536 && lds > lds_attr) {
+        (void)hipFuncSetAttribute((const void*)k_roi_tables, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        lds_attr = lds;
+    }
+    hipLaunchKernelGGL(k_roi_tables, dim3(grid), dim3(256), lds, st, a);
 }
 
 void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0 || a.equal1) return;
     const long tiles = (long)a.slot_cap * ((a.th + 6 + ROI_T - 1) / ROI_T) * ((a.tw + 6 + ROI_T - 1) / ROI_T);
+    if (tiles > INT_MAX) return;   // the engine bounds slot_cap far below this
     const long want = (tiles + 3) / 4;
     const int grid = (int)(want < 16384 ? want : 16384);
     hipLaunchKernelGGL(k_roi_warp, dim3(grid), dim3(256), 0, st, a);
@@ -843,18 +971,18 @@ void launch_roi_corr(const RoiArgs& a, hipStream_t st) {
     const size_t lds = roi_corr_lds(a.roi_pitch, a.tw, a.rc);
     static size_t lds_attr = 0;
     if (lds > 65536 && lds > lds_attr) {
-        (void)hipFuncSetAttribute((const void*)k_roi_corr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)k_roi_corr<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         lds_attr = lds;
     }
-    const long items = (long)a.slot_cap * a.nchunk;
-    const int grid = (int)(items < 8192 ? items : 8192);
-    hipLaunchKernelGGL(k_roi_corr, dim3(grid), dim3(256), lds, st, a);
+    const long items = (long)a.slot_cap * ((a.th + kBandRows - 1) / kBandRows);
+    const int grid = (int)(items < 16384 ? items : 16384);
+    hipLaunchKernelGGL(k_roi_corr<0>, dim3(grid), dim3(256), lds, st, a);
 }
 
 void launch_roi_eval(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0) return;
     const int grid = a.slot_cap < 4096 ? a.slot_cap : 4096;
-    hipLaunchKernelGGL(k_roi_eval, dim3(grid), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(k_roi_eval, dim3(grid), dim3(256), 0, st, a);
 }
 
 // ============================================================================================== step
