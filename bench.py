@@ -35,7 +35,7 @@ def log(*a):
 # kernels of each profiled family (fpm_profile_* families, include/fpm.h FPM_K_*)
 FAMILY_KERNELS = {"pyr_down": ["k_pyr_down"], "top_warp": ["k_warp"], "top_ncc": ["k_ncc_map"], "top_nms": ["k_nms"],
                   "roi_warp": ["k_roi_tables", "k_roi_warp"], "roi_corr": ["k_roi_corr"], "roi_eval": ["k_roi_eval"],
-                  "cand": ["k_cand_init", "k_cand_step"]}
+                  "cand": ["k_cand_init"]}
 TRAFFIC_CSV = os.path.join(REPO, "profiles", "latest", "pmc_traffic.csv")
 
 

@@ -149,6 +149,11 @@ struct fpm_ctx {
     // profiling
     bool prof = false;
     KProf kp[FPM_K_COUNT];
+    // the whole device-resident search captured once per (plan, source slab) and replayed as one hipGraph
+    hipGraphExec_t graph = nullptr;
+    uint64_t graph_plan = ~0ull;
+    const void* graph_src = nullptr;
+    uint64_t plan_builds = 0;
 };
 
 #define HIP_TRY(expr)                                                                   \
@@ -406,7 +411,8 @@ int build_plan(fpm_ctx* ctx) {
                                max_chunks * 49 * 12;
         const size_t budget = (size_t)16 << 30;   // of 288 GB HBM; rounds only beyond this
         const size_t want = (size_t)P.C * P.n3;
-        P.slot_cap = (int)std::max<size_t>(1, std::min(want, budget / per_roi));
+        // rounds hold whole candidates (k_roi_eval steps a candidate from its n3 records)
+        P.slot_cap = (int)std::max<size_t>((size_t)P.n3, std::min(want, budget / per_roi) / P.n3 * P.n3);
         HIP_TRY(P.d_tab.ensure((size_t)P.slot_cap * 2 * (P.tabw + P.tabh) * sizeof(int32_t)));
         HIP_TRY(P.d_tdesc.ensure((size_t)P.slot_cap * P.tdesc_stride * sizeof(int4)));
         HIP_TRY(P.d_roi.ensure((size_t)P.slot_cap * P.roi_stride));
@@ -463,6 +469,7 @@ int build_plan(fpm_ctx* ctx) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     P.valid = true;
     ctx->plan_gen = ctx->tmpl_gen;
+    ctx->plan_builds++;
     return FPM_OK;
 }
 
@@ -529,7 +536,13 @@ int enqueue_search(fpm_ctx* ctx) {
         for (int a = 0; a < P.nang; ++a)
             bytes += (int64_t)P.top[a].bw * P.top[a].bh + (int64_t)tt.w * tt.h + 4LL * P.map_w[a] * P.map_h[a];
         ProfScope ps(ctx, FPM_K_TOP_NCC, bytes * S);
-        launch_ncc_map(P.d_jobs.as<NccJob>(P.off_ncc), J, P.max_map, tt.w * tt.h, st);
+        if (ncc_tile_fits(tt.w, tt.h)) {
+            int mw = 0, mh = 0;
+            for (int a = 0; a < P.nang; ++a) { mw = std::max(mw, P.map_w[a]); mh = std::max(mh, P.map_h[a]); }
+            launch_ncc_tile(P.d_jobs.as<NccJob>(P.off_ncc), J, mw, mh, st);
+        } else {
+            launch_ncc_map(P.d_jobs.as<NccJob>(P.off_ncc), J, P.max_map, tt.w * tt.h, st);
+        }
     }
     {
         int64_t bytes = 0;
@@ -581,17 +594,29 @@ int enqueue_search(fpm_ctx* ctx) {
         ra.live_count = livecnt + d;
         ra.state = P.d_state.as<CandState>();
         ra.nodes = P.d_nodes.as<AngleNode>() + P.node_off[d];
-        ra.tab = P.d_tab.as<int32_t>(); ra.tabw = P.tabw; ra.tabh = P.tabh;
+        // per-level scratch geometry (the buffers are sized for the largest level)
+        ra.tab = P.d_tab.as<int32_t>(); ra.tabw = roi_pitch_for(tl.w); ra.tabh = round_up(tl.h + 6, 4);
         ra.tdesc = P.d_tdesc.as<int4>(); ra.tdesc_stride = P.tdesc_stride;
-        ra.roi = P.d_roi.as<uint8_t>(); ra.roi_pitch = P.roi_pitch; ra.roi_stride = P.roi_stride;
+        ra.roi = P.d_roi.as<uint8_t>(); ra.roi_pitch = roi_pitch_for(tl.w); ra.roi_stride = P.roi_stride;
         ra.rowsum = P.d_rowsum.as<uint32_t>();
         ra.wsum = P.d_wsum.as<uint32_t>();
         ra.wsq = P.d_wsq.as<uint64_t>();
         ra.rec = P.d_rec.as<RoiRecord>();
+        ra.step = l > 0 ? 1 : 0;   // candidate step fused into k_roi_eval (layer 0 is decided on the host)
+        ra.mark_reached0 = l - 1 == 0 ? 1 : 0;
+        ra.live_out = live[(d + 1) & 1];
+        ra.live_out_count = livecnt + d + 1;
+        ra.thr = P.layer_score[l];
         const int total_rois = P.C * P.n3;
+        const bool small = roi_small_fits(tl.w, tl.h);   // one-kernel refinement of the ROI in LDS
         for (int base = 0; base < total_rois; base += P.slot_cap) {
             ra.slot_base = base;
             ra.slot_cap = std::min(P.slot_cap, total_rois - base);
+            if (small) {
+                ProfScope ps(ctx, FPM_K_ROI_CORR, 0);
+                launch_roi_small(ra, st);
+                continue;
+            }
             {
                 ProfScope ps(ctx, FPM_K_ROI_WARP, 0);
                 launch_roi_tables(ra, st);
@@ -606,21 +631,9 @@ int enqueue_search(fpm_ctx* ctx) {
                 launch_roi_eval(ra, st);
             }
         }
-        if (l > 0) {
+        if (small && ra.step) {
             ProfScope ps(ctx, FPM_K_CAND, 0);
-            StepArgs sa;
-            sa.live_in = live[d & 1];
-            sa.live_in_count = livecnt + d;
-            sa.live_out = live[(d + 1) & 1];
-            sa.live_out_count = livecnt + d + 1;
-            sa.state = P.d_state.as<CandState>();
-            sa.rec = P.d_rec.as<RoiRecord>();
-            sa.nodes = P.d_nodes.as<AngleNode>() + P.node_off[d];
-            sa.n3 = P.n3;
-            sa.W = lv.w; sa.H = lv.h;
-            sa.mark_reached0 = l - 1 == 0 ? 1 : 0;
-            sa.thr = P.layer_score[l];
-            launch_cand_step(sa, P.C, st);
+            launch_cand_step(ra, P.C, st);
         }
     }
     HIP_TRY(hipGetLastError());
@@ -747,10 +760,32 @@ void finish_source(fpm_ctx* ctx, int s, std::vector<fpm_result>& out) {
     }
 }
 
+// Launch the search: replay the captured graph (every pointer and launch shape is fixed by the plan and the
+// source slab; data-dependent work sizes live in device counters), or enqueue it eagerly when profiling.
+int launch_search(fpm_ctx* ctx) {
+    if (ctx->prof) return enqueue_search(ctx);   // per-launch HIP events need the eager path
+    if (!ctx->graph || ctx->graph_plan != ctx->plan_builds || ctx->graph_src != ctx->d_src.p) {
+        if (ctx->graph) { (void)hipGraphExecDestroy(ctx->graph); ctx->graph = nullptr; }
+        hipGraph_t g = nullptr;
+        HIP_TRY(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+        const int rc = enqueue_search(ctx);
+        const hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+        if (rc != FPM_OK) { if (g) (void)hipGraphDestroy(g); return rc; }
+        HIP_TRY(e);
+        const hipError_t ie = hipGraphInstantiate(&ctx->graph, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        HIP_TRY(ie);
+        ctx->graph_plan = ctx->plan_builds;
+        ctx->graph_src = ctx->d_src.p;
+    }
+    HIP_TRY(hipGraphLaunch(ctx->graph, ctx->stream));
+    return FPM_OK;
+}
+
 int run_staged(fpm_ctx* ctx, std::vector<std::vector<fpm_result>>& results) {
     int rc = build_plan(ctx);
     if (rc != FPM_OK) return rc;
-    rc = enqueue_search(ctx);
+    rc = launch_search(ctx);
     if (rc != FPM_OK) return rc;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     prof_collect(ctx);
@@ -772,12 +807,16 @@ int run_staged(fpm_ctx* ctx, std::vector<std::vector<fpm_result>>& results) {
             const int64_t rois = (int64_t)lc[d] * P.n3;
             const int rc = roi_pick_rc(t.w, t.h);
             const int64_t nch = (t.h + rc - 1) / rc;
+            if (roi_small_fits(t.w, t.h)) {   // one kernel: source samples + template in, one record out
+                ctx->kp[FPM_K_ROI_CORR].bytes +=
+                    rois * ((int64_t)(t.w + 6) * (t.h + 6) + (int64_t)t.w * t.h + (int64_t)sizeof(RoiRecord));
+                continue;
+            }
             // warp: ROI bytes written (its source taps are a gather, not counted); corr: ROI + template read,
-            // row sums + window partials written
+            // row sums + window partials written; eval: row sums + partials read, one record written
             ctx->kp[FPM_K_ROI_WARP].bytes += rois * (int64_t)(t.w + 6) * (t.h + 6);
             ctx->kp[FPM_K_ROI_CORR].bytes +=
                 rois * ((int64_t)(t.w + 6) * (t.h + 6) + (int64_t)t.w * t.h + (int64_t)t.h * 49 * 4 + nch * 49 * 12);
-            // eval kernel: row sums + partials read, one record written
             ctx->kp[FPM_K_ROI_EVAL].bytes += rois * ((int64_t)t.h * 49 * 4 + nch * 49 * 12 + (int64_t)sizeof(RoiRecord));
         }
     }
@@ -840,6 +879,7 @@ int fpm_destroy(fpm_ctx* ctx) {
     if (!ctx) return FPM_E_INVALID_ARG;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->graph) (void)hipGraphExecDestroy(ctx->graph);
     ctx->plan.release();
     ctx->d_tmpl.release(); ctx->d_tmpl8.release(); ctx->d_tsum.release(); ctx->d_src.release();
     ctx->d_op_a.release(); ctx->d_op_b.release(); ctx->d_op_job.release();
@@ -1107,7 +1147,8 @@ int fpm_op_ncc_map(fpm_ctx* ctx, const uint8_t* src, int32_t w, int32_t h, size_
     j.mean = t.mean; j.norm = t.norm; j.inv_area = t.inv_area;
     HIP_TRY(hipMemcpyAsync(ctx->d_op_job.p, &j, sizeof(j), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpy2DAsync(ctx->d_op_a.p, sp, src, ss, w, h, hipMemcpyHostToDevice, ctx->stream));
-    launch_ncc_map(ctx->d_op_job.as<NccJob>(), 1, ow * oh, t.w * t.h, ctx->stream);
+    if (ncc_tile_fits(t.w, t.h)) launch_ncc_tile(ctx->d_op_job.as<NccJob>(), 1, ow, oh, ctx->stream);
+    else launch_ncc_map(ctx->d_op_job.as<NccJob>(), 1, ow * oh, t.w * t.h, ctx->stream);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(out, ctx->d_op_b.p, sizeof(float) * (size_t)ow * oh, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));

@@ -104,7 +104,7 @@ struct RoiArgs {
     double mean, norm, inv_area;
     const int32_t* live;
     const int32_t* live_count;
-    const CandState* state;
+    CandState* state;        // read by the ROI kernels, stepped by k_roi_eval
     const AngleNode* nodes;  // level nodes; child = parent * n3 + j
     int32_t* tab;            // [slot] fixed-point warp tables: ad[tabw], bd[tabw], x0[tabh], y0[tabh]
     int32_t tabw, tabh;
@@ -117,34 +117,31 @@ struct RoiArgs {
     uint32_t* wsum;          // [slot][nchunk][49] window-sum partials of I
     uint64_t* wsq;           // [slot][nchunk][49] window-sum partials of I^2
     RoiRecord* rec;          // [cand * n3 + j]
-};
-
-struct StepArgs {
-    const int32_t* live_in;
-    const int32_t* live_in_count;
+    // candidate step fused into k_roi_eval (TemplateMatcher.cpp:329-366) when step != 0
+    int32_t step;            // 1: best of n3, early break, back-mapping, append to live_out
+    int32_t mark_reached0;   // next layer is 0
     int32_t* live_out;
     int32_t* live_out_count;
-    CandState* state;
-    const RoiRecord* rec;
-    const AngleNode* nodes;
-    int32_t n3;
-    int32_t W, H;            // level size (ptSrcCenter)
-    int32_t mark_reached0;   // next layer is 0
     double thr;              // vecLayerScore[layer]
 };
+
 
 // launchers (stream-ordered, no synchronisation)
 void launch_pyr_down(const uint8_t* src, int sw, int sh, int sp, size_t s_img, uint8_t* dst, int dw, int dh,
                      int dp, size_t d_img, int nimg, hipStream_t st);
 void launch_warp(const WarpJob* jobs, int njobs, int max_pixels, hipStream_t st);
 void launch_ncc_map(const NccJob* jobs, int njobs, int max_out, int tmpl_bytes, hipStream_t st);
+bool ncc_tile_fits(int tw, int th);   // LDS-tiled variant applies (templates up to 128 x 64)
+void launch_ncc_tile(const NccJob* jobs, int njobs, int max_ow, int max_oh, hipStream_t st);
 void launch_nms(const NmsArgs& a, int njobs, int max_map, hipStream_t st);
 void launch_cand_init(const CandInitArgs& a, hipStream_t st);
 void launch_roi_tables(const RoiArgs& a, hipStream_t st);
 void launch_roi_warp(const RoiArgs& a, hipStream_t st);
 void launch_roi_corr(const RoiArgs& a, hipStream_t st);
 void launch_roi_eval(const RoiArgs& a, hipStream_t st);
-void launch_cand_step(const StepArgs& a, int max_items, hipStream_t st);
+bool roi_small_fits(int tw, int th);   // the single-kernel small-template refinement applies
+void launch_roi_small(const RoiArgs& a, hipStream_t st);
+void launch_cand_step(const RoiArgs& a, int max_items, hipStream_t st);
 int roi_pick_rc(int tw, int th);
 int roi_pitch_for(int tw);
 int roi_tiles_for(int tw, int th);   // 32x32 warp tiles of a (tw+6) x (th+6) ROI

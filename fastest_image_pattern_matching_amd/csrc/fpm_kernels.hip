@@ -255,12 +255,110 @@ __global__ __launch_bounds__(256) void k_ncc_map(const NccJob* __restrict__ jobs
     }
 }
 
+// LDS-tiled NCC for small templates (the top layer: area <= MinReduceArea by construction).  A 256-thread
+// workgroup computes a 64 x 16 tile of one map; its canvas window ((16 + th - 1) rows x (64 + 4*ntw + 4) bytes)
+// and the template (rows of ntw words, zero beyond tw) are staged in LDS.  A thread owns 4 adjacent outputs of
+// one row: per template word it funnel-shifts two canvas words into the 4 byte alignments and accumulates the
+// correlation (v_dot4_u32_u8 with the template word), the window sum (with a 0x01 mask word) and the window sum of
+// squares (masked word with itself).  Exact u32 row sums, then the same f32 fold / TM_CCORR rounding and f64
+// normalisation as k_ncc_map.
+constexpr int NT_W = 64, NT_H = 16;
+constexpr int NT_MAXW = 32;                 // template words per row (tw <= 128)
+constexpr int NT_MAXH = 64;                 // template rows
+
+__global__ __launch_bounds__(256) void k_ncc_tile(const NccJob* __restrict__ jobs, int tiles_x) {
+    __shared__ uint32_t Tw[NT_MAXH * NT_MAXW];
+    __shared__ uint32_t Mw[NT_MAXW];
+    __shared__ uint32_t Iw[(NT_H + NT_MAXH) * (NT_W / 4 + NT_MAXW + 2)];
+    const NccJob& j = jobs[blockIdx.y];
+    const int tx0 = (blockIdx.x % tiles_x) * NT_W, ty0 = (blockIdx.x / tiles_x) * NT_H;
+    if (tx0 >= j.ow || ty0 >= j.oh) return;   // uniform: this map has fewer tiles
+    const int tw = j.tw, th = j.th, ntw = (tw + 3) >> 2;
+    const int iwq = NT_W / 4 + ntw + 1;        // canvas words per staged row
+    const int irows = NT_H + th - 1;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < th * ntw; i += 256) {
+        const int r = i / ntw, k = i - r * ntw;
+        uint32_t w = 0;
+        for (int b = 0; b < 4; ++b) {
+            const int c = 4 * k + b;
+            if (c < tw) w |= (uint32_t)j.tmpl[(size_t)r * j.tp + c] << (8 * b);
+        }
+        Tw[r * ntw + k] = w;
+    }
+    if (tid < ntw) {
+        uint32_t m = 0;
+        for (int b = 0; b < 4; ++b)
+            if (4 * tid + b < tw) m |= 1u << (8 * b);
+        Mw[tid] = m;
+    }
+    for (int i = tid; i < irows * iwq; i += 256) {
+        const int r = i / iwq, k = i - r * iwq;
+        const int y = ty0 + r, x = tx0 + 4 * k;
+        Iw[r * iwq + k] = (y < j.ih && x + 4 <= j.ip) ? *(const uint32_t*)(j.img + (size_t)y * j.ip + x) : 0u;
+    }
+    __syncthreads();
+    if (j.equal1) {
+        for (int i = tid; i < NT_W * NT_H; i += 256) {
+            const int y = ty0 + i / NT_W, x = tx0 + i % NT_W;
+            if (x < j.ow && y < j.oh) j.out[(size_t)y * j.ow + x] = 1.f;
+        }
+        return;
+    }
+    const int ly = tid >> 4, lx = (tid & 15) * 4;   // outputs (tx0 + lx .. +3, ty0 + ly)
+    float accF[4] = {0.f, 0.f, 0.f, 0.f};
+    uint64_t accI[4] = {0, 0, 0, 0};
+    uint32_t sI[4] = {0, 0, 0, 0}, sQ[4] = {0, 0, 0, 0};
+    for (int r = 0; r < th; ++r) {
+        const uint32_t* ir = Iw + (ly + r) * iwq + (lx >> 2);
+        const uint32_t* tr = Tw + r * ntw;
+        uint32_t d[4] = {0, 0, 0, 0};
+        uint32_t w0 = ir[0];
+        for (int k = 0; k < ntw; ++k) {
+            const uint32_t w1 = ir[k + 1];
+            const uint32_t t = tr[k], m = Mw[k];
+            const uint32_t mff = m * 0xffu;
+            const uint32_t sh[4] = {w0, __builtin_amdgcn_alignbyte(w1, w0, 1), __builtin_amdgcn_alignbyte(w1, w0, 2),
+                                    __builtin_amdgcn_alignbyte(w1, w0, 3)};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                d[q] = __builtin_amdgcn_udot4(t, sh[q], d[q], false);
+                sI[q] = __builtin_amdgcn_udot4(m, sh[q], sI[q], false);
+                sQ[q] = __builtin_amdgcn_udot4(sh[q] & mff, sh[q], sQ[q], false);
+            }
+            w0 = w1;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (j.fold) accF[q] = accF[q] + (float)(int)d[q];   // TemplateMatcher.cpp:507
+            else accI[q] += d[q];
+        }
+    }
+    const int y = ty0 + ly;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int x = tx0 + lx + q;
+        if (x < j.ow && y < j.oh) {
+            const double num = j.fold ? (double)accF[q] : (double)(float)(double)accI[q];
+            j.out[(size_t)y * j.ow + x] = ccoeff(num, (double)sI[q], (double)sQ[q], j.mean, j.norm, j.inv_area);
+        }
+    }
+}
+
 void launch_ncc_map(const NccJob* jobs, int njobs, int max_out, int tmpl_bytes, hipStream_t st) {
     if (njobs <= 0 || max_out <= 0) return;
     int gx = (max_out + 255) / 256;
     if (gx > 2048) gx = 2048;
     const int in_lds = tmpl_bytes <= 32768 ? 1 : 0;
     hipLaunchKernelGGL(k_ncc_map, dim3(gx, njobs), dim3(256), in_lds ? tmpl_bytes : 0, st, jobs, in_lds);
+}
+
+bool ncc_tile_fits(int tw, int th) { return tw <= 4 * NT_MAXW && th <= NT_MAXH; }
+
+void launch_ncc_tile(const NccJob* jobs, int njobs, int max_ow, int max_oh, hipStream_t st) {
+    if (njobs <= 0 || max_ow <= 0 || max_oh <= 0) return;
+    const int tiles_x = (max_ow + NT_W - 1) / NT_W, tiles_y = (max_oh + NT_H - 1) / NT_H;
+    hipLaunchKernelGGL(k_ncc_tile, dim3(tiles_x * tiles_y, njobs), dim3(256), 0, st, jobs, tiles_x);
 }
 
 // ============================================================================================== K5
@@ -427,12 +525,16 @@ void launch_cand_init(const CandInitArgs& a, hipStream_t st) {
 }
 
 // ============================================================================================== K6+K7+K8
-// Refinement ROIs (getRotatedROI + MatchTemplate(bUseSIMD) + minMaxLoc, TemplateMatcher.cpp:309-328), as four
-// short kernels over the device-compacted list of live (candidate, angle) ROIs:
-//   k_roi_tables  per ROI: the fixed-point warp tables (adelta/bdelta per column, X0/Y0 per row)
+// Refinement ROIs (getRotatedROI + MatchTemplate(bUseSIMD) + minMaxLoc, TemplateMatcher.cpp:309-328), per layer
+// as four kernels over the device-compacted list of live (candidate, angle) ROIs:
+//   k_roi_tables  per ROI: the fixed-point warp tables (adelta/bdelta per column, X0/Y0 per row) and one
+//                 descriptor per 32x32 tile (source footprint box, interior flag)
 //   k_roi_warp    per 32x32 ROI tile and wave: LDS-staged footprint + bilinear gathers -> ROI bytes in HBM
-//   k_roi_corr    per (ROI, 16 template rows): exact int32 row dot products for all 49 offsets + window sums
-//   k_roi_eval    per ROI: ordered f32 fold (:505-508), f64 CCOEFF normalisation, argmax, border, 3x3
+//   k_roi_corr    per (ROI, band of 32 template rows): exact row dot products for all 49 offsets on the matrix
+//                 cores + window sums
+//   k_roi_eval    per live candidate: ordered f32 fold (:505-508), CCOEFF, argmax, 3x3, candidate step
+// (A single fused kernel per layer was measured slower: at its LDS/VGPR footprint the latency-bound sampling
+// loses the occupancy it needs; see DESIGN.md.)
 // ---- geometry of the refinement scratch ----------------------------------------------------------------------
 constexpr int ROI_RC = kMmaRows;     // template rows per correlation chunk
 constexpr int ROI_T = 32;            // warp tile: 32 x 32 ROI pixels per wave task
@@ -716,6 +818,36 @@ __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, int sh) {
     return sh == 0 ? lo : __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
 
+// The 7 shifted banded GEMM tiles of one wave: acc[d] += A(16 template rows) x B_d(16 ROI rows shifted by d) over
+// nk k-steps of 64 bytes.  ap / bp: this lane's A row / B row at byte 16*(lane >> 4) of k-step 0 (16-byte aligned).
+__device__ __forceinline__ void band_mfma(const uint8_t* ap, const uint8_t* bp, int nk, fpm_v4i acc[7]) {
+    fpm_v4i c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0, c4 = c0, c5 = c0, c6 = c0;
+    for (int k = 0; k < nk; ++k) {
+        const fpm_v4i av = *(const fpm_v4i*)__builtin_assume_aligned(ap + 64 * k, 16);
+        const uint8_t* bk = (const uint8_t*)__builtin_assume_aligned(bp + 64 * k, 16);
+        const uint4 lo = *(const uint4*)bk;
+        const uint2 hi = *(const uint2*)(bk + 16);
+        const uint32_t w0 = lo.x, w1 = lo.y, w2 = lo.z, w3 = lo.w, w4 = hi.x, w5 = hi.y;
+        // shift d: bytes [d, d + 16) of w0..w5 (d >> 2 whole words, then alignbyte by d & 3)
+        const uint32_t a10 = __builtin_amdgcn_alignbyte(w1, w0, 1), a21 = __builtin_amdgcn_alignbyte(w2, w1, 1),
+                       a32 = __builtin_amdgcn_alignbyte(w3, w2, 1), a43 = __builtin_amdgcn_alignbyte(w4, w3, 1),
+                       a54 = __builtin_amdgcn_alignbyte(w5, w4, 1);
+        const uint32_t b10 = __builtin_amdgcn_alignbyte(w1, w0, 2), b21 = __builtin_amdgcn_alignbyte(w2, w1, 2),
+                       b32 = __builtin_amdgcn_alignbyte(w3, w2, 2), b43 = __builtin_amdgcn_alignbyte(w4, w3, 2),
+                       b54 = __builtin_amdgcn_alignbyte(w5, w4, 2);
+        const uint32_t e10 = __builtin_amdgcn_alignbyte(w1, w0, 3), e21 = __builtin_amdgcn_alignbyte(w2, w1, 3),
+                       e32 = __builtin_amdgcn_alignbyte(w3, w2, 3), e43 = __builtin_amdgcn_alignbyte(w4, w3, 3);
+        c0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)w0, (int)w1, (int)w2, (int)w3}, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)a10, (int)a21, (int)a32, (int)a43}, c1, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)b10, (int)b21, (int)b32, (int)b43}, c2, 0, 0, 0);
+        c3 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)e10, (int)e21, (int)e32, (int)e43}, c3, 0, 0, 0);
+        c4 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)w1, (int)w2, (int)w3, (int)w4}, c4, 0, 0, 0);
+        c5 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)a21, (int)a32, (int)a43, (int)a54}, c5, 0, 0, 0);
+        c6 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)b21, (int)b32, (int)b43, (int)b54}, c6, 0, 0, 0);
+    }
+    acc[0] = c0; acc[1] = c1; acc[2] = c2; acc[3] = c3; acc[4] = c4; acc[5] = c5; acc[6] = c6;
+}
+
 // MODE (profiling ablations in scripts/roi_microbench.hip; the product uses 0): 2 = no MFMA loop, 3 = no staging
 template <int MODE>
 __global__ __launch_bounds__(256) void k_roi_corr(RoiArgs a) {
@@ -803,31 +935,8 @@ __global__ __launch_bounds__(256) void k_roi_corr(RoiArgs a) {
             int sr = kMmaRows * nt + n;
             if (sr >= nsrc) sr = 0;   // column outside the band: computed, never stored
             const uint8_t* bp = SB + (size_t)sr * SBp + 16 * g;
-            fpm_v4i c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0, c4 = c0, c5 = c0, c6 = c0;
-            for (int k = 0; k < a.nk; ++k) {
-                const fpm_v4i av = *(const fpm_v4i*)__builtin_assume_aligned(ap + 64 * k, 16);
-                const uint8_t* bk = (const uint8_t*)__builtin_assume_aligned(bp + 64 * k, 16);
-                const uint4 lo = *(const uint4*)bk;
-                const uint2 hi = *(const uint2*)(bk + 16);
-                const uint32_t w0 = lo.x, w1 = lo.y, w2 = lo.z, w3 = lo.w, w4 = hi.x, w5 = hi.y;
-                // shift d: bytes [d, d + 16) of w0..w5 (o = d >> 2 words, then alignbyte by d & 3)
-                const uint32_t a10 = __builtin_amdgcn_alignbyte(w1, w0, 1), a21 = __builtin_amdgcn_alignbyte(w2, w1, 1),
-                               a32 = __builtin_amdgcn_alignbyte(w3, w2, 1), a43 = __builtin_amdgcn_alignbyte(w4, w3, 1),
-                               a54 = __builtin_amdgcn_alignbyte(w5, w4, 1);
-                const uint32_t b10 = __builtin_amdgcn_alignbyte(w1, w0, 2), b21 = __builtin_amdgcn_alignbyte(w2, w1, 2),
-                               b32 = __builtin_amdgcn_alignbyte(w3, w2, 2), b43 = __builtin_amdgcn_alignbyte(w4, w3, 2),
-                               b54 = __builtin_amdgcn_alignbyte(w5, w4, 2);
-                const uint32_t e10 = __builtin_amdgcn_alignbyte(w1, w0, 3), e21 = __builtin_amdgcn_alignbyte(w2, w1, 3),
-                               e32 = __builtin_amdgcn_alignbyte(w3, w2, 3), e43 = __builtin_amdgcn_alignbyte(w4, w3, 3);
-                c0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)w0, (int)w1, (int)w2, (int)w3}, c0, 0, 0, 0);
-                c1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)a10, (int)a21, (int)a32, (int)a43}, c1, 0, 0, 0);
-                c2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)b10, (int)b21, (int)b32, (int)b43}, c2, 0, 0, 0);
-                c3 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)e10, (int)e21, (int)e32, (int)e43}, c3, 0, 0, 0);
-                c4 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)w1, (int)w2, (int)w3, (int)w4}, c4, 0, 0, 0);
-                c5 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)a21, (int)a32, (int)a43, (int)a54}, c5, 0, 0, 0);
-                c6 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)b21, (int)b32, (int)b43, (int)b54}, c6, 0, 0, 0);
-            }
-            const fpm_v4i acc[7] = {c0, c1, c2, c3, c4, c5, c6};
+            fpm_v4i acc[7];
+            band_mfma(ap, bp, a.nk, acc);
             // D_dx: col = lane & 15 -> source row 16*nt + n, row = 4*(lane >> 4) + r -> template row 16*mt + 4g + r
             uint32_t* rs_out = a.rowsum + (((size_t)th * 49 + 3) & ~(size_t)3) * slot + (size_t)T0 * 49;
             const uint32_t kFix = 16384u * (uint32_t)tw;
@@ -862,85 +971,431 @@ __global__ __launch_bounds__(256) void k_roi_corr(RoiArgs a) {
     }
 }
 
-// ---- K8: per ROI: ordered f32 fold of the 49 row-sum series (:505-508), window sums, CCOEFF, argmax, 3x3.
-// The [th][49] row sums stream through LDS in blocks of kEvalRows rows; the next block's loads are in flight
-// (registers) while 49 lanes fold the current block in row order.
-constexpr int kEvalRows = 128;
-constexpr int kEvalVec = (kEvalRows * 49 / 4 + 255) / 256;   // uint4 per thread per block
+// One bilinear ROI pixel from a staged footprint, BORDER_CONSTANT(0) rules of remapBilinear (general path).
+__device__ __forceinline__ int ft_tap_general(const uint8_t* FT, int ftw, int bxa, int by0, int W, int H, int X, int Y) {
+    const int sx = sat_s16(X >> kInterBits), sy = sat_s16(Y >> kInterBits);
+    const int fx = X & (kInterTab - 1), fy = Y & (kInterTab - 1);
+    const uint8_t* p = FT + (sy - by0) * ftw + (sx - bxa);
+    int v0, v1, v2, v3;
+    if ((unsigned)sx < (unsigned)(W - 1) && (unsigned)sy < (unsigned)(H - 1)) {
+        v0 = p[0]; v1 = p[1]; v2 = p[ftw]; v3 = p[ftw + 1];
+    } else if (sx >= W || sx + 1 < 0 || sy >= H || sy + 1 < 0) {
+        return 0;
+    } else {
+        const bool x0 = sx >= 0 && sx < W, x1 = sx + 1 >= 0 && sx + 1 < W;
+        const bool y0 = sy >= 0 && sy < H, y1 = sy + 1 >= 0 && sy + 1 < H;
+        v0 = x0 && y0 ? p[0] : 0;
+        v1 = x1 && y0 ? p[1] : 0;
+        v2 = x0 && y1 ? p[ftw] : 0;
+        v3 = x1 && y1 ? p[ftw + 1] : 0;
+    }
+    const int h0 = 32 * v0 + fx * (v1 - v0), h1 = 32 * v2 + fx * (v3 - v2);
+    return (32 * h0 + fy * (h1 - h0) + 512) >> 10;
+}
 
-__global__ __launch_bounds__(256) void k_roi_eval(RoiArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t blk[kEvalRows * 49];
-    __shared__ float sc[64];
-    const int tid = threadIdx.x;
+// ---- K6-K8 for small templates: one workgroup per ROI does the whole refinement of the ROI in LDS (tables,
+// 32x32-tile sampling from wave footprints, exact row / window sums, the band-by-band banded GEMM on the matrix
+// cores, the ordered f32 fold, CCOEFF, argmax, 3x3) and writes its RoiRecord; k_cand_step then steps the
+// candidates.  Used where the ROI, the template and one band of row sums fit the LDS budget (upper layers), so a
+// layer costs two launches instead of four and no scratch leaves the CU.
+struct SmallLayout {
+    int sbp, tbp, rh, u, tab, sum, rs, sc, total;
+};
+__host__ __device__ inline SmallLayout small_layout(int tw, int th) {
+    SmallLayout L;
+    L.sbp = roi_pitch_calc(tw);
+    L.tbp = tmpl_lds_pitch(64 * ((tw + 63) / 64));
+    L.rh = th + 6;
+    const int th16 = (th + kMmaRows - 1) / kMmaRows * kMmaRows;
+    L.u = ((L.rh + 16) * L.sbp + 15) & ~15;       // SB rows + slack rows read by the last band's N tiles
+    const int ub = th16 * L.tbp > 4 * ROI_FT ? th16 * L.tbp : 4 * ROI_FT;
+    L.tab = L.u + ub;
+    L.sum = L.tab + 4 * (2 * L.sbp + 2 * ((L.rh + 3) & ~3));
+    L.rs = L.sum + 4 * (2 * L.rh + 2 * 7 * L.rh) + 8 * 49 * 2;
+    L.sc = L.rs + 4 * kBandRows * 49;
+    L.total = L.sc + 4 * 64;
+    return L;
+}
+constexpr int kSmallLdsMax = 72 * 1024;
+bool roi_small_fits(int tw, int th) { return small_layout(tw, th).total <= kSmallLdsMax; }
+
+__global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int tw = a.tw, th = a.th, RW = tw + 6, RH = th + 6, W = a.W, H = a.H;
+    const SmallLayout LY = small_layout(tw, th);
+    const int SBp = LY.sbp, TBp = LY.tbp;
+    uint8_t* SB = smem;                                  // RH ROI rows x SBp (u8, then ^ 0x80)
+    uint8_t* TB = smem + LY.u;                           // template rows (i8) x TBp
+    uint8_t* FTall = smem + LY.u;                        // (sampling phase) 4 wave footprints
+    int32_t* lad = (int32_t*)(smem + LY.tab);
+    int32_t* lbd = lad + SBp;
+    int32_t* lx0 = lbd + SBp;
+    int32_t* ly0 = lx0 + ((RH + 3) & ~3);
+    uint32_t* rall = (uint32_t*)(smem + LY.sum);
+    uint32_t* rallq = rall + RH;
+    uint32_t* wi = rallq + RH;                           // [row][dx]
+    uint32_t* wq = wi + RH * 7;
+    uint64_t* tot = (uint64_t*)(((uintptr_t)(wq + RH * 7) + 7) & ~(uintptr_t)7);   // [2][49] window totals
+    uint32_t* rs = (uint32_t*)(smem + LY.rs);            // kBandRows x 49 row sums of the current band
+    float* sc = (float*)(smem + LY.sc);
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int rois = roi_count(a);
-    const int th = a.th;
-    const int nblk = (th + kEvalRows - 1) / kEvalRows;
+    const int q4 = SBp >> 4, nwr = (RW + 3) >> 2;
+    const int txn = (RW + ROI_T - 1) / ROI_T, tyn = (RH + ROI_T - 1) / ROI_T;
+    const int g = lane >> 4, n = lane & 15;
+    const int mt = wv & 1, nt = mt + (wv >> 1);
+    const int lr = lane >> 3, lg = lane & 7;
     for (int slot = blockIdx.x; slot < rois; slot += gridDim.x) {
         int id, jj;
         roi_slot(a, slot, id, jj);
-        RoiRecord* out = a.rec + (size_t)id * a.n3 + jj;
-        if (a.equal1) {   // CCOEFF_Denominator: matResult = 1 everywhere (:529-533)
-            if (tid == 0) {
-                out->score = 1.f; out->mx = 0; out->my = 0; out->on_border = 1;
-                for (int k = 0; k < 9; ++k) out->vec[k] = 0.f;
+        const uint8_t* lvl = a.level + (size_t)(id / a.per_source) * a.level_stride;
+        __syncthreads();
+        {   // warpAffine tables of this ROI (getRotatedROI :1074-1090)
+            const CandState st = a.state[id];
+            const AngleNode nd = a.nodes[st.node * a.n3 + jj];
+            double M[6];
+            roi_matrix(W, H, f2(st.lt.x * 2, st.lt.y * 2), nd.c, nd.s, M);
+            for (int x = tid; x < RW; x += 256) {
+                lad[x] = rint_i(M[0] * x * kAbScale);
+                lbd[x] = rint_i(M[3] * x * kAbScale);
             }
-            continue;
-        }
-        const size_t total4 = ((size_t)th * 49 + 3) >> 2;         // uint4 per ROI series (slot stride 4*total4)
-        const uint32_t* rs = a.rowsum + (size_t)slot * total4 * 4;
-        uint64_t s1 = 0, s2 = 0;
-        if (tid < 49) {   // window sums over the chunk partials (independent of the fold)
-            const uint32_t* ws = a.wsum + (size_t)slot * a.nchunk * 49 + tid;
-            const uint64_t* wq = a.wsq + (size_t)slot * a.nchunk * 49 + tid;
-            for (int c = 0; c < a.nchunk; ++c) { s1 += ws[(size_t)c * 49]; s2 += wq[(size_t)c * 49]; }
-        }
-        float accF = 0.f;
-        uint64_t accI = 0;
-        uint4 v[kEvalVec];
-        auto load_block = [&](int b) {
-            const size_t base4 = (size_t)b * (kEvalRows * 49 / 4);
-#pragma unroll
-            for (int i = 0; i < kEvalVec; ++i) {
-                const size_t q = base4 + tid + 256 * i;
-                v[i] = (tid + 256 * i < kEvalRows * 49 / 4 && q < total4) ? ((const uint4*)rs)[q] : make_uint4(0, 0, 0, 0);
+            for (int y = tid; y < RH; y += 256) {
+                lx0[y] = rint_i((M[1] * y + M[2]) * kAbScale) + kRoundDelta;
+                ly0[y] = rint_i((M[4] * y + M[5]) * kAbScale) + kRoundDelta;
             }
-        };
-        load_block(0);
-        for (int b = 0; b < nblk; ++b) {
-            __syncthreads();   // previous block folded
+        }
+        __syncthreads();
+        {   // sample the ROI into SB, one 32x32 tile per wave at a time
+            uint8_t* FT = FTall + wv * ROI_FT;
+            for (int task = wv; task < txn * tyn; task += 4) {
+                const int ty = task / txn, tx = task - ty * txn;
+                const int cx0 = tx * ROI_T, cx1 = min(cx0 + ROI_T, RW) - 1;
+                const int ry0 = ty * ROI_T, ry1 = min(ry0 + ROI_T, RH) - 1;
+                int bx0 = INT_MAX, bx1 = INT_MIN, by0 = INT_MAX, by1 = INT_MIN;
 #pragma unroll
-            for (int i = 0; i < kEvalVec; ++i)
-                if (tid + 256 * i < kEvalRows * 49 / 4) ((uint4*)blk)[tid + 256 * i] = v[i];
-            __syncthreads();
-            if (b + 1 < nblk) load_block(b + 1);
-            const int rows = min(kEvalRows, th - b * kEvalRows);
-            if (tid < 49) {
-                if (a.fold) {
-                    for (int t = 0; t < rows; ++t) accF = accF + (float)(int)blk[t * 49 + tid];   // :507, row order
-                } else {
-                    for (int t = 0; t < rows; ++t) accI += blk[t * 49 + tid];
+                for (int k = 0; k < 4; ++k) {
+                    const int c = (k & 1) ? cx1 : cx0, r = (k & 2) ? ry1 : ry0;
+                    const int X = (lx0[r] + lad[c]) >> (kAbBits - kInterBits);
+                    const int Y = (ly0[r] + lbd[c]) >> (kAbBits - kInterBits);
+                    bx0 = min(bx0, X >> kInterBits); bx1 = max(bx1, X >> kInterBits);
+                    by0 = min(by0, Y >> kInterBits); by1 = max(by1, Y >> kInterBits);
+                }
+                const bool interior = bx0 - 1 >= 0 && bx1 + 1 <= W - 2 && by0 - 1 >= 0 && by1 + 1 <= H - 2;
+                bx0 = max(bx0 - 1, 0); by0 = max(by0 - 1, 0);
+                bx1 = min(bx1 + 2, W - 1); by1 = min(by1 + 2, H - 1);
+                const bool any = bx0 <= bx1 && by0 <= by1;
+                const int bxa = bx0 & ~3;
+                int ftw = any ? ((bx1 - bxa + 4) & ~3) : 0;
+                if (((ftw >> 2) & 1) == 0) ftw += 4;
+                const int fth = any ? by1 - by0 + 1 : 0;
+                const int wpr = ftw >> 2;
+                const bool in_lds = wpr <= 16 && ftw * fth <= ROI_FT;
+                wave_sync();
+                if (any && in_lds) {
+                    const int c = lane & 15;
+                    if (c < wpr) {
+                        const int gx = bxa + 4 * c;
+                        const uint8_t* gsrc = lvl + (size_t)by0 * a.P + gx;
+                        for (int r = lane >> 4; r < fth; r += 4)
+                            *(uint32_t*)(FT + r * ftw + 4 * c) = gx < a.P ? *(const uint32_t*)(gsrc + (size_t)r * a.P) : 0u;
+                    }
+                }
+                wave_sync();
+                const int c0 = cx0 + 4 * lg;
+                if (c0 > cx1) continue;
+                for (int i = 0; i < 4; ++i) {
+                    const int r = ry0 + lr + 8 * i;
+                    if (r > ry1) break;
+                    const int X0 = lx0[r], Y0 = ly0[r];
+                    uint32_t pk = 0;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int X = (X0 + lad[c0 + u]) >> (kAbBits - kInterBits);
+                        const int Y = (Y0 + lbd[c0 + u]) >> (kAbBits - kInterBits);
+                        int v;
+                        if (interior && in_lds) {
+                            const int fx = X & (kInterTab - 1), fy = Y & (kInterTab - 1);
+                            const uint8_t* p = FT + __mul24((Y >> kInterBits) - by0, ftw) + ((X >> kInterBits) - bxa);
+                            const int v0 = p[0], v1 = p[1], v2 = p[ftw], v3 = p[ftw + 1];
+                            const int h0 = 32 * v0 + __mul24(fx, v1 - v0), h1 = 32 * v2 + __mul24(fx, v3 - v2);
+                            v = (32 * h0 + __mul24(fy, h1 - h0) + 512) >> 10;
+                        } else {
+                            v = in_lds ? ft_tap_general(FT, ftw, bxa, by0, W, H, X, Y) : roi_tap(lvl, W, H, a.P, X, Y);
+                        }
+                        if (c0 + u >= RW) v = 0;
+                        pk |= (uint32_t)v << (8 * u);
+                    }
+                    *(uint32_t*)(SB + r * SBp + c0) = pk;
                 }
             }
         }
-        if (tid < 49) {
-            const double num = a.fold ? (double)accF : (double)(float)(double)accI;
-            sc[tid] = ccoeff(num, (double)s1, (double)s2, a.mean, a.norm, a.inv_area);
+        __syncthreads();
+        for (int r = wv; r < RH; r += 4) {   // exact full-row sums, bytes flipped to the signed MFMA operand
+            uint32_t s1 = 0, s2 = 0;
+            for (int c = lane; c < q4; c += 64) {
+                uint4 v = *(uint4*)(SB + (size_t)r * SBp + 16 * c);
+                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t x = 4 * c + k < nwr ? w4[k] : 0u;
+                    s1 = __builtin_amdgcn_udot4(x, 0x01010101u, s1, false);
+                    s2 = __builtin_amdgcn_udot4(x, x, s2, false);
+                }
+                v.x ^= 0x80808080u; v.y ^= 0x80808080u; v.z ^= 0x80808080u; v.w ^= 0x80808080u;
+                *(uint4*)(SB + (size_t)r * SBp + 16 * c) = v;
+            }
+            s1 = wave_sum_u32(s1);
+            s2 = wave_sum_u32(s2);
+            if (lane == 0) { rall[r] = s1; rallq[r] = s2; }
+        }
+        {   // all template rows (padded to 16) of the i8 slab
+            const int trows = (th + kMmaRows - 1) / kMmaRows * kMmaRows, tq = a.tp8 >> 4;
+            for (int i = tid; i < trows * tq; i += 256) {
+                const int r = i / tq, c = i - r * tq;
+                *(uint4*)(TB + (size_t)r * TBp + 16 * c) = *(const uint4*)((const uint8_t*)a.tmpl8 + (size_t)r * a.tp8 + 16 * c);
+            }
         }
         __syncthreads();
-        if (tid == 0) {
+        for (int i = tid; i < RH * 7; i += 256) {   // window [dx, dx + tw) of every row
+            const int r = i / 7, dx = i - r * 7;
+            const uint8_t* sbr = SB + (size_t)r * SBp;
+            uint32_t q1 = rall[r], q2 = rallq[r];
+            for (int c = 0; c < dx; ++c) { const uint32_t v = sbr[c] ^ 0x80u; q1 -= v; q2 -= v * v; }
+            for (int c = dx + tw; c < RW; ++c) { const uint32_t v = sbr[c] ^ 0x80u; q1 -= v; q2 -= v * v; }
+            wi[i] = q1;
+            wq[i] = q2;
+        }
+        __syncthreads();
+        if (tid < 49) {   // window totals of the 49 positions (exact)
+            const int pdy = tid / 7, ddx = tid - pdy * 7;
+            uint64_t s1 = 0, s2 = 0;
+            for (int t = 0; t < th; ++t) { s1 += wi[(t + pdy) * 7 + ddx]; s2 += wq[(t + pdy) * 7 + ddx]; }
+            tot[tid] = s1;
+            tot[49 + tid] = s2;
+        }
+        float accF = 0.f;
+        uint64_t accI = 0;
+        const uint32_t kFix = 16384u * (uint32_t)tw;
+        for (int T0 = 0; T0 < th; T0 += kBandRows) {   // bands in row order: MFMA -> LDS row sums -> fold
+            const int rb = min(kBandRows, th - T0), nsrc = rb + 6;
+            if (kMmaRows * mt < rb && kMmaRows * nt < nsrc) {
+                const uint8_t* ap = TB + (size_t)(T0 + kMmaRows * mt + n) * TBp + 16 * g;
+                const uint8_t* bp = SB + (size_t)(T0 + kMmaRows * nt + n) * SBp + 16 * g;   // slack rows cover sr >= RH
+                fpm_v4i acc[7];
+                band_mfma(ap, bp, a.nk, acc);
+                const int s_ = kMmaRows * nt + n;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int t = kMmaRows * mt + 4 * g + r, dy = s_ - t;
+                    if (t < rb && s_ < nsrc && dy >= 0 && dy < 7) {
+                        const uint32_t ts = (uint32_t)a.tsum[T0 + t];
+#pragma unroll
+                        for (int d = 0; d < 7; ++d)
+                            rs[t * 49 + dy * 7 + d] = (uint32_t)acc[d][r] + 128u * (wi[(T0 + s_) * 7 + d] + ts) - kFix;
+                    }
+                }
+            }
+            __syncthreads();
+            if (tid < 49) {
+                if (a.fold) {
+                    for (int t = 0; t < rb; ++t) accF = accF + (float)(int)rs[t * 49 + tid];   // :507, row order
+                } else {
+                    for (int t = 0; t < rb; ++t) accI += rs[t * 49 + tid];
+                }
+            }
+            __syncthreads();
+        }
+        if (tid < 49) {
+            const double num = a.fold ? (double)accF : (double)(float)(double)accI;
+            sc[tid] = ccoeff(num, (double)tot[tid], (double)tot[49 + tid], a.mean, a.norm, a.inv_area);
+        }
+        __syncthreads();
+        if (tid == 0) {   // cv::minMaxLoc: first maximum in row-major order
             float best = sc[0];
             int bi = 0;
             for (int k = 1; k < 49; ++k)
                 if (sc[k] > best) { best = sc[k]; bi = k; }
             const int mx = bi % 7, my = bi / 7;
-            out->score = best;
-            out->mx = (int16_t)mx;
-            out->my = (int16_t)my;
+            RoiRecord r;
+            r.score = best;
+            r.mx = (int16_t)mx;
+            r.my = (int16_t)my;
             const int border = (mx == 0 || my == 0 || mx == 6 || my == 6) ? 1 : 0;
-            out->on_border = border;
+            r.on_border = border;
             for (int x = -1; x <= 1; ++x)
-                for (int y = -1; y <= 1; ++y)
-                    out->vec[(x + 1) * 3 + (y + 1)] = border ? 0.f : sc[(my + y) * 7 + (mx + x)];
+                for (int y = -1; y <= 1; ++y) r.vec[(x + 1) * 3 + (y + 1)] = border ? 0.f : sc[(my + y) * 7 + (mx + x)];
+            a.rec[(size_t)id * a.n3 + jj] = r;
+        }
+    }
+}
+
+// candidate step of :329-366 from the n3 records of each live candidate (after k_roi_small)
+__global__ __launch_bounds__(256) void k_cand_step(RoiArgs a) {
+    const int n = *a.live_count;
+    for (int li = blockIdx.x * 256 + threadIdx.x; li < n; li += gridDim.x * 256) {
+        const int id = a.live[li];
+        CandState s = a.state[id];
+        const RoiRecord* r = a.rec + (size_t)id * a.n3;
+        int imax = 0;
+        double big = -1;
+        for (int k = 0; k < a.n3; ++k)
+            if ((double)r[k].score > big) { imax = k; big = r[k].score; }
+        if ((double)r[imax].score < a.thr) {   // :331-332
+            s.alive = 0;
+            a.state[id] = s;
+            continue;
+        }
+        const int child = s.node * a.n3 + imax;
+        const AngleNode nd = a.nodes[child];
+        const F2 sc = f2((a.W - 1) / 2.0f, (a.H - 1) / 2.0f);
+        const F2 r0 = rotate_pt(f2(s.lt.x * 2, s.lt.y * 2), sc, nd.c, nd.s);   // :350-353
+        const F2 pad = f2(r0.x - 3, r0.y - 3);
+        F2 p = f2((float)((double)r[imax].mx + pad.x), (float)((double)r[imax].my + pad.y));
+        p = rotate_pt(p, sc, nd.cn, nd.sn);
+        s.lt = p;          // :366
+        s.node = child;    // :363
+        s.reached0 = a.mark_reached0;
+        a.state[id] = s;
+        a.live_out[atomicAdd(a.live_out_count, 1)] = id;
+    }
+}
+
+// ---- K8: per live candidate (one wave per refinement angle j): ordered f32 fold of the ROI's 49 row-sum series
+// (:505-508), window sums, CCOEFF, argmax, border, 3x3 -> RoiRecord; then (layers > 0) the candidate step of
+// :329-366: best of the n3 angles, early break below vecLayerScore, back-mapping of ptLT, append to the next live
+// list.  Each wave streams its [th][49] series through wave-private LDS in blocks of kEvalRows rows, the next
+// block's loads in flight while 49 lanes fold the current one in row order.  No workgroup barrier in the loop.
+constexpr int kEvalRows = 64;
+constexpr int kEvalVec = (kEvalRows * 49 / 4 + 63) / 64;   // uint4 per lane per block
+
+__device__ void eval_roi(const RoiArgs& a, int slot, int lane, uint32_t* blk, float* sc, RoiRecord* out,
+                         RoiRecord* keep) {
+    const int th = a.th;
+    if (a.equal1) {   // CCOEFF_Denominator: matResult = 1 everywhere (:529-533)
+        if (lane == 0) {
+            RoiRecord r;
+            r.score = 1.f; r.mx = 0; r.my = 0; r.on_border = 1;
+            for (int k = 0; k < 9; ++k) r.vec[k] = 0.f;
+            *out = r;
+            *keep = r;
+        }
+        return;
+    }
+    const size_t total4 = ((size_t)th * 49 + 3) >> 2;   // uint4 per ROI series (slot stride 4 * total4)
+    const uint4* rs = (const uint4*)(a.rowsum + (size_t)slot * total4 * 4);
+    uint64_t s1 = 0, s2 = 0;
+    if (lane < 49) {   // window sums over the chunk partials
+        const uint32_t* ws = a.wsum + (size_t)slot * a.nchunk * 49 + lane;
+        const uint64_t* wq = a.wsq + (size_t)slot * a.nchunk * 49 + lane;
+        int c = 0;
+        for (; c + 8 <= a.nchunk; c += 8) {
+            uint32_t x[8];
+            uint64_t y[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) { x[u] = ws[(size_t)(c + u) * 49]; y[u] = wq[(size_t)(c + u) * 49]; }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) { s1 += x[u]; s2 += y[u]; }
+        }
+        for (; c < a.nchunk; ++c) { s1 += ws[(size_t)c * 49]; s2 += wq[(size_t)c * 49]; }
+    }
+    constexpr int BQ = kEvalRows * 49 / 4;   // uint4 per block
+    const int nblk = (th + kEvalRows - 1) / kEvalRows;
+    uint4 v[kEvalVec];
+    auto load_block = [&](int b) {
+#pragma unroll
+        for (int i = 0; i < kEvalVec; ++i) {
+            const size_t q = (size_t)b * BQ + lane + 64 * i;
+            v[i] = (lane + 64 * i < BQ && q < total4) ? rs[q] : make_uint4(0, 0, 0, 0);
+        }
+    };
+    float accF = 0.f;
+    uint64_t accI = 0;
+    load_block(0);
+    for (int b = 0; b < nblk; ++b) {
+        wave_sync();   // previous block folded
+#pragma unroll
+        for (int i = 0; i < kEvalVec; ++i)
+            if (lane + 64 * i < BQ) ((uint4*)blk)[lane + 64 * i] = v[i];
+        wave_sync();
+        if (b + 1 < nblk) load_block(b + 1);
+        const int rows = min(kEvalRows, th - b * kEvalRows);
+        if (lane < 49) {
+            if (a.fold) {
+                int t = 0;
+                for (; t + 8 <= rows; t += 8) {   // 8 LDS reads in flight, adds in row order (:507)
+                    uint32_t x[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) x[u] = blk[(t + u) * 49 + lane];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) accF = accF + (float)(int)x[u];
+                }
+                for (; t < rows; ++t) accF = accF + (float)(int)blk[t * 49 + lane];
+            } else {
+                for (int t = 0; t < rows; ++t) accI += blk[t * 49 + lane];
+            }
+        }
+    }
+    if (lane < 49) {
+        const double num = a.fold ? (double)accF : (double)(float)(double)accI;
+        sc[lane] = ccoeff(num, (double)s1, (double)s2, a.mean, a.norm, a.inv_area);
+    }
+    wave_sync();
+    if (lane == 0) {   // cv::minMaxLoc: first maximum in row-major order
+        float best = sc[0];
+        int bi = 0;
+        for (int k = 1; k < 49; ++k)
+            if (sc[k] > best) { best = sc[k]; bi = k; }
+        const int mx = bi % 7, my = bi / 7;
+        RoiRecord r;
+        r.score = best;
+        r.mx = (int16_t)mx;
+        r.my = (int16_t)my;
+        const int border = (mx == 0 || my == 0 || mx == 6 || my == 6) ? 1 : 0;
+        r.on_border = border;
+        for (int x = -1; x <= 1; ++x)
+            for (int y = -1; y <= 1; ++y) r.vec[(x + 1) * 3 + (y + 1)] = border ? 0.f : sc[(my + y) * 7 + (mx + x)];
+        *out = r;
+        *keep = r;
+    }
+}
+
+__global__ __launch_bounds__(192) void k_roi_eval(RoiArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t blk_all[3][kEvalRows * 49];
+    __shared__ float sc_all[3][64];
+    __shared__ RoiRecord recs[3];
+    const int lane = threadIdx.x & 63, j = threadIdx.x >> 6;   // wave j <-> refinement angle j
+    const int rois = roi_count(a);
+    const int c_lo = a.slot_base / a.n3, c_hi = (a.slot_base + rois) / a.n3;   // rounds hold whole candidates
+    for (int li = c_lo + blockIdx.x; li < c_hi; li += gridDim.x) {
+        const int id = a.live[li];
+        const int slot = li * a.n3 + j - a.slot_base;
+        __syncthreads();   // previous candidate's records consumed
+        eval_roi(a, slot, lane, blk_all[j], sc_all[j], a.rec + (size_t)id * a.n3 + j, &recs[j]);
+        if (!a.step) continue;
+        __syncthreads();
+        if (threadIdx.x == 0) {   // TemplateMatcher.cpp:329-366
+            CandState s = a.state[id];
+            int imax = 0;
+            double big = -1;
+            for (int k = 0; k < a.n3; ++k)
+                if ((double)recs[k].score > big) { imax = k; big = recs[k].score; }
+            if ((double)recs[imax].score < a.thr) {   // :331-332
+                s.alive = 0;
+                a.state[id] = s;
+            } else {
+                const int child = s.node * a.n3 + imax;
+                const AngleNode nd = a.nodes[child];
+                const F2 sc = f2((a.W - 1) / 2.0f, (a.H - 1) / 2.0f);
+                const F2 r0 = rotate_pt(f2(s.lt.x * 2, s.lt.y * 2), sc, nd.c, nd.s);   // :350-353
+                const F2 pad = f2(r0.x - 3, r0.y - 3);
+                F2 p = f2((float)((double)recs[imax].mx + pad.x), (float)((double)recs[imax].my + pad.y));
+                p = rotate_pt(p, sc, nd.cn, nd.sn);
+                s.lt = p;          // :366
+                s.node = child;    // :363 (angle = node angle)
+                s.reached0 = a.mark_reached0;
+                a.state[id] = s;
+                a.live_out[atomicAdd(a.live_out_count, 1)] = id;
+            }
         }
     }
 }
@@ -981,45 +1436,31 @@ void launch_roi_corr(const RoiArgs& a, hipStream_t st) {
 
 void launch_roi_eval(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0) return;
-    const int grid = a.slot_cap < 4096 ? a.slot_cap : 4096;
-    hipLaunchKernelGGL(k_roi_eval, dim3(grid), dim3(256), 0, st, a);
+    const int cands = (a.slot_cap + a.n3 - 1) / a.n3;
+    const int grid = cands < 4096 ? cands : 4096;
+    hipLaunchKernelGGL(k_roi_eval, dim3(grid), dim3(64 * a.n3), 0, st, a);
 }
 
-// ============================================================================================== step
-__global__ __launch_bounds__(256) void k_cand_step(StepArgs a) {
-    const int n = *a.live_in_count;
-    for (int li = blockIdx.x * 256 + threadIdx.x; li < n; li += gridDim.x * 256) {
-        const int id = a.live_in[li];
-        CandState s = a.state[id];
-        const RoiRecord* r = a.rec + (size_t)id * a.n3;
-        int imax = 0;
-        double big = -1;
-        for (int j = 0; j < a.n3; ++j)
-            if ((double)r[j].score > big) { imax = j; big = r[j].score; }
-        if ((double)r[imax].score < a.thr) {   // :331-332
-            s.alive = 0;
-            a.state[id] = s;
-            continue;
-        }
-        const int child = s.node * a.n3 + imax;
-        const AngleNode nd = a.nodes[child];
-        const F2 sc = f2((a.W - 1) / 2.0f, (a.H - 1) / 2.0f);
-        // :350-353
-        const F2 r0 = rotate_pt(f2(s.lt.x * 2, s.lt.y * 2), sc, nd.c, nd.s);
-        const F2 pad = f2(r0.x - 3, r0.y - 3);
-        F2 p = f2((float)((double)r[imax].mx + pad.x), (float)((double)r[imax].my + pad.y));
-        p = rotate_pt(p, sc, nd.cn, nd.sn);
-        s.lt = p;          // :366
-        s.node = child;    // :363 (angle = node angle)
-        s.reached0 = a.mark_reached0;
-        a.state[id] = s;
-        const int slot = atomicAdd(a.live_out_count, 1);
-        a.live_out[slot] = id;
+void launch_roi_small(const RoiArgs& a, hipStream_t st) {
+    if (a.slot_cap <= 0) return;
+    if (a.equal1) {   // records of ones (CCOEFF_Denominator :529-533); the step follows in k_cand_step
+        RoiArgs b = a;
+        b.step = 0;
+        launch_roi_eval(b, st);
+        return;
     }
+    const size_t lds = (size_t)small_layout(a.tw, a.th).total;
+    static size_t lds_attr = 0;
+    if (lds > 65536 && lds > lds_attr) {
+        (void)hipFuncSetAttribute((const void*)k_roi_small, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        lds_attr = lds;
+    }
+    const int grid = a.slot_cap < 8192 ? a.slot_cap : 8192;
+    hipLaunchKernelGGL(k_roi_small, dim3(grid), dim3(256), lds, st, a);
 }
 
-void launch_cand_step(const StepArgs& a, int max_items, hipStream_t st) {
-    if (max_items <= 0) return;
+void launch_cand_step(const RoiArgs& a, int max_items, hipStream_t st) {
+    if (max_items <= 0 || !a.step) return;
     int grid = (max_items + 255) / 256;
     if (grid > 1024) grid = 1024;
     hipLaunchKernelGGL(k_cand_step, dim3(grid), dim3(256), 0, st, a);

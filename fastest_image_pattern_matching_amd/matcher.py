@@ -66,7 +66,8 @@ class TemplateMatcher:
         self._lib.fpm_params_default(C.byref(self._params))
         self._last_time = 0.0
         self._user_rect = None
-        self._cap = 4096
+        self._cap = 64                 # results per source; grown on FPM_E_CAPACITY
+        self._bufs = None              # reusable ctypes result buffers for match_staged
 
     def __del__(self):
         ctx = getattr(self, "_ctx", None)
@@ -146,8 +147,9 @@ class TemplateMatcher:
         n_src = self._staged
         self._push()
         while True:
-            out = (L.Result * (self._cap * n_src))()
-            n = (C.c_int32 * n_src)()
+            if self._bufs is None or self._bufs[0] != (n_src, self._cap):
+                self._bufs = ((n_src, self._cap), (L.Result * (self._cap * n_src))(), (C.c_int32 * n_src)())
+            _, out, n = self._bufs
             rc = self._check(self._lib.fpm_match_staged(self._ctx, out, self._cap, n), "match_staged")
             if rc == L.FPM_E_CAPACITY:
                 self._cap = max(self._cap * 2, max(n))

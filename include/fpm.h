@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define FPM_ABI_VERSION 1
+#define FPM_ABI_VERSION 2
 
 /* status codes */
 #define FPM_OK 0
@@ -136,9 +136,9 @@ int fpm_search_stats(const fpm_ctx* ctx, int64_t* stats, int32_t cap);
 #define FPM_K_TOP_NCC 2    /* K3+K4 top-layer CCORR + normalisation                        */
 #define FPM_K_TOP_NMS 3    /* K5 peak extraction                                           */
 #define FPM_K_ROI_WARP 4   /* K6 refinement ROI tables + LDS-staged bilinear sampling      */
-#define FPM_K_ROI_CORR 5   /* K7 refinement per-row int32 correlation + window sums        */
-#define FPM_K_ROI_EVAL 6   /* K8 row fold + normalisation + argmax + 3x3                   */
-#define FPM_K_CAND 7       /* candidate init / best-of-3 / early break / back-mapping      */
+#define FPM_K_ROI_CORR 5   /* K7 refinement row correlation (i8 MFMA) + window sums        */
+#define FPM_K_ROI_EVAL 6   /* K8 row fold + normalisation + argmax + 3x3 + candidate step  */
+#define FPM_K_CAND 7       /* candidate init from the top-layer peaks                      */
 #define FPM_K_COUNT 8
 int fpm_profile_enable(fpm_ctx* ctx, int32_t enable);
 int fpm_profile_reset(fpm_ctx* ctx);

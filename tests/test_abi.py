@@ -44,7 +44,8 @@ def test_defaults_equal_reference_constructor(fpm_lib):
 
 
 def test_abi_version(fpm_lib):
-    assert fpm_lib.fpm_abi_version() == 1
+    hdr = open(os.path.join(REPO, "include", "fpm.h")).read()
+    assert fpm_lib.fpm_abi_version() == int(re.search(r"#define FPM_ABI_VERSION (\d+)", hdr).group(1))
 
 
 def test_null_arguments_are_rejected_without_a_device(fpm_lib):

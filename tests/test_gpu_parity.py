@@ -90,6 +90,23 @@ def test_ncc_map_all_layers(hip, templates, fold):
         assert np.array_equal(hip.ncc_map(img, layer, fold), o.ncc_map(img, layer, fold)), layer
 
 
+@pytest.mark.parametrize("shape", [(48, 63), (150, 200), (77, 131)])
+def test_ncc_map_tiled_multi_tile(hip, templates, shape):
+    """The LDS-tiled top-layer NCC over maps spanning several (and partial) 64 x 16 tiles, TM_CCORR and fold."""
+    t = templates["Dst7"]
+    hip.setMinReduceArea(256)
+    hip.learnPattern(t)
+    o = oracle.OracleMatcher()
+    o.learnPattern(t)
+    levels, _ = o.template_levels()
+    top = len(levels) - 1
+    rng = np.random.default_rng(shape[0] * 7 + shape[1])
+    img = rng.integers(0, 256, shape, dtype=np.uint8)
+    img[10:10 + levels[top][0].shape[0], 20:20 + levels[top][0].shape[1]] = levels[top][0]
+    for fold in (False, True):
+        assert np.array_equal(hip.ncc_map(img, top, fold), o.ncc_map(img, top, fold)), (shape, fold)
+
+
 # ---------------------------------------------------------------------------------------------------- search
 def _scene_rotated(templates, name, poses, size, seed, bg=(128, 10)):
     t = templates[name]
