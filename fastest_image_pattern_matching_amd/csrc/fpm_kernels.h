@@ -123,6 +123,7 @@ struct RoiArgs {
     int32_t* live_out;
     int32_t* live_out_count;
     double thr;              // vecLayerScore[layer]
+    uint64_t* stamps;        // profiling ablations only (scripts/roi_microbench.hip): per-phase s_memtime stamps
 };
 
 
@@ -140,6 +141,7 @@ void launch_roi_warp(const RoiArgs& a, hipStream_t st);
 void launch_roi_corr(const RoiArgs& a, hipStream_t st);
 void launch_roi_eval(const RoiArgs& a, hipStream_t st);
 bool roi_small_fits(int tw, int th);   // the single-kernel small-template refinement applies
+size_t roi_small_lds(int tw, int th);
 void launch_roi_small(const RoiArgs& a, hipStream_t st);
 void launch_cand_step(const RoiArgs& a, int max_items, hipStream_t st);
 int roi_pick_rc(int tw, int th);

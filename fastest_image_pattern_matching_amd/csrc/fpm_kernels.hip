@@ -610,6 +610,74 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Global -> LDS staging with several loads in flight per thread (a load-then-store loop would otherwise wait one
+// full memory round trip per iteration).
+// (a) footprint rows of a tile: lane -> word column lane & 15 (< wpr), rows (lane >> 4) + 4i
+template <int B>
+__device__ __forceinline__ void stage_footprint(uint8_t* FT, int ftw, int wpr, int fth, const uint8_t* gsrc,
+                                                size_t gpitch, int gx0, int gP, int lane) {
+    const int c = lane & 15;
+    if (c >= wpr) return;
+    const int gx = gx0 + 4 * c;
+    const bool inb = gx < gP;
+    const uint8_t* gp = gsrc + 4 * c + (size_t)(lane >> 4) * gpitch;
+    uint8_t* lp = FT + 4 * c + (lane >> 4) * ftw;
+    const size_t gstep = 4 * gpitch;
+    const int lstep = 4 * ftw;
+    for (int r0 = lane >> 4; r0 < fth; r0 += 4 * B) {   // B rows' loads in flight (VGPRs vs occupancy)
+        uint32_t v[B];
+#pragma unroll
+        for (int i = 0; i < B; ++i) v[i] = (inb && r0 + 4 * i < fth) ? *(const uint32_t*)(gp + i * gstep) : 0u;
+#pragma unroll
+        for (int i = 0; i < B; ++i)
+            if (r0 + 4 * i < fth) *(uint32_t*)(lp + i * lstep) = v[i];
+        gp += B * gstep;
+        lp += B * lstep;
+    }
+}
+// (b) a rows x q16 block of 16-byte vectors (workgroup-wide, nthr threads): dst pitch dp, src pitch sp
+__device__ __forceinline__ void stage_block16(uint8_t* dst, int dp, const uint8_t* src, size_t sp, int rows, int q16,
+                                              int tid, int nthr) {
+    const int total = rows * q16;
+    int r = tid / q16, c = tid - (tid / q16) * q16;     // (r, c) of element tid, advanced by nthr per step
+    const int dr = nthr / q16, dc = nthr - dr * q16;
+    for (int i0 = tid; i0 < total; i0 += 4 * nthr) {
+        uint4 v[4];
+        int rr[4], cc[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            rr[k] = r; cc[k] = c;
+            v[k] = (i0 + k * nthr < total) ? *(const uint4*)(src + (size_t)r * sp + 16 * c) : make_uint4(0, 0, 0, 0);
+            r += dr; c += dc;
+            if (c >= q16) { c -= q16; ++r; }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (i0 + k * nthr < total) *(uint4*)(dst + (size_t)rr[k] * dp + 16 * cc[k]) = v[k];
+    }
+}
+// (c) a rows x wpr block of dwords (workgroup-wide), zero where the source column gx0 + 4c >= gP
+__device__ __forceinline__ void stage_block4(uint8_t* dst, int dp, const uint8_t* src, size_t sp, int rows, int wpr,
+                                             int gx0, int gP, int tid, int nthr) {
+    const int total = rows * wpr;
+    int r = tid / wpr, c = tid - (tid / wpr) * wpr;
+    const int dr = nthr / wpr, dc = nthr - dr * wpr;
+    for (int i0 = tid; i0 < total; i0 += 8 * nthr) {
+        uint32_t v[8];
+        int rr[8], cc[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            rr[k] = r; cc[k] = c;
+            v[k] = (i0 + k * nthr < total && gx0 + 4 * c < gP) ? *(const uint32_t*)(src + (size_t)r * sp + 4 * c) : 0u;
+            r += dr; c += dc;
+            if (c >= wpr) { c -= wpr; ++r; }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (i0 + k * nthr < total) *(uint32_t*)(dst + (size_t)rr[k] * dp + 4 * cc[k]) = v[k];
+    }
+}
+
 // ---- K6a: per-ROI fixed-point warp tables (getRotatedROI -> warpAffine's adelta/bdelta/X0/Y0) and, from them,
 // one descriptor per 32x32 ROI tile: the tile's source footprint box (corner samples +-1 px: the fixed-point map
 // is two roundings of a linear map, so every pixel's tap lies within the corners' range +-1) and flags
@@ -680,6 +748,7 @@ __global__ __launch_bounds__(256) void k_roi_tables(RoiArgs a) {
 // together; the tile's source footprint is staged into wave-private LDS with dword loads; every lane produces
 // 4 rows x 4 pixels by gathering the bilinear taps from LDS and stores them as dwords.  Interior tiles take a
 // branch-free path; others follow remapBilinear's BORDER_CONSTANT(0) rules per pixel.  No workgroup barrier.
+template <int FB>
 __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t ft_all[4][ROI_FT];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -715,15 +784,7 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
         const bool in_lds = (flags & kTileLds) != 0;
         const int wpr = ftw >> 2;
         wave_sync();   // previous task's gathers are done with FT
-        if ((flags & kTileAny) && in_lds) {   // lane -> word column lane & 15, rows (lane >> 4) + 4i
-            const int c = lane & 15;
-            if (c < wpr) {
-                const int gx = bxa + 4 * c;
-                const uint8_t* gsrc = lvl + (size_t)by0 * a.P + gx;
-                for (int r = lane >> 4; r < fth; r += 4)
-                    *(uint32_t*)(FT + r * ftw + 4 * c) = gx < a.P ? *(const uint32_t*)(gsrc + (size_t)r * a.P) : 0u;
-            }
-        }
+        if ((flags & kTileAny) && in_lds) stage_footprint<FB>(FT, ftw, wpr, fth, lvl + (size_t)by0 * a.P + bxa, a.P, bxa, a.P, lane);
         wave_sync();
         if (c0 > cx1) continue;
         const int adv[4] = {A.x, A.y, A.z, A.w}, bdv[4] = {B.x, B.y, B.z, B.w};
@@ -874,11 +935,11 @@ __global__ __launch_bounds__(256) void k_roi_corr(RoiArgs a) {
         __syncthreads();   // previous item done with SB / wi
         if (tid < kBandSrc) { rall[tid] = 0; rallq[tid] = 0; }
         __syncthreads();
-        if (MODE != 3) {   // stage: wave wv stages rows wv + 4i; row sums by wave reduction
+        if (MODE != 3) {   // stage: wave wv stages rows wv + 4i (kStageBatch rows' loads in flight), bytes ^ 0x80
             const uint8_t* rsrc = a.roi + (size_t)slot * a.roi_stride + (size_t)T0 * a.roi_pitch;
             for (int c0 = 0; c0 < q4; c0 += 64) {
                 const int c = c0 + lane;
-                for (int i0 = 0; i0 < kStageRows; i0 += kStageBatch) {   // kStageBatch rows' loads in flight
+                for (int i0 = 0; i0 < kStageRows; i0 += kStageBatch) {
                     uint4 v[kStageBatch];
 #pragma unroll
                     for (int i = 0; i < kStageBatch; ++i) {
@@ -889,34 +950,43 @@ __global__ __launch_bounds__(256) void k_roi_corr(RoiArgs a) {
 #pragma unroll
                     for (int i = 0; i < kStageBatch; ++i) {
                         const int r = wv + 4 * (i0 + i);
-                        if (r >= nsrc) break;   // wave-uniform
-                        uint32_t s1 = 0, s2 = 0;
-                        const uint32_t w4[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            const uint32_t x = 4 * c + k < nwr ? w4[k] : 0u;
-                            s1 = __builtin_amdgcn_udot4(x, 0x01010101u, s1, false);
-                            s2 = __builtin_amdgcn_udot4(x, x, s2, false);
-                        }
-                        if (c < q4) {
+                        if (r < nsrc && c < q4) {
                             uint4 x = v[i];
                             x.x ^= 0x80808080u; x.y ^= 0x80808080u; x.z ^= 0x80808080u; x.w ^= 0x80808080u;
                             *(uint4*)(SB + (size_t)r * SBp + 16 * c) = x;
                         }
-                        s1 = wave_sum_u32(s1);
-                        s2 = wave_sum_u32(s2);
-                        if (lane == 0) { rall[r] += s1; rallq[r] += s2; }
                     }
                 }
             }
         }
-        {   // template rows T0 .. T0 + 16*ceil(rb/16) - 1 of the i8 slab
-            const int trows = (rb + kMmaRows - 1) / kMmaRows * kMmaRows, tq = a.tp8 >> 4;
-            const uint8_t* tsrc = (const uint8_t*)a.tmpl8 + (size_t)T0 * a.tp8;
-            for (int i = tid; i < trows * tq; i += 256) {
-                const int r = i / tq, c = i - r * tq;
-                *(uint4*)(TB + (size_t)r * TBp + 16 * c) = *(const uint4*)(tsrc + (size_t)r * a.tp8 + 16 * c);
+        __syncthreads();
+        if (tid < 4 * nsrc) {   // exact full-row sums of I and I^2: thread (row, quarter of the row's words)
+            const int r = tid >> 2, qq = tid & 3;
+            const int per = (nwr + 3) >> 2, k0 = qq * per, k1 = min(nwr, k0 + per);
+            const uint32_t* row = (const uint32_t*)(SB + (size_t)r * SBp);
+            uint32_t s1 = 0, s2 = 0;
+            int k = k0;
+            for (; k + 8 <= k1; k += 8) {
+                uint32_t x[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) x[u] = row[k + u] ^ 0x80808080u;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    s1 = __builtin_amdgcn_udot4(x[u], 0x01010101u, s1, false);
+                    s2 = __builtin_amdgcn_udot4(x[u], x[u], s2, false);
+                }
             }
+            for (; k < k1; ++k) {
+                const uint32_t x = row[k] ^ 0x80808080u;
+                s1 = __builtin_amdgcn_udot4(x, 0x01010101u, s1, false);
+                s2 = __builtin_amdgcn_udot4(x, x, s2, false);
+            }
+            atomicAdd(&rall[r], s1);
+            atomicAdd(&rallq[r], s2);
+        }
+        {   // template rows T0 .. T0 + 16*ceil(rb/16) - 1 of the i8 slab
+            const int trows = (rb + kMmaRows - 1) / kMmaRows * kMmaRows;
+            stage_block16(TB, TBp, (const uint8_t*)a.tmpl8 + (size_t)T0 * a.tp8, a.tp8, trows, a.tp8 >> 4, tid, 256);
         }
         __syncthreads();
         for (int i = tid; i < nsrc * 7; i += 256) {   // window [dx, dx + tw): full row minus <= 6 edge pixels
@@ -1018,7 +1088,11 @@ __host__ __device__ inline SmallLayout small_layout(int tw, int th) {
 }
 constexpr int kSmallLdsMax = 72 * 1024;
 bool roi_small_fits(int tw, int th) { return small_layout(tw, th).total <= kSmallLdsMax; }
+size_t roi_small_lds(int tw, int th) { return (size_t)small_layout(tw, th).total; }
 
+// MODE (profiling ablations in scripts/roi_microbench.hip; the product uses 0): 1 = tables + sampling only,
+// 2 = + row / window sums, 3 = + bands without the fold, 9 = full with per-phase s_memtime stamps (a.stamps)
+template <int MODE>
 __global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tw = a.tw, th = a.th, RW = tw + 6, RH = th + 6, W = a.W, H = a.H;
@@ -1045,7 +1119,11 @@ __global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
     const int g = lane >> 4, n = lane & 15;
     const int mt = wv & 1, nt = mt + (wv >> 1);
     const int lr = lane >> 3, lg = lane & 7;
+    auto STAMP = [&](int k) {
+        if (MODE == 9 && tid == 0 && blockIdx.x < 64) a.stamps[blockIdx.x * 16 + k] = __builtin_readcyclecounter();
+    };
     for (int slot = blockIdx.x; slot < rois; slot += gridDim.x) {
+        STAMP(0);
         int id, jj;
         roi_slot(a, slot, id, jj);
         const uint8_t* lvl = a.level + (size_t)(id / a.per_source) * a.level_stride;
@@ -1065,7 +1143,56 @@ __global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
             }
         }
         __syncthreads();
-        {   // sample the ROI into SB, one 32x32 tile per wave at a time
+        STAMP(1);
+        // the ROI's whole source footprint (corner samples +-1 px, see k_roi_tables) if it fits the U region
+        int gbx0 = INT_MAX, gbx1 = INT_MIN, gby0 = INT_MAX, gby1 = INT_MIN;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int c = (k & 1) ? RW - 1 : 0, r = (k & 2) ? RH - 1 : 0;
+            const int X = (lx0[r] + lad[c]) >> (kAbBits - kInterBits);
+            const int Y = (ly0[r] + lbd[c]) >> (kAbBits - kInterBits);
+            gbx0 = min(gbx0, X >> kInterBits); gbx1 = max(gbx1, X >> kInterBits);
+            gby0 = min(gby0, Y >> kInterBits); gby1 = max(gby1, Y >> kInterBits);
+        }
+        const bool g_interior = gbx0 - 1 >= 0 && gbx1 + 1 <= W - 2 && gby0 - 1 >= 0 && gby1 + 1 <= H - 2;
+        gbx0 = max(gbx0 - 1, 0); gby0 = max(gby0 - 1, 0);
+        gbx1 = min(gbx1 + 2, W - 1); gby1 = min(gby1 + 2, H - 1);
+        const bool g_any = gbx0 <= gbx1 && gby0 <= gby1;
+        const int gbxa = gbx0 & ~3;
+        const int gftw = g_any ? ((gbx1 - gbxa + 4) & ~3) + 4 : 4;   // +4: odd-ish pitch vs banks
+        const int gfth = g_any ? gby1 - gby0 + 1 : 0;
+        if (g_any && gftw * gfth <= LY.tab - LY.u) {   // wave-uniform (same values in every thread)
+            uint8_t* FT = FTall;
+            const int wpr = gftw >> 2;
+            stage_block4(FT, gftw, lvl + (size_t)gby0 * a.P + gbxa, a.P, gfth, wpr, gbxa, a.P, tid, 256);
+            __syncthreads();
+            const int ngrp = (RW + 3) >> 2;
+            for (int i = tid; i < RH * ngrp; i += 256) {   // thread -> (row, 4 columns)
+                const int r = i / ngrp, c0 = 4 * (i - r * ngrp);
+                const int X0 = lx0[r], Y0 = ly0[r];
+                uint32_t pk = 0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int X = (X0 + lad[c0 + u]) >> (kAbBits - kInterBits);
+                    const int Y = (Y0 + lbd[c0 + u]) >> (kAbBits - kInterBits);
+                    int v;
+                    if (g_interior) {
+                        const int fx = X & (kInterTab - 1), fy = Y & (kInterTab - 1);
+                        const uint8_t* p = FT + __mul24((Y >> kInterBits) - gby0, gftw) + ((X >> kInterBits) - gbxa);
+                        const int v0 = p[0], v1 = p[1], v2 = p[gftw], v3 = p[gftw + 1];
+                        const int h0 = 32 * v0 + __mul24(fx, v1 - v0), h1 = 32 * v2 + __mul24(fx, v3 - v2);
+                        v = (32 * h0 + __mul24(fy, h1 - h0) + 512) >> 10;
+                    } else {
+                        v = ft_tap_general(FT, gftw, gbxa, gby0, W, H, X, Y);
+                    }
+                    if (c0 + u >= RW) v = 0;
+                    pk |= (uint32_t)v << (8 * u);
+                }
+                *(uint32_t*)(SB + r * SBp + c0) = pk;
+            }
+        } else if (!g_any) {   // the ROI lies entirely outside the image: all zero (BORDER_CONSTANT 0)
+            for (int i = tid; i < RH * (SBp >> 2); i += 256) ((uint32_t*)SB)[i] = 0u;
+        } else {   // footprint too large: one 32x32 tile per wave at a time
             uint8_t* FT = FTall + wv * ROI_FT;
             for (int task = wv; task < txn * tyn; task += 4) {
                 const int ty = task / txn, tx = task - ty * txn;
@@ -1091,15 +1218,7 @@ __global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
                 const int wpr = ftw >> 2;
                 const bool in_lds = wpr <= 16 && ftw * fth <= ROI_FT;
                 wave_sync();
-                if (any && in_lds) {
-                    const int c = lane & 15;
-                    if (c < wpr) {
-                        const int gx = bxa + 4 * c;
-                        const uint8_t* gsrc = lvl + (size_t)by0 * a.P + gx;
-                        for (int r = lane >> 4; r < fth; r += 4)
-                            *(uint32_t*)(FT + r * ftw + 4 * c) = gx < a.P ? *(const uint32_t*)(gsrc + (size_t)r * a.P) : 0u;
-                    }
-                }
+                if (any && in_lds) stage_footprint<4>(FT, ftw, wpr, fth, lvl + (size_t)by0 * a.P + bxa, a.P, bxa, a.P, lane);
                 wave_sync();
                 const int c0 = cx0 + 4 * lg;
                 if (c0 > cx1) continue;
@@ -1130,32 +1249,43 @@ __global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
             }
         }
         __syncthreads();
-        for (int r = wv; r < RH; r += 4) {   // exact full-row sums, bytes flipped to the signed MFMA operand
+        if (MODE == 1) continue;
+        STAMP(2);
+        for (int r = tid; r < RH; r += 256) {   // exact full-row sums of I and I^2, one thread per row
+            const uint32_t* row = (const uint32_t*)(SB + (size_t)r * SBp);
             uint32_t s1 = 0, s2 = 0;
-            for (int c = lane; c < q4; c += 64) {
-                uint4 v = *(uint4*)(SB + (size_t)r * SBp + 16 * c);
-                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+            int k = 0;
+            for (; k + 8 <= nwr; k += 8) {
+                uint32_t x[8];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t x = 4 * c + k < nwr ? w4[k] : 0u;
-                    s1 = __builtin_amdgcn_udot4(x, 0x01010101u, s1, false);
-                    s2 = __builtin_amdgcn_udot4(x, x, s2, false);
+                for (int u = 0; u < 8; ++u) x[u] = row[k + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    s1 = __builtin_amdgcn_udot4(x[u], 0x01010101u, s1, false);
+                    s2 = __builtin_amdgcn_udot4(x[u], x[u], s2, false);
                 }
-                v.x ^= 0x80808080u; v.y ^= 0x80808080u; v.z ^= 0x80808080u; v.w ^= 0x80808080u;
-                *(uint4*)(SB + (size_t)r * SBp + 16 * c) = v;
             }
-            s1 = wave_sum_u32(s1);
-            s2 = wave_sum_u32(s2);
-            if (lane == 0) { rall[r] = s1; rallq[r] = s2; }
-        }
-        {   // all template rows (padded to 16) of the i8 slab
-            const int trows = (th + kMmaRows - 1) / kMmaRows * kMmaRows, tq = a.tp8 >> 4;
-            for (int i = tid; i < trows * tq; i += 256) {
-                const int r = i / tq, c = i - r * tq;
-                *(uint4*)(TB + (size_t)r * TBp + 16 * c) = *(const uint4*)((const uint8_t*)a.tmpl8 + (size_t)r * a.tp8 + 16 * c);
+            for (; k < nwr; ++k) {
+                const uint32_t x = row[k];
+                s1 = __builtin_amdgcn_udot4(x, 0x01010101u, s1, false);
+                s2 = __builtin_amdgcn_udot4(x, x, s2, false);
             }
+            rall[r] = s1;
+            rallq[r] = s2;
         }
         __syncthreads();
+        for (int i = tid; i < RH * q4; i += 256) {   // bytes flipped to the signed MFMA operand
+            uint4* v = (uint4*)SB + i;   // rows are contiguous (pitch SBp = 16 * q4)
+            uint4 x = *v;
+            x.x ^= 0x80808080u; x.y ^= 0x80808080u; x.z ^= 0x80808080u; x.w ^= 0x80808080u;
+            *v = x;
+        }
+        {   // all template rows (padded to 16) of the i8 slab
+            const int trows = (th + kMmaRows - 1) / kMmaRows * kMmaRows;
+            stage_block16(TB, TBp, (const uint8_t*)a.tmpl8, a.tp8, trows, a.tp8 >> 4, tid, 256);
+        }
+        __syncthreads();
+        STAMP(3);
         for (int i = tid; i < RH * 7; i += 256) {   // window [dx, dx + tw) of every row
             const int r = i / 7, dx = i - r * 7;
             const uint8_t* sbr = SB + (size_t)r * SBp;
@@ -1166,13 +1296,24 @@ __global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
             wq[i] = q2;
         }
         __syncthreads();
+        STAMP(4);
         if (tid < 49) {   // window totals of the 49 positions (exact)
             const int pdy = tid / 7, ddx = tid - pdy * 7;
             uint64_t s1 = 0, s2 = 0;
-            for (int t = 0; t < th; ++t) { s1 += wi[(t + pdy) * 7 + ddx]; s2 += wq[(t + pdy) * 7 + ddx]; }
+            int t = 0;
+            for (; t + 8 <= th; t += 8) {   // 8 LDS reads of each in flight
+                uint32_t x[8], y[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) { x[u] = wi[(t + u + pdy) * 7 + ddx]; y[u] = wq[(t + u + pdy) * 7 + ddx]; }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) { s1 += x[u]; s2 += y[u]; }
+            }
+            for (; t < th; ++t) { s1 += wi[(t + pdy) * 7 + ddx]; s2 += wq[(t + pdy) * 7 + ddx]; }
             tot[tid] = s1;
             tot[49 + tid] = s2;
         }
+        if (MODE == 2) continue;
+        STAMP(5);
         float accF = 0.f;
         uint64_t accI = 0;
         const uint32_t kFix = 16384u * (uint32_t)tw;
@@ -1196,9 +1337,17 @@ __global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
                 }
             }
             __syncthreads();
-            if (tid < 49) {
+            if (MODE != 3 && tid < 49) {
                 if (a.fold) {
-                    for (int t = 0; t < rb; ++t) accF = accF + (float)(int)rs[t * 49 + tid];   // :507, row order
+                    int t = 0;
+                    for (; t + 8 <= rb; t += 8) {   // 8 LDS reads in flight, adds in row order (:507)
+                        uint32_t x[8];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) x[u] = rs[(t + u) * 49 + tid];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) accF = accF + (float)(int)x[u];
+                    }
+                    for (; t < rb; ++t) accF = accF + (float)(int)rs[t * 49 + tid];
                 } else {
                     for (int t = 0; t < rb; ++t) accI += rs[t * 49 + tid];
                 }
@@ -1210,6 +1359,7 @@ __global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
             sc[tid] = ccoeff(num, (double)tot[tid], (double)tot[49 + tid], a.mean, a.norm, a.inv_area);
         }
         __syncthreads();
+        STAMP(6);
         if (tid == 0) {   // cv::minMaxLoc: first maximum in row-major order
             float best = sc[0];
             int bi = 0;
@@ -1226,6 +1376,7 @@ __global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
                 for (int y = -1; y <= 1; ++y) r.vec[(x + 1) * 3 + (y + 1)] = border ? 0.f : sc[(my + y) * 7 + (mx + x)];
             a.rec[(size_t)id * a.n3 + jj] = r;
         }
+        STAMP(7);
     }
 }
 
@@ -1412,13 +1563,14 @@ void launch_roi_tables(const RoiArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_roi_tables, dim3(grid), dim3(256), lds, st, a);
 }
 
+constexpr int kWarpFootBatch = 2;   // footprint rows in flight per lane (measured: see DESIGN.md)
 void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0 || a.equal1) return;
     const long tiles = (long)a.slot_cap * ((a.th + 6 + ROI_T - 1) / ROI_T) * ((a.tw + 6 + ROI_T - 1) / ROI_T);
     if (tiles > INT_MAX) return;   // the engine bounds slot_cap far below this
     const long want = (tiles + 3) / 4;
     const int grid = (int)(want < 16384 ? want : 16384);
-    hipLaunchKernelGGL(k_roi_warp, dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_roi_warp<kWarpFootBatch>, dim3(grid), dim3(256), 0, st, a);
 }
 
 void launch_roi_corr(const RoiArgs& a, hipStream_t st) {
@@ -1452,11 +1604,11 @@ void launch_roi_small(const RoiArgs& a, hipStream_t st) {
     const size_t lds = (size_t)small_layout(a.tw, a.th).total;
     static size_t lds_attr = 0;
     if (lds > 65536 && lds > lds_attr) {
-        (void)hipFuncSetAttribute((const void*)k_roi_small, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)k_roi_small<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         lds_attr = lds;
     }
     const int grid = a.slot_cap < 8192 ? a.slot_cap : 8192;
-    hipLaunchKernelGGL(k_roi_small, dim3(grid), dim3(256), lds, st, a);
+    hipLaunchKernelGGL(k_roi_small<0>, dim3(grid), dim3(256), lds, st, a);
 }
 
 void launch_cand_step(const RoiArgs& a, int max_items, hipStream_t st) {

@@ -101,6 +101,14 @@ int main(int argc, char** argv) {
     };
     timeit([&] { launch_roi_tables(a, 0); }, "prod tables");
     timeit([&] { launch_roi_warp(a, 0); }, "prod warp");
+    {
+        const long tiles = (long)a.slot_cap * ((TH + 6 + 31) / 32) * ((TW + 6 + 31) / 32);
+        const int grid = (int)std::min<long>((tiles + 3) / 4, 16384);
+        timeit([&] { hipLaunchKernelGGL(k_roi_warp<1>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 1");
+        timeit([&] { hipLaunchKernelGGL(k_roi_warp<2>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 2");
+        timeit([&] { hipLaunchKernelGGL(k_roi_warp<4>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 4");
+        timeit([&] { hipLaunchKernelGGL(k_roi_warp<8>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 8");
+    }
     timeit([&] { launch_roi_corr(a, 0); }, "prod corr");
     timeit([&] { launch_roi_eval(a, 0); }, "prod eval");
     {
@@ -139,6 +147,62 @@ int main(int argc, char** argv) {
             (void)RW;
         }
         printf("corr host check: %s (%d mismatches)\n", bad ? "FAIL" : "OK", bad);
+    }
+    {   // small-template single-kernel refinement at Src7 layer-3 geometry: 96x66 template, 503x380 level,
+        // 224 candidates x 3 angles (8 sources x 28), grid sized like the product (slot_cap WGs, most idle)
+        const int TW3 = 96, TH3 = 66, W3 = 503, H3 = 380, nc3 = 28, C3 = nsrc * nc3;
+        RoiArgs b = a;
+        b.W = W3; b.H = H3; b.tw = TW3; b.th = TH3;
+        const int p8 = 128, rows8 = 80;
+        std::vector<int8_t> t8((size_t)p8 * rows8 + 64, 0);
+        std::vector<int32_t> ts(rows8, 0);
+        for (int y = 0; y < TH3; ++y)
+            for (int x = 0; x < TW3; ++x) { t8[(size_t)y * p8 + x] = (int8_t)(tm[(size_t)y * TP + x] ^ 0x80); ts[y] += tm[(size_t)y * TP + x]; }
+        int8_t* d8; int32_t* dts;
+        CK(hipMalloc(&d8, t8.size())); CK(hipMalloc(&dts, ts.size() * 4));
+        CK(hipMemcpy(d8, t8.data(), t8.size(), hipMemcpyHostToDevice));
+        CK(hipMemcpy(dts, ts.data(), ts.size() * 4, hipMemcpyHostToDevice));
+        b.tmpl8 = d8; b.tp8 = p8; b.nk = 2; b.tsum = dts;
+        b.nchunk = (TH3 + 15) / 16; b.rc = 16; b.per_source = nc3;
+        std::vector<CandState> st3(C3);
+        std::vector<int> live3(C3);
+        for (int i = 0; i < C3; ++i) {
+            st3[i].lt = f2(40.f + 11.f * (i % 23), 30.f + 9.f * (i % 19));
+            st3[i].node = i % C; st3[i].alive = 1; st3[i].reached0 = 0;
+            live3[i] = i;
+        }
+        CandState* d_st3; int *d_live3, *d_cnt3;
+        CK(hipMalloc(&d_st3, sizeof(CandState) * C3)); CK(hipMalloc(&d_live3, 4 * C3)); CK(hipMalloc(&d_cnt3, 4));
+        CK(hipMemcpy(d_st3, st3.data(), sizeof(CandState) * C3, hipMemcpyHostToDevice));
+        CK(hipMemcpy(d_live3, live3.data(), 4 * C3, hipMemcpyHostToDevice));
+        CK(hipMemcpy(d_cnt3, &C3, 4, hipMemcpyHostToDevice));
+        b.state = d_st3; b.live = d_live3; b.live_count = d_cnt3;
+        b.slot_cap = 7872;   // the product's plan capacity for this batch (most WGs find no ROI)
+        const size_t lds = roi_small_lds(TW3, TH3);
+        printf("small L3: rois %d lds %zu\n", C3 * n3, lds);
+        timeit([&] { launch_roi_small(b, 0); }, "small prod");
+        timeit([&] { hipLaunchKernelGGL(k_roi_small<1>, dim3(7872), dim3(256), lds, 0, b); }, "small sample only");
+        timeit([&] { hipLaunchKernelGGL(k_roi_small<2>, dim3(7872), dim3(256), lds, 0, b); }, "small +sums");
+        timeit([&] { hipLaunchKernelGGL(k_roi_small<3>, dim3(7872), dim3(256), lds, 0, b); }, "small +bands nofold");
+        timeit([&] { hipLaunchKernelGGL(k_roi_small<0>, dim3(C3 * n3), dim3(256), lds, 0, b); }, "small exact grid");
+        {   // per-phase s_memtime stamps of the first 64 workgroups
+            uint64_t* d_stamps;
+            CK(hipMalloc(&d_stamps, 64 * 16 * 8));
+            CK(hipMemset(d_stamps, 0, 64 * 16 * 8));
+            b.stamps = d_stamps;
+            hipLaunchKernelGGL(k_roi_small<9>, dim3(C3 * n3), dim3(256), lds, 0, b);
+            CK(hipDeviceSynchronize());
+            std::vector<uint64_t> hs(64 * 16);
+            CK(hipMemcpy(hs.data(), d_stamps, hs.size() * 8, hipMemcpyDeviceToHost));
+            const char* names[7] = {"ids+tables", "sampling", "sums+tmpl", "edges", "totals", "bands+fold", "argmax+rec"};
+            double acc[7] = {0};
+            for (int w = 0; w < 64; ++w)
+                for (int k = 0; k < 7; ++k) acc[k] += (double)(hs[w * 16 + k + 1] - hs[w * 16 + k]);
+            printf("small L3 phases (cycles, mean of 64 WGs):");
+            for (int k = 0; k < 7; ++k) printf(" %s %.0f", names[k], acc[k] / 64);
+            printf("\n");
+            b.stamps = nullptr;
+        }
     }
     {
         const size_t bytes = img.size(), n16 = bytes / 16;
