@@ -32,33 +32,31 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-# kernels of each profiled family (fpm_profile_* families, include/fpm.h FPM_K_*)
-FAMILY_KERNELS = {"pyr_down": ["k_pyr_down"], "top_warp": ["k_warp"], "top_ncc": ["k_ncc_map"], "top_nms": ["k_nms"],
-                  "roi_warp": ["k_roi_tables", "k_roi_warp"], "roi_corr": ["k_roi_corr"], "roi_eval": ["k_roi_eval"],
-                  "cand": ["k_cand_init"]}
 TRAFFIC_CSV = os.path.join(REPO, "profiles", "latest", "pmc_traffic.csv")
 
 
-def pmc_traffic(family):
-    """HBM bytes per launch of `family` from the committed PMC summary (scripts/pmc_bench.sh: separate FETCH_SIZE /
-    WRITE_SIZE passes over this same bench command, FETCH_SIZE doubled for gfx950); None if not collected."""
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` (a profiling index name, _lib.KERNEL_NAMES) from the committed PMC summary
+    (scripts/pmc_bench.sh: separate FETCH_SIZE / WRITE_SIZE passes over `bench.py --skip-latency`, FETCH_SIZE
+    doubled for gfx950, per-dispatch means); None if not collected for this kernel."""
     import csv
+
+    from fastest_image_pattern_matching_amd import _lib as L
 
     if not os.path.exists(TRAFFIC_CSV):
         return None
-    per = {}
+    fetch, write = {}, {}
     with open(TRAFFIC_CSV) as fh:
         for row in csv.DictReader(fh):
-            if row["counter"].startswith(("FETCH_BYTES", "WRITE_BYTES")):
-                per.setdefault(row["kernel"], 0.0)
-                per[row["kernel"]] += float(row["mean_per_dispatch"])
-    tot, found = 0.0, False
-    for k in FAMILY_KERNELS.get(family, []):
-        for name, v in per.items():
-            if name.startswith(f"fpm::{k}(") or name.startswith(f"void fpm::{k}<"):
-                tot += v
-                found = True
-    return int(tot) if found else None
+            if row["counter"].startswith("FETCH_BYTES"):
+                fetch[row["kernel"]] = float(row["mean_per_dispatch"])
+            elif row["counter"].startswith("WRITE_BYTES"):
+                write[row["kernel"]] = float(row["mean_per_dispatch"])
+    for sym in L.KERNEL_SYMBOLS.get(kernel, []):
+        for name in fetch:
+            if (name.startswith(f"fpm::{sym}(") or name.startswith(f"void fpm::{sym}<")) and name in write:
+                return int(fetch[name] + write[name])
+    return None
 
 
 def make_sources(templ, n, seed0):
@@ -93,6 +91,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=8, help="Src7 sources searched per GPU per step")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (0 = skip)")
+    ap.add_argument("--skip-latency", action="store_true",
+                    help="skip the single-search latency probe (PMC runs: only batch dispatches)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -124,13 +124,15 @@ def main():
         setattr(m._params, k, v)
     assert m.learnPattern(templ)
     # single-search latency (host upload included) for the record, after one warm call builds the plan
-    single = m.match(sources[0])
-    lat = []
-    for _ in range(5):
-        t0 = time.perf_counter()
-        single = m.match(sources[0])
-        lat.append(time.perf_counter() - t0)
-    lat_e2e = float(np.median(lat))
+    lat_e2e = None
+    if not args.skip_latency:
+        m.match(sources[0])
+        lat = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            m.match(sources[0])
+            lat.append(time.perf_counter() - t0)
+        lat_e2e = float(np.median(lat))
     m.stage(sources)
     for _ in range(args.warmup):
         m.match_staged()
@@ -201,7 +203,7 @@ def main():
             "parallelism": f"sources sharded over {world} GPU(s), one process per GPU",
         },
         "ms_per_search": round(elapsed * 1e3 / (args.batch * args.steps), 4),
-        "single_search_ms_end_to_end": round(lat_e2e * 1e3, 3),
+        "single_search_ms_end_to_end": round(lat_e2e * 1e3, 3) if lat_e2e is not None else None,
         "matches_per_search": n_matches,
         "kernels": kern,
         "roofline": roofline,
@@ -216,7 +218,6 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
-    del single
 
 
 if __name__ == "__main__":

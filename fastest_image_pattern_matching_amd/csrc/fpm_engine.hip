@@ -571,6 +571,7 @@ int enqueue_search(fpm_ctx* ctx) {
         ca.nang = P.nang; ca.cap = P.cap; ca.total = P.C;
         ca.center = P.center;
         ca.refine = L > 0 ? (L == 1 ? 2 : 1) : 0;
+        ProfScope ps(ctx, FPM_K_CAND_INIT, 0);
         launch_cand_init(ca, st);
     }
     for (int l = L - 1; l >= 0; --l) {
@@ -613,13 +614,16 @@ int enqueue_search(fpm_ctx* ctx) {
             ra.slot_base = base;
             ra.slot_cap = std::min(P.slot_cap, total_rois - base);
             if (small) {
-                ProfScope ps(ctx, FPM_K_ROI_CORR, 0);
+                ProfScope ps(ctx, FPM_K_ROI_SMALL, 0);
                 launch_roi_small(ra, st);
                 continue;
             }
             {
-                ProfScope ps(ctx, FPM_K_ROI_WARP, 0);
+                ProfScope ps(ctx, FPM_K_ROI_TABLES, 0);
                 launch_roi_tables(ra, st);
+            }
+            {
+                ProfScope ps(ctx, FPM_K_ROI_WARP, 0);
                 launch_roi_warp(ra, st);
             }
             {
@@ -632,7 +636,7 @@ int enqueue_search(fpm_ctx* ctx) {
             }
         }
         if (small && ra.step) {
-            ProfScope ps(ctx, FPM_K_CAND, 0);
+            ProfScope ps(ctx, FPM_K_CAND_STEP, 0);
             launch_cand_step(ra, P.C, st);
         }
     }
@@ -808,13 +812,15 @@ int run_staged(fpm_ctx* ctx, std::vector<std::vector<fpm_result>>& results) {
             const int rc = roi_pick_rc(t.w, t.h);
             const int64_t nch = (t.h + rc - 1) / rc;
             if (roi_small_fits(t.w, t.h)) {   // one kernel: source samples + template in, one record out
-                ctx->kp[FPM_K_ROI_CORR].bytes +=
+                ctx->kp[FPM_K_ROI_SMALL].bytes +=
                     rois * ((int64_t)(t.w + 6) * (t.h + 6) + (int64_t)t.w * t.h + (int64_t)sizeof(RoiRecord));
                 continue;
             }
-            // warp: ROI bytes written (its source taps are a gather, not counted); corr: ROI + template read,
-            // row sums + window partials written; eval: row sums + partials read, one record written
-            ctx->kp[FPM_K_ROI_WARP].bytes += rois * (int64_t)(t.w + 6) * (t.h + 6);
+            // tables: written tables + descriptors; warp: one source sample per ROI pixel read + the ROI written;
+            // corr: ROI + template read, row sums + window partials written; eval: those read, one record written
+            ctx->kp[FPM_K_ROI_TABLES].bytes +=
+                rois * (int64_t)(8 * (t.w + 6) + 8 * (t.h + 6) + 16 * (((t.w + 37) / 32) * ((t.h + 37) / 32)));
+            ctx->kp[FPM_K_ROI_WARP].bytes += rois * 2 * (int64_t)(t.w + 6) * (t.h + 6);
             ctx->kp[FPM_K_ROI_CORR].bytes +=
                 rois * ((int64_t)(t.w + 6) * (t.h + 6) + (int64_t)t.w * t.h + (int64_t)t.h * 49 * 4 + nch * 49 * 12);
             ctx->kp[FPM_K_ROI_EVAL].bytes += rois * ((int64_t)t.h * 49 * 4 + nch * 49 * 12 + (int64_t)sizeof(RoiRecord));

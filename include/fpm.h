@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define FPM_ABI_VERSION 2
+#define FPM_ABI_VERSION 3
 
 /* status codes */
 #define FPM_OK 0
@@ -128,18 +128,22 @@ int fpm_template_level(const fpm_ctx* ctx, int32_t level, int32_t* w, int32_t* h
  * Returns the number of entries written. */
 int fpm_search_stats(const fpm_ctx* ctx, int64_t* stats, int32_t cap);
 
-/* Kernel timing: when enabled, HIP events bracket every launch of each kernel family on the context's
- * stream; fpm_profile_get returns total milliseconds, launch count and algorithmic bytes moved (inputs +
- * outputs, u8 = 1 B, f32 = 4 B) accumulated since the last reset. */
-#define FPM_K_PYR 0        /* K1 pyrDown                                                   */
-#define FPM_K_TOP_WARP 1   /* K2 top-layer rotation                                        */
-#define FPM_K_TOP_NCC 2    /* K3+K4 top-layer CCORR + normalisation                        */
-#define FPM_K_TOP_NMS 3    /* K5 peak extraction                                           */
-#define FPM_K_ROI_WARP 4   /* K6 refinement ROI tables + LDS-staged bilinear sampling      */
-#define FPM_K_ROI_CORR 5   /* K7 refinement row correlation (i8 MFMA) + window sums        */
-#define FPM_K_ROI_EVAL 6   /* K8 row fold + normalisation + argmax + 3x3 + candidate step  */
-#define FPM_K_CAND 7       /* candidate init from the top-layer peaks                      */
-#define FPM_K_COUNT 8
+/* Kernel timing: when enabled, HIP events bracket every launch of each kernel on the context's stream (the
+ * search then runs eagerly instead of as a replayed graph); fpm_profile_get returns total milliseconds, launch
+ * count and algorithmic bytes (compulsory inputs + outputs, u8 = 1 B, f32 = 4 B) accumulated since the last
+ * reset.  One index per kernel. */
+#define FPM_K_PYR 0         /* k_pyr_down     K1 pyrDown                                          */
+#define FPM_K_TOP_WARP 1    /* k_warp         K2 top-layer rotation                               */
+#define FPM_K_TOP_NCC 2     /* k_ncc_tile / k_ncc_map  K3+K4 top-layer CCORR + normalisation      */
+#define FPM_K_TOP_NMS 3     /* k_nms          K5 peak extraction                                  */
+#define FPM_K_CAND_INIT 4   /* k_cand_init    candidates from the top-layer peaks                 */
+#define FPM_K_ROI_TABLES 5  /* k_roi_tables   K6a refinement warp tables + tile descriptors       */
+#define FPM_K_ROI_WARP 6    /* k_roi_warp     K6b refinement ROI sampling                         */
+#define FPM_K_ROI_CORR 7    /* k_roi_corr     K7 refinement row correlation (i8 MFMA) + windows   */
+#define FPM_K_ROI_EVAL 8    /* k_roi_eval     K8 row fold, CCOEFF, argmax, 3x3, candidate step    */
+#define FPM_K_ROI_SMALL 9   /* k_roi_small    K6-K8 in one kernel for small templates             */
+#define FPM_K_CAND_STEP 10  /* k_cand_step    candidate step after k_roi_small                    */
+#define FPM_K_COUNT 11
 int fpm_profile_enable(fpm_ctx* ctx, int32_t enable);
 int fpm_profile_reset(fpm_ctx* ctx);
 int fpm_profile_get(const fpm_ctx* ctx, int32_t kernel, double* total_ms, int64_t* launches,
