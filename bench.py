@@ -91,6 +91,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=8, help="Src7 sources searched per GPU per step")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (0 = skip)")
+    ap.add_argument("--contexts", type=int, default=2, help="concurrent contexts (HIP streams) per GPU")
     ap.add_argument("--skip-latency", action="store_true",
                     help="skip the single-search latency probe (PMC runs: only batch dispatches)")
     args = ap.parse_args()
@@ -133,17 +134,39 @@ def main():
             m.match(sources[0])
             lat.append(time.perf_counter() - t0)
         lat_e2e = float(np.median(lat))
-    m.stage(sources)
+    # G contexts (one HIP stream each) on this GPU, each holding batch / G of the sources: a step launches every
+    # context's device pass, then finishes them in order, so host post-processing and the upper pyramid layers'
+    # latency-bound kernels of one context overlap device work of the others
+    G = max(1, min(args.contexts, args.batch))
+    chunks = [sources[i * args.batch // G:(i + 1) * args.batch // G] for i in range(G)]
+    ctxs = [m] + [TemplateMatcher(local) for _ in range(G - 1)]
+    for c, ch in zip(ctxs, chunks):
+        for k, v in PARAMS.items():
+            setattr(c._params, k, v)
+        if c is not m:
+            assert c.learnPattern(templ)
+        c.stage(ch)
+    ref = [r for c in ctxs for r in c.match_staged()]   # object results once, for the report and checks
+    views = [c.match_staged_array() for c in ctxs]
+    assert [len(r) for r in ref] == [int(x) for cnt, _ in views for x in cnt]
+
+    def step():
+        for c in ctxs:
+            c.match_staged_launch()
+        return [c.match_staged_finish_array() for c in ctxs]
+
     for _ in range(args.warmup):
-        m.match_staged()
-    log(f"[rank {rank}] warm; timing {args.steps} steps x {args.batch} sources")
+        step()
+    log(f"[rank {rank}] warm; timing {args.steps} steps x {args.batch} sources over {G} context(s)")
 
     barrier_sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        res = m.match_staged()
+        step()   # device passes + host finish (C++); results as array views
     barrier_sync()
     elapsed = time.perf_counter() - t0
+    res = ref
+    dev_ms, host_ms, call_ms = m.profile_last()
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -158,11 +181,14 @@ def main():
     else:
         n_matches = [len(r) for r in res]
 
-    # kernel-level pass with HIP events around every launch
+    # kernel-level pass: one context over the whole batch, eager launches with HIP events around each kernel (the
+    # kernels' own durations, not time shared with another context's stream)
+    m.stage(sources)
+    m.match_staged_array()
     m.profile(True)
     m.profile_reset()
     for _ in range(args.steps):
-        m.match_staged()
+        m.match_staged_array()
     m.profile(False)
     kern = {}
     for k, name in enumerate(L.KERNEL_NAMES):
@@ -200,9 +226,13 @@ def main():
                         "SIMD fold on",
             "sources_per_gpu_per_step": args.batch,
             "global_batch": args.batch * world,
-            "parallelism": f"sources sharded over {world} GPU(s), one process per GPU",
+            "parallelism": f"sources sharded over {world} GPU(s), one process per GPU; {G} concurrent contexts "
+                           f"(HIP streams) per GPU",
+            "contexts_per_gpu": G,
         },
         "ms_per_search": round(elapsed * 1e3 / (args.batch * args.steps), 4),
+        "last_step_split_ms_ctx0": {"device": round(dev_ms, 4), "host_finish": round(host_ms, 4),
+                                    "launch_to_finish": round(call_ms, 4)},
         "single_search_ms_end_to_end": round(lat_e2e * 1e3, 3) if lat_e2e is not None else None,
         "matches_per_search": n_matches,
         "kernels": kern,

@@ -75,6 +75,8 @@ SIGNATURES = {
                             C.POINTER(C.c_int32), C.POINTER(C.c_double)]),
     "fpm_stage_sources": (C.c_int, [_P, C.POINTER(_U8P), C.c_int32, C.c_int32, C.c_int32, C.c_size_t]),
     "fpm_match_staged": (C.c_int, [_P, C.POINTER(Result), C.c_int32, C.POINTER(C.c_int32)]),
+    "fpm_match_staged_launch": (C.c_int, [_P]),
+    "fpm_match_staged_finish": (C.c_int, [_P, C.POINTER(Result), C.c_int32, C.POINTER(C.c_int32)]),
     "fpm_op_pyr_down": (C.c_int, [_P, _U8P, C.c_int32, C.c_int32, C.c_size_t, _U8P, C.c_size_t]),
     "fpm_op_warp_affine": (C.c_int, [_P, _U8P, C.c_int32, C.c_int32, C.c_size_t, C.POINTER(C.c_double), _U8P,
                                      C.c_int32, C.c_int32, C.c_size_t, C.c_int32]),
@@ -89,6 +91,7 @@ SIGNATURES = {
     "fpm_profile_reset": (C.c_int, [_P]),
     "fpm_profile_get": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                   C.POINTER(C.c_int64)]),
+    "fpm_profile_last": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
 }
 
 _lib = None

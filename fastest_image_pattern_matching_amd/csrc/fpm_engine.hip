@@ -54,7 +54,7 @@ struct PinBuf {
         if (bytes <= n && p) return hipSuccess;
         if (p) { (void)hipHostFree(p); p = nullptr; n = 0; }
         if (bytes == 0) bytes = 256;
-        hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+        hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocMapped);   // device-visible (k_pack writes it)
         if (e == hipSuccess) n = bytes;
         return e;
     }
@@ -105,7 +105,8 @@ struct Plan {
     int slot_cap = 0;                          // ROIs per refinement round (bounded scratch)
     size_t off_warp = 0, off_ncc = 0, off_nms = 0;
     PinBuf h_out;
-    size_t h_counts = 0, h_peaks = 0, h_state = 0, h_rec = 0, h_live = 0, h_total = 0;
+    size_t h_counts = 0, h_peaks = 0, h_live = 0, h_live0 = 0, h_state = 0, h_rec = 0, h_total = 0;
+    char* h_dev = nullptr;   // device-side address of h_out (k_pack writes it over PCIe)
     void release() {
         for (DevBuf* b : {&d_canvas, &d_map, &d_bmax, &d_bloc, &d_jobs, &d_nodes, &d_top, &d_topn, &d_peaks,
                           &d_counts, &d_state, &d_live, &d_livecnt, &d_rec, &d_rowsum, &d_wsum, &d_wsq, &d_tab, &d_roi, &d_tdesc})
@@ -154,6 +155,11 @@ struct fpm_ctx {
     uint64_t graph_plan = ~0ull;
     const void* graph_src = nullptr;
     uint64_t plan_builds = 0;
+    // timing of the last search (fpm_profile_last)
+    hipEvent_t t_ev[2] = {nullptr, nullptr};
+    double last_device_ms = 0, last_host_ms = 0, last_call_ms = 0;
+    std::chrono::steady_clock::time_point t_call0;
+    bool pending = false;    // a staged search is in flight (fpm_match_staged_launch)
 };
 
 #define HIP_TRY(expr)                                                                   \
@@ -458,14 +464,20 @@ int build_plan(fpm_ctx* ctx) {
                                sizeof(AngleNode) * P.nodes[d].size(), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(P.d_top.p, P.top.data(), sizeof(TopAngle) * P.nang, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(P.d_topn.p, P.top_nodes.data(), sizeof(AngleNode) * P.nang, hipMemcpyHostToDevice, ctx->stream));
-    // pinned host staging for the single device->host copy
+    // pinned host buffer written by k_pack: counts | peaks | live counts | layer-0 ids | states | records
     P.h_counts = 0;
     P.h_peaks = round_up(sizeof(int32_t) * J, (size_t)256);
-    P.h_state = P.h_peaks + round_up(sizeof(Peak) * (size_t)P.C, (size_t)256);
+    P.h_live = P.h_peaks + round_up(sizeof(Peak) * (size_t)P.C, (size_t)256);
+    P.h_live0 = P.h_live + round_up(sizeof(int32_t) * (L + 2), (size_t)256);
+    P.h_state = P.h_live0 + round_up(sizeof(int32_t) * (size_t)P.C, (size_t)256);
     P.h_rec = P.h_state + round_up(sizeof(CandState) * (size_t)P.C, (size_t)256);
-    P.h_live = P.h_rec + round_up(sizeof(RoiRecord) * (size_t)P.C * P.n3, (size_t)256);
-    P.h_total = P.h_live + sizeof(int32_t) * (L + 2);
+    P.h_total = P.h_rec + sizeof(RoiRecord) * (size_t)P.C * P.n3;
     HIP_TRY(P.h_out.ensure(P.h_total));
+    {
+        void* dp = nullptr;
+        HIP_TRY(hipHostGetDevicePointer(&dp, P.h_out.p, 0));
+        P.h_dev = (char*)dp;
+    }
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     P.valid = true;
     ctx->plan_gen = ctx->tmpl_gen;
@@ -641,20 +653,29 @@ int enqueue_search(fpm_ctx* ctx) {
         }
     }
     HIP_TRY(hipGetLastError());
-    // the single device -> host copy
-    char* h = P.h_out.as<char>();
-    HIP_TRY(hipMemcpyAsync(h + P.h_counts, P.d_counts.p, sizeof(int32_t) * J, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(h + P.h_peaks, P.d_peaks.p, sizeof(Peak) * (size_t)P.C, hipMemcpyDeviceToHost, st));
-    if (L > 0) {
-        HIP_TRY(hipMemcpyAsync(h + P.h_state, P.d_state.p, sizeof(CandState) * (size_t)P.C, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(h + P.h_rec, P.d_rec.p, sizeof(RoiRecord) * (size_t)P.C * P.n3, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(h + P.h_live, P.d_livecnt.p, sizeof(int32_t) * (L + 2), hipMemcpyDeviceToHost, st));
+    // results into pinned host memory (one kernel; only the layer-0 candidates' states and records)
+    {
+        PackArgs pa;
+        pa.counts = P.d_counts.as<int32_t>(); pa.J = J;
+        pa.peaks = P.d_peaks.as<Peak>(); pa.C = P.C;
+        pa.livecnt = livecnt; pa.nlive = L + 2;
+        pa.live0 = L > 0 ? live[(L - 1) & 1] : nullptr;
+        pa.live0_count = livecnt + (L > 0 ? L - 1 : 0);
+        pa.state = P.d_state.as<CandState>();
+        pa.rec = P.d_rec.as<RoiRecord>();
+        pa.n3 = P.n3;
+        pa.host = P.h_dev;
+        pa.o_counts = P.h_counts; pa.o_peaks = P.h_peaks; pa.o_live = P.h_live;
+        pa.o_live0 = P.h_live0; pa.o_state0 = P.h_state; pa.o_rec0 = P.h_rec;
+        launch_pack(pa, st);
+        HIP_TRY(hipGetLastError());
     }
     return FPM_OK;
 }
 
 // host finish for source s (TemplateMatcher.cpp:214-432)
-void finish_source(fpm_ctx* ctx, int s, std::vector<fpm_result>& out) {
+// pos[id] = index of candidate id in the layer-0 live list (k_pack's compact states / records), -1 if absent
+void finish_source(fpm_ctx* ctx, int s, std::vector<fpm_result>& out, const std::vector<int>& pos) {
     Plan& P = ctx->plan;
     const int L = P.L;
     const char* h = P.h_out.as<char>();
@@ -662,43 +683,37 @@ void finish_source(fpm_ctx* ctx, int s, std::vector<fpm_result>& out) {
     const Peak* peaks = (const Peak*)(h + P.h_peaks);
     const CandState* state = (const CandState*)(h + P.h_state);
     const RoiRecord* rec = (const RoiRecord*)(h + P.h_rec);
-    struct TopCand { double score; int id; };
-    std::vector<HostMatch> cand;
-    std::vector<int> ids;
+    // std::sort(vecMatchParameter, compareScoreBig2Small) (:214) over the top candidates in the reference's
+    // insertion order (angle-major, then peak order).  The permutation std::sort produces depends only on the
+    // sequence of comparison results, so sorting light (score, id) keys with the same comparator reproduces the
+    // reference's order of equal scores exactly.
+    struct Key { double score; int id; int a; };
+    std::vector<Key> order;
+    order.reserve(64);
     for (int a = 0; a < P.nang; ++a) {
         const int job = s * P.nang + a;
-        for (int r = 0; r < counts[job]; ++r) {
-            const int id = job * P.cap + r;
-            const Peak& pk = peaks[id];
-            HostMatch m{};
-            const F2 pt = f2((float)pk.x - P.top[a].tx, (float)pk.y - P.top[a].ty);
-            m.ptx = pt.x; m.pty = pt.y;
-            m.score = pk.score;
-            m.angle = P.angles[a];
-            cand.push_back(m);
-            ids.push_back(id);
-        }
+        for (int r = 0; r < counts[job]; ++r) order.push_back({(double)peaks[job * P.cap + r].score, job * P.cap + r, a});
     }
-    // std::sort(vecMatchParameter, compareScoreBig2Small) (:214): sort an index permutation with the same
-    // comparator and sequence so ties resolve exactly as the reference's introsort does.
-    std::vector<std::pair<HostMatch, int>> order(cand.size());
-    for (size_t i = 0; i < cand.size(); ++i) order[i] = {cand[i], ids[i]};
-    std::sort(order.begin(), order.end(),
-              [](const std::pair<HostMatch, int>& l, const std::pair<HostMatch, int>& r) { return l.first.score > r.first.score; });
+    std::sort(order.begin(), order.end(), [](const Key& l, const Key& r) { return l.score > r.score; });
     std::vector<HostMatch> all;
     const TmplLevel& t0 = ctx->tmpl[0];
-    for (auto& oc : order) {
-        HostMatch& c = oc.first;
-        const int id = oc.second;
+    for (const Key& k : order) {
+        const int id = k.id;
         if (L == 0) {   // iTopLayer <= iStopLayer (:272-276)
+            const Peak& pk = peaks[id];
+            HostMatch c{};
+            const F2 pt = f2((float)pk.x - P.top[k.a].tx, (float)pk.y - P.top[k.a].ty);
+            c.score = pk.score;
+            c.angle = P.angles[k.a];
             const double rad = -c.angle * kD2R;
-            const F2 lt = rotate_pt(f2((float)c.ptx, (float)c.pty), P.center, std::cos(rad), std::sin(rad));
+            const F2 lt = rotate_pt(f2(pt.x, pt.y), P.center, std::cos(rad), std::sin(rad));
             c.ptx = lt.x; c.pty = lt.y;
             all.push_back(c);
             continue;
         }
-        const CandState& cs = state[id];
-        if (!cs.reached0) continue;     // broke out at a layer > 0 (:331-332)
+        const int li = pos[id];
+        if (li < 0) continue;           // broke out at a layer > 0 (:331-332)
+        const CandState& cs = state[li];
         // layer 0 (:282-358) from the device's ROI records
         const int d = L - 1;
         const double astep = std::atan(2.0 / std::max(t0.w, t0.h)) * kR2D;
@@ -707,7 +722,7 @@ void finish_source(fpm_ctx* ctx, int s, std::vector<fpm_result>& out) {
         int imax = 0;
         double big = -1;
         for (int j = 0; j < P.n3; ++j) {
-            const RoiRecord& r = rec[(size_t)id * P.n3 + j];
+            const RoiRecord& r = rec[(size_t)li * P.n3 + j];
             HostMatch m{};
             m.ptx = r.mx; m.pty = r.my;
             m.score = r.score;
@@ -786,16 +801,46 @@ int launch_search(fpm_ctx* ctx) {
     return FPM_OK;
 }
 
-int run_staged(fpm_ctx* ctx, std::vector<std::vector<fpm_result>>& results) {
+// First half of a staged search: plan, then the whole device pass enqueued on the context's stream (no wait).
+int start_staged(fpm_ctx* ctx) {
+    ctx->t_call0 = std::chrono::steady_clock::now();
     int rc = build_plan(ctx);
     if (rc != FPM_OK) return rc;
+    if (!ctx->t_ev[0]) {
+        HIP_TRY(hipEventCreate(&ctx->t_ev[0]));
+        HIP_TRY(hipEventCreate(&ctx->t_ev[1]));
+    }
+    HIP_TRY(hipEventRecord(ctx->t_ev[0], ctx->stream));
     rc = launch_search(ctx);
     if (rc != FPM_OK) return rc;
+    HIP_TRY(hipEventRecord(ctx->t_ev[1], ctx->stream));
+    ctx->pending = true;
+    return FPM_OK;
+}
+
+// Second half: wait for the device pass, then the host's reference-order post-processing per source.
+int complete_staged(fpm_ctx* ctx, std::vector<std::vector<fpm_result>>& results) {
+    if (!ctx->pending) { ctx->err = "no search in flight"; return FPM_E_INVALID_ARG; }
+    ctx->pending = false;
+    const auto c0 = ctx->t_call0;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    const auto c1 = std::chrono::steady_clock::now();
+    {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, ctx->t_ev[0], ctx->t_ev[1]) == hipSuccess) ctx->last_device_ms = ms;
+    }
     prof_collect(ctx);
     Plan& P = ctx->plan;
     results.assign(P.S, {});
-    for (int s = 0; s < P.S; ++s) finish_source(ctx, s, results[s]);
+    std::vector<int> pos;
+    if (P.L > 0) {
+        const char* hb = P.h_out.as<char>();
+        const int n0 = ((const int32_t*)(hb + P.h_live))[P.L - 1];
+        const int32_t* ids = (const int32_t*)(hb + P.h_live0);
+        pos.assign(P.C, -1);
+        for (int li = 0; li < n0; ++li) pos[ids[li]] = li;
+    }
+    for (int s = 0; s < P.S; ++s) finish_source(ctx, s, results[s], pos);
     // stats: [angles, top candidates, live entering layer L-1 .. 0] (totals over the batch)
     const char* h = P.h_out.as<char>();
     const int32_t* counts = (const int32_t*)(h + P.h_counts);
@@ -826,7 +871,16 @@ int run_staged(fpm_ctx* ctx, std::vector<std::vector<fpm_result>>& results) {
             ctx->kp[FPM_K_ROI_EVAL].bytes += rois * ((int64_t)t.h * 49 * 4 + nch * 49 * 12 + (int64_t)sizeof(RoiRecord));
         }
     }
+    const auto c2 = std::chrono::steady_clock::now();
+    ctx->last_host_ms = std::chrono::duration<double, std::milli>(c2 - c1).count();
+    ctx->last_call_ms = std::chrono::duration<double, std::milli>(c2 - c0).count();
     return FPM_OK;
+}
+
+int run_staged(fpm_ctx* ctx, std::vector<std::vector<fpm_result>>& results) {
+    const int rc = start_staged(ctx);
+    if (rc != FPM_OK) return rc;
+    return complete_staged(ctx, results);
 }
 
 int upload_sources(fpm_ctx* ctx, const uint8_t* const* grays, int count, int w, int h, size_t stride) {
@@ -886,6 +940,8 @@ int fpm_destroy(fpm_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->graph) (void)hipGraphExecDestroy(ctx->graph);
+    for (hipEvent_t e : ctx->t_ev)
+        if (e) (void)hipEventDestroy(e);
     ctx->plan.release();
     ctx->d_tmpl.release(); ctx->d_tmpl8.release(); ctx->d_tsum.release(); ctx->d_src.release();
     ctx->d_op_a.release(); ctx->d_op_b.release(); ctx->d_op_job.release();
@@ -965,7 +1021,7 @@ int fpm_learn(fpm_ctx* ctx, const uint8_t* gray, int32_t w, int32_t h, size_t st
             lv[l].tsum_off = os;
             os += round_up(lv[l].h, kMmaRows);
         }
-        o8 += 64;   // slack: k_roi_corr prefetches one 64-byte block past a row's last
+        o8 += 256;   // slack: k_roi_corr prefetches up to 2 64-byte blocks past a row's last
         std::vector<int8_t> h8(o8, 0);
         std::vector<int32_t> hs(os, 0);
         for (int l = 0; l <= L; ++l)
@@ -1004,6 +1060,7 @@ int fpm_stage_sources(fpm_ctx* ctx, const uint8_t* const* grays, int32_t count, 
     if (!grays || count <= 0 || w <= 0 || h <= 0 || stride < (size_t)w) { ctx->err = "bad sources"; return FPM_E_INVALID_ARG; }
     for (int i = 0; i < count; ++i)
         if (!grays[i]) { ctx->err = "null source"; return FPM_E_INVALID_ARG; }
+    if (ctx->pending) { ctx->err = "a search is in flight (fpm_match_staged_finish first)"; return FPM_E_INVALID_ARG; }
     int rc = check_sizes(ctx, w, h);
     if (rc != FPM_OK) return rc;
     HIP_TRY(hipSetDevice(ctx->device));
@@ -1013,23 +1070,42 @@ int fpm_stage_sources(fpm_ctx* ctx, const uint8_t* const* grays, int32_t count, 
     return FPM_OK;
 }
 
-int fpm_match_staged(fpm_ctx* ctx, fpm_result* out, int32_t cap, int32_t* n_results) {
-    if (!ctx || !n_results) return FPM_E_INVALID_ARG;
-    if (!ctx->learned) { ctx->err = "template not learned"; return FPM_E_NOT_LEARNED; }
-    if (ctx->S <= 0) { ctx->err = "no staged sources"; return FPM_E_INVALID_ARG; }
-    HIP_TRY(hipSetDevice(ctx->device));
-    std::vector<std::vector<fpm_result>> res;
-    int rc = run_staged(ctx, res);
-    if (rc != FPM_OK) return rc;
+static int copy_results(const std::vector<std::vector<fpm_result>>& res, fpm_result* out, int32_t cap,
+                        int32_t* n_results) {
     int status = FPM_OK;
-    for (int s = 0; s < ctx->S; ++s) {
+    for (size_t s = 0; s < res.size(); ++s) {
         n_results[s] = (int32_t)res[s].size();
         for (int i = 0; i < (int)res[s].size(); ++i) {
-            if (i < cap && out) out[(size_t)s * cap + i] = res[s][i];
+            if (i < cap && out) out[s * (size_t)cap + i] = res[s][i];
             else status = FPM_E_CAPACITY;
         }
     }
     return status;
+}
+
+int fpm_match_staged_launch(fpm_ctx* ctx) {
+    if (!ctx) return FPM_E_INVALID_ARG;
+    if (!ctx->learned) { ctx->err = "template not learned"; return FPM_E_NOT_LEARNED; }
+    if (ctx->S <= 0) { ctx->err = "no staged sources"; return FPM_E_INVALID_ARG; }
+    if (ctx->pending) { ctx->err = "a search is already in flight"; return FPM_E_INVALID_ARG; }
+    HIP_TRY(hipSetDevice(ctx->device));
+    return start_staged(ctx);
+}
+
+int fpm_match_staged_finish(fpm_ctx* ctx, fpm_result* out, int32_t cap, int32_t* n_results) {
+    if (!ctx || !n_results) return FPM_E_INVALID_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    std::vector<std::vector<fpm_result>> res;
+    const int rc = complete_staged(ctx, res);
+    if (rc != FPM_OK) return rc;
+    return copy_results(res, out, cap, n_results);
+}
+
+int fpm_match_staged(fpm_ctx* ctx, fpm_result* out, int32_t cap, int32_t* n_results) {
+    if (!n_results) return FPM_E_INVALID_ARG;
+    const int rc = fpm_match_staged_launch(ctx);
+    if (rc != FPM_OK) return rc;
+    return fpm_match_staged_finish(ctx, out, cap, n_results);
 }
 
 // TemplateMatcher::match (TemplateMatcher.cpp:97-437)
@@ -1038,6 +1114,7 @@ int fpm_match(fpm_ctx* ctx, const uint8_t* gray, int32_t w, int32_t h, size_t st
     if (!ctx || !n_results) return FPM_E_INVALID_ARG;
     *n_results = 0;
     if (!gray || w <= 0 || h <= 0 || stride < (size_t)w) { ctx->err = "empty source"; return FPM_E_INVALID_ARG; }
+    if (ctx->pending) { ctx->err = "a search is in flight (fpm_match_staged_finish first)"; return FPM_E_INVALID_ARG; }
     int rc = check_sizes(ctx, w, h);
     if (rc != FPM_OK) return rc;
     HIP_TRY(hipSetDevice(ctx->device));
@@ -1171,6 +1248,14 @@ int fpm_profile_enable(fpm_ctx* ctx, int32_t enable) {
 int fpm_profile_reset(fpm_ctx* ctx) {
     if (!ctx) return FPM_E_INVALID_ARG;
     for (auto& k : ctx->kp) { k.ms = 0; k.launches = 0; k.bytes = 0; k.used = 0; }
+    return FPM_OK;
+}
+
+int fpm_profile_last(const fpm_ctx* ctx, double* device_ms, double* host_ms, double* call_ms) {
+    if (!ctx || !device_ms || !host_ms || !call_ms) return FPM_E_INVALID_ARG;
+    *device_ms = ctx->last_device_ms;
+    *host_ms = ctx->last_host_ms;
+    *call_ms = ctx->last_call_ms;
     return FPM_OK;
 }
 

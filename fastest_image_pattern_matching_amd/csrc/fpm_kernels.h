@@ -127,6 +127,22 @@ struct RoiArgs {
 };
 
 
+// Final pack of a search's results into pinned host memory (replaces several device -> host copies): top-peak
+// counts and peaks, live counts, and for the candidates that reached layer 0 (the layer-0 live list) their ids,
+// states and refinement records, compacted by live index.
+struct PackArgs {
+    const int32_t* counts; int32_t J;
+    const Peak* peaks; int32_t C;
+    const int32_t* livecnt; int32_t nlive;
+    const int32_t* live0;          // layer-0 live list (nullptr when the top layer is layer 0)
+    const int32_t* live0_count;
+    const CandState* state;
+    const RoiRecord* rec;
+    int32_t n3;
+    char* host;                    // pinned host buffer
+    size_t o_counts, o_peaks, o_live, o_live0, o_state0, o_rec0;
+};
+
 // launchers (stream-ordered, no synchronisation)
 void launch_pyr_down(const uint8_t* src, int sw, int sh, int sp, size_t s_img, uint8_t* dst, int dw, int dh,
                      int dp, size_t d_img, int nimg, hipStream_t st);
@@ -144,10 +160,11 @@ bool roi_small_fits(int tw, int th);   // the single-kernel small-template refin
 size_t roi_small_lds(int tw, int th);
 void launch_roi_small(const RoiArgs& a, hipStream_t st);
 void launch_cand_step(const RoiArgs& a, int max_items, hipStream_t st);
+void launch_pack(const PackArgs& a, hipStream_t st);
 int roi_pick_rc(int tw, int th);
 int roi_pitch_for(int tw);
 int roi_tiles_for(int tw, int th);   // 32x32 warp tiles of a (tw+6) x (th+6) ROI
-size_t roi_corr_lds(int roi_pitch, int tw, int rc);
+size_t roi_corr_lds(int roi_pitch, int tw, int rc, bool global_a);
 constexpr int kMmaRows = 16;   // template rows per MFMA correlation chunk (M of v_mfma_i32_16x16x64_i8)
 
 }  // namespace fpm

@@ -559,10 +559,10 @@ __host__ __device__ inline int tmpl_lds_pitch(int tp8) {
     return q * 16;
 }
 
-size_t roi_corr_lds(int roi_pitch, int tw, int /*rc*/) {
+size_t roi_corr_lds(int roi_pitch, int tw, int /*rc*/, bool ga) {
     constexpr int src_rows = 2 * kMmaRows + 6;
     const int tp8 = 64 * ((tw + 63) / 64);
-    return (size_t)src_rows * roi_pitch + (size_t)2 * kMmaRows * tmpl_lds_pitch(tp8) +
+    return (size_t)src_rows * roi_pitch + (ga ? 0 : (size_t)2 * kMmaRows * tmpl_lds_pitch(tp8)) +
            sizeof(uint32_t) * (2 * src_rows + 2 * 7 * src_rows) + 64;
 }
 
@@ -909,16 +909,51 @@ __device__ __forceinline__ void band_mfma(const uint8_t* ap, const uint8_t* bp, 
     acc[0] = c0; acc[1] = c1; acc[2] = c2; acc[3] = c3; acc[4] = c4; acc[5] = c5; acc[6] = c6;
 }
 
+// The same with the A fragments read from the global i8 slab (L2-resident, shared by every ROI of the layer):
+// two k-steps of A in flight; the empty asm keeps the compiler from sinking the prefetch to its use.
+// The slab carries >= 256 bytes of slack past its last row.
+__device__ __forceinline__ void band_mfma_ga(const int8_t* ap, const uint8_t* bp, int nk, fpm_v4i acc[7]) {
+    fpm_v4i c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0, c4 = c0, c5 = c0, c6 = c0;
+    fpm_v4i p0 = *(const fpm_v4i*)ap, p1 = *(const fpm_v4i*)(ap + 64);
+    for (int k = 0; k < nk; ++k) {
+        const fpm_v4i av = p0;
+        p0 = p1;
+        p1 = *(const fpm_v4i*)(ap + 64 * (k + 2));
+        asm volatile("" ::: "memory");
+        const uint8_t* bk = (const uint8_t*)__builtin_assume_aligned(bp + 64 * k, 16);
+        const uint4 lo = *(const uint4*)bk;
+        const uint2 hi = *(const uint2*)(bk + 16);
+        const uint32_t w0 = lo.x, w1 = lo.y, w2 = lo.z, w3 = lo.w, w4 = hi.x, w5 = hi.y;
+        const uint32_t a10 = __builtin_amdgcn_alignbyte(w1, w0, 1), a21 = __builtin_amdgcn_alignbyte(w2, w1, 1),
+                       a32 = __builtin_amdgcn_alignbyte(w3, w2, 1), a43 = __builtin_amdgcn_alignbyte(w4, w3, 1),
+                       a54 = __builtin_amdgcn_alignbyte(w5, w4, 1);
+        const uint32_t b10 = __builtin_amdgcn_alignbyte(w1, w0, 2), b21 = __builtin_amdgcn_alignbyte(w2, w1, 2),
+                       b32 = __builtin_amdgcn_alignbyte(w3, w2, 2), b43 = __builtin_amdgcn_alignbyte(w4, w3, 2),
+                       b54 = __builtin_amdgcn_alignbyte(w5, w4, 2);
+        const uint32_t e10 = __builtin_amdgcn_alignbyte(w1, w0, 3), e21 = __builtin_amdgcn_alignbyte(w2, w1, 3),
+                       e32 = __builtin_amdgcn_alignbyte(w3, w2, 3), e43 = __builtin_amdgcn_alignbyte(w4, w3, 3);
+        c0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)w0, (int)w1, (int)w2, (int)w3}, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)a10, (int)a21, (int)a32, (int)a43}, c1, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)b10, (int)b21, (int)b32, (int)b43}, c2, 0, 0, 0);
+        c3 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)e10, (int)e21, (int)e32, (int)e43}, c3, 0, 0, 0);
+        c4 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)w1, (int)w2, (int)w3, (int)w4}, c4, 0, 0, 0);
+        c5 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)a21, (int)a32, (int)a43, (int)a54}, c5, 0, 0, 0);
+        c6 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)b21, (int)b32, (int)b43, (int)b54}, c6, 0, 0, 0);
+    }
+    acc[0] = c0; acc[1] = c1; acc[2] = c2; acc[3] = c3; acc[4] = c4; acc[5] = c5; acc[6] = c6;
+}
+
 // MODE (profiling ablations in scripts/roi_microbench.hip; the product uses 0): 2 = no MFMA loop, 3 = no staging
-template <int MODE>
-__global__ __launch_bounds__(256) void k_roi_corr(RoiArgs a) {
+// GA: A operand read from the global i8 slab (no template rows in LDS); WPE: register cap (waves per SIMD)
+template <int MODE, bool GA, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_corr(RoiArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tw = a.tw, th = a.th, RW = tw + 6;
     const int SBp = a.roi_pitch;
     const int TBp = tmpl_lds_pitch(a.tp8);
     uint8_t* SB = smem;                                        // kBandSrc rows x SBp, bytes ^ 0x80
-    uint8_t* TB = SB + (size_t)kBandSrc * SBp;                 // kBandRows template rows (i8) x TBp
-    uint32_t* rall = (uint32_t*)(TB + (size_t)kBandRows * TBp); // full-row sums of I
+    uint8_t* TB = SB + (size_t)kBandSrc * SBp;                 // kBandRows template rows (i8) x TBp (!GA)
+    uint32_t* rall = (uint32_t*)(TB + (GA ? 0 : (size_t)kBandRows * TBp)); // full-row sums of I
     uint32_t* rallq = rall + kBandSrc;                         // full-row sums of I^2
     uint32_t* wi = rallq + kBandSrc;                           // [row][dx] window sums of I
     uint32_t* wq = wi + kBandSrc * 7;                          // [row][dx] window sums of I^2
@@ -984,7 +1019,7 @@ __global__ __launch_bounds__(256) void k_roi_corr(RoiArgs a) {
             atomicAdd(&rall[r], s1);
             atomicAdd(&rallq[r], s2);
         }
-        {   // template rows T0 .. T0 + 16*ceil(rb/16) - 1 of the i8 slab
+        if (!GA) {   // template rows T0 .. T0 + 16*ceil(rb/16) - 1 of the i8 slab
             const int trows = (rb + kMmaRows - 1) / kMmaRows * kMmaRows;
             stage_block16(TB, TBp, (const uint8_t*)a.tmpl8 + (size_t)T0 * a.tp8, a.tp8, trows, a.tp8 >> 4, tid, 256);
         }
@@ -1001,12 +1036,14 @@ __global__ __launch_bounds__(256) void k_roi_corr(RoiArgs a) {
         __syncthreads();
         const bool active = kMmaRows * mt < rb && kMmaRows * nt < nsrc;   // wave-uniform
         if (MODE != 2 && active) {
-            const uint8_t* ap = TB + (size_t)(kMmaRows * mt + n) * TBp + 16 * g;
             int sr = kMmaRows * nt + n;
             if (sr >= nsrc) sr = 0;   // column outside the band: computed, never stored
             const uint8_t* bp = SB + (size_t)sr * SBp + 16 * g;
             fpm_v4i acc[7];
-            band_mfma(ap, bp, a.nk, acc);
+            if (GA)
+                band_mfma_ga(a.tmpl8 + (size_t)(T0 + kMmaRows * mt + n) * a.tp8 + 16 * g, bp, a.nk, acc);
+            else
+                band_mfma(TB + (size_t)(kMmaRows * mt + n) * TBp + 16 * g, bp, a.nk, acc);
             // D_dx: col = lane & 15 -> source row 16*nt + n, row = 4*(lane >> 4) + r -> template row 16*mt + 4g + r
             uint32_t* rs_out = a.rowsum + (((size_t)th * 49 + 3) & ~(size_t)3) * slot + (size_t)T0 * 49;
             const uint32_t kFix = 16384u * (uint32_t)tw;
@@ -1573,17 +1610,20 @@ void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_roi_warp<kWarpFootBatch>, dim3(grid), dim3(256), 0, st, a);
 }
 
+constexpr bool kCorrGlobalA = true;   // measured in scripts/roi_microbench.hip
+constexpr int kCorrWaves = 3;
 void launch_roi_corr(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0 || a.equal1) return;
-    const size_t lds = roi_corr_lds(a.roi_pitch, a.tw, a.rc);
+    const size_t lds = roi_corr_lds(a.roi_pitch, a.tw, a.rc, kCorrGlobalA);
     static size_t lds_attr = 0;
     if (lds > 65536 && lds > lds_attr) {
-        (void)hipFuncSetAttribute((const void*)k_roi_corr<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)k_roi_corr<0, kCorrGlobalA, kCorrWaves>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         lds_attr = lds;
     }
     const long items = (long)a.slot_cap * ((a.th + kBandRows - 1) / kBandRows);
     const int grid = (int)(items < 16384 ? items : 16384);
-    hipLaunchKernelGGL(k_roi_corr<0>, dim3(grid), dim3(256), lds, st, a);
+    hipLaunchKernelGGL((k_roi_corr<0, kCorrGlobalA, kCorrWaves>), dim3(grid), dim3(256), lds, st, a);
 }
 
 void launch_roi_eval(const RoiArgs& a, hipStream_t st) {
@@ -1616,6 +1656,38 @@ void launch_cand_step(const RoiArgs& a, int max_items, hipStream_t st) {
     int grid = (max_items + 255) / 256;
     if (grid > 1024) grid = 1024;
     hipLaunchKernelGGL(k_cand_step, dim3(grid), dim3(256), 0, st, a);
+}
+
+// ============================================================================================== pack
+__global__ __launch_bounds__(256) void k_pack(PackArgs a) {
+    const int tid = blockIdx.x * 256 + threadIdx.x, nthr = gridDim.x * 256;
+    int32_t* hc = (int32_t*)(a.host + a.o_counts);
+    for (int i = tid; i < a.J; i += nthr) hc[i] = a.counts[i];
+    int4* hp = (int4*)(a.host + a.o_peaks);
+    for (int i = tid; i < a.C; i += nthr) hp[i] = *(const int4*)(a.peaks + i);
+    int32_t* hl = (int32_t*)(a.host + a.o_live);
+    for (int i = tid; i < a.nlive; i += nthr) hl[i] = a.livecnt[i];
+    if (a.live0) {
+        const int n0 = *a.live0_count;
+        int32_t* hi = (int32_t*)(a.host + a.o_live0);
+        CandState* hs = (CandState*)(a.host + a.o_state0);
+        for (int li = tid; li < n0; li += nthr) {
+            const int id = a.live0[li];
+            hi[li] = id;
+            hs[li] = a.state[id];
+        }
+        uint32_t* hr = (uint32_t*)(a.host + a.o_rec0);
+        constexpr int RW = sizeof(RoiRecord) / 4;
+        for (int i = tid; i < n0 * a.n3 * RW; i += nthr) {
+            const int q = i / RW, w = i - q * RW, li = q / a.n3, j = q - li * a.n3;
+            hr[i] = ((const uint32_t*)(a.rec + (size_t)a.live0[li] * a.n3 + j))[w];
+        }
+    }
+    __threadfence_system();
+}
+
+void launch_pack(const PackArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL(k_pack, dim3(16), dim3(256), 0, st, a);
 }
 
 }  // namespace fpm

@@ -33,6 +33,11 @@ class SingleTargetMatch:
         return SingleTargetMatch((r.lt_x, r.lt_y), (r.rt_x, r.rt_y), (r.rb_x, r.rb_y), (r.lb_x, r.lb_y),
                                  (r.cx, r.cy), r.angle, r.score)
 
+    @staticmethod
+    def from_row(r) -> "SingleTargetMatch":
+        v = [float(x) for x in r]
+        return SingleTargetMatch((v[0], v[1]), (v[2], v[3]), (v[4], v[5]), (v[6], v[7]), (v[8], v[9]), v[10], v[11])
+
     def getCenterQPoint(self):
         return self.ptCenter
 
@@ -144,19 +149,44 @@ class TemplateMatcher:
         self._staged = len(gs)
 
     def match_staged(self) -> List[List[SingleTargetMatch]]:
-        n_src = self._staged
+        counts, res = self.match_staged_array()
+        return [[SingleTargetMatch.from_row(res[s, i]) for i in range(counts[s])] for s in range(len(counts))]
+
+    def _views(self, n_src):
+        if self._bufs is None or self._bufs[0] != (n_src, self._cap):
+            out = (L.Result * (self._cap * n_src))()
+            n = (C.c_int32 * n_src)()
+            views = (np.frombuffer(n, dtype=np.int32), np.frombuffer(out, dtype=np.float64).reshape(n_src, self._cap, 12))
+            self._bufs = ((n_src, self._cap), out, n, views)
+        return self._bufs
+
+    def match_staged_array(self):
+        """Like match_staged, returning (counts[int32, n_src], results[f64, n_src, cap, 12]) views of reused buffers
+        (fields in s_SingleTargetMatch order) instead of Python objects; valid until the next call."""
+        self.match_staged_launch()
+        return self.match_staged_finish_array()
+
+    def match_staged_launch(self):
+        """Enqueue the device pass over the staged sources and return (fpm_match_staged_launch)."""
         self._push()
+        rc = self._check(self._lib.fpm_match_staged_launch(self._ctx), "match_staged_launch")
+        if rc != L.FPM_OK:
+            raise RuntimeError(f"fpm_match_staged_launch failed with {rc}: {self.last_error()}")
+
+    def match_staged_finish_array(self):
+        """Wait for the launched pass and post-process it (fpm_match_staged_finish); array views as
+        match_staged_array.  On a full result buffer the search is re-run with a larger one."""
+        n_src = self._staged
         while True:
-            if self._bufs is None or self._bufs[0] != (n_src, self._cap):
-                self._bufs = ((n_src, self._cap), (L.Result * (self._cap * n_src))(), (C.c_int32 * n_src)())
-            _, out, n = self._bufs
-            rc = self._check(self._lib.fpm_match_staged(self._ctx, out, self._cap, n), "match_staged")
+            _, out, n, views = self._views(n_src)
+            rc = self._check(self._lib.fpm_match_staged_finish(self._ctx, out, self._cap, n), "match_staged_finish")
             if rc == L.FPM_E_CAPACITY:
                 self._cap = max(self._cap * 2, max(n))
+                self.match_staged_launch()
                 continue
             if rc != L.FPM_OK:
-                raise RuntimeError(f"fpm_match_staged failed with {rc}: {self.last_error()}")
-            return [[SingleTargetMatch.from_c(out[s * self._cap + i]) for i in range(n[s])] for s in range(n_src)]
+                raise RuntimeError(f"fpm_match_staged_finish failed with {rc}: {self.last_error()}")
+            return views
 
     def search_stats(self) -> List[int]:
         buf = (C.c_int64 * 64)()
@@ -249,6 +279,12 @@ class TemplateMatcher:
 
     def profile_reset(self):
         self._lib.fpm_profile_reset(self._ctx)
+
+    def profile_last(self):
+        """(device_ms, host_ms, call_ms) of the last search call (fpm_profile_last)."""
+        d, h, c = C.c_double(), C.c_double(), C.c_double()
+        self._lib.fpm_profile_last(self._ctx, C.byref(d), C.byref(h), C.byref(c))
+        return d.value, h.value, c.value
 
     def profile_get(self, kernel: int):
         ms, n, b = C.c_double(), C.c_int64(), C.c_int64()

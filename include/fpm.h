@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define FPM_ABI_VERSION 3
+#define FPM_ABI_VERSION 5
 
 /* status codes */
 #define FPM_OK 0
@@ -99,6 +99,11 @@ int fpm_match(fpm_ctx* ctx, const uint8_t* gray, int32_t width, int32_t height, 
 int fpm_stage_sources(fpm_ctx* ctx, const uint8_t* const* grays, int32_t count, int32_t width,
                       int32_t height, size_t stride);
 int fpm_match_staged(fpm_ctx* ctx, fpm_result* out, int32_t cap_per_source, int32_t* n_results);
+/* fpm_match_staged split in two: _launch enqueues the whole device pass on the context's stream and returns;
+ * _finish waits for it and runs the host post-processing.  Several contexts (one stream each) on one device
+ * can have searches in flight at once; the staged sources must not be re-staged in between. */
+int fpm_match_staged_launch(fpm_ctx* ctx);
+int fpm_match_staged_finish(fpm_ctx* ctx, fpm_result* out, int32_t cap_per_source, int32_t* n_results);
 
 /* --- pixel operators (L1 kernels exposed for parity tests and standalone use) ----------------------- */
 /* cv::pyrDown (8U, 5x5 Gaussian, reflect-101), as called by cv::buildPyramid (TemplateMatcher.cpp:55,124).
@@ -148,6 +153,10 @@ int fpm_profile_enable(fpm_ctx* ctx, int32_t enable);
 int fpm_profile_reset(fpm_ctx* ctx);
 int fpm_profile_get(const fpm_ctx* ctx, int32_t kernel, double* total_ms, int64_t* launches,
                     int64_t* bytes);
+/* Timing of the last fpm_match / fpm_match_staged call (always collected): device_ms = GPU time of the search
+ * (events around the whole device pass, results copy included), host_ms = host post-processing after the device
+ * pass (reference-order sort, layer-0 decision, filters, conversion), call_ms = wall time of the call. */
+int fpm_profile_last(const fpm_ctx* ctx, double* device_ms, double* host_ms, double* call_ms);
 
 #ifdef __cplusplus
 }

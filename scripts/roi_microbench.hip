@@ -82,7 +82,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&a.wsum, (size_t)C * n3 * a.nchunk * 49 * 4));
     CK(hipMalloc(&a.wsq, (size_t)C * n3 * a.nchunk * 49 * 8));
     CK(hipMalloc(&a.rec, sizeof(RoiRecord) * C * n3));
-        printf("rois %d rc %d chunks %d corr lds %zu\n", C * n3, a.rc, a.nchunk, roi_corr_lds(roi_pitch_for(TW), TW, a.rc));
+        printf("rois %d rc %d chunks %d corr lds %zu / %zu\n", C * n3, a.rc, a.nchunk, roi_corr_lds(roi_pitch_for(TW), TW, a.rc, false), roi_corr_lds(roi_pitch_for(TW), TW, a.rc, true));
     // ---- product kernels (tables -> warp -> corr -> eval) --------------------------------------------------
     a.tabw = roi_pitch_for(TW); a.tabh = ((TH + 6) + 3) & ~3;
     a.roi_pitch = roi_pitch_for(TW); a.roi_stride = ((size_t)a.roi_pitch * (TH + 7) + 255) & ~(size_t)255;
@@ -112,10 +112,15 @@ int main(int argc, char** argv) {
     timeit([&] { launch_roi_corr(a, 0); }, "prod corr");
     timeit([&] { launch_roi_eval(a, 0); }, "prod eval");
     {
-        const size_t lds = roi_corr_lds(a.roi_pitch, a.tw, a.rc);
-        const int grid = std::min(C * n3 * ((TH + kBandRows - 1) / kBandRows), 16384);
-        timeit([&] { hipLaunchKernelGGL(k_roi_corr<2>, dim3(grid), dim3(256), lds, 0, a); }, "corr no mfma");
-        timeit([&] { hipLaunchKernelGGL(k_roi_corr<3>, dim3(grid), dim3(256), lds, 0, a); }, "corr no staging");
+        const size_t lds0 = roi_corr_lds(a.roi_pitch, a.tw, a.rc, false), lds1 = roi_corr_lds(a.roi_pitch, a.tw, a.rc, true);
+        const int grid = std::min(C * n3 * ((TH + 31) / 32), 16384);
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, false, 1>), dim3(grid), dim3(256), lds0, 0, a); }, "corr ldsA free");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, false, 4>), dim3(grid), dim3(256), lds0, 0, a); }, "corr ldsA w4");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 1>), dim3(grid), dim3(256), lds1, 0, a); }, "corr globA free");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3>), dim3(grid), dim3(256), lds1, 0, a); }, "corr globA w3");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 4>), dim3(grid), dim3(256), lds1, 0, a); }, "corr globA w4");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<2, true, 4>), dim3(grid), dim3(256), lds1, 0, a); }, "corr globA w4 no mfma");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<3, true, 4>), dim3(grid), dim3(256), lds1, 0, a); }, "corr globA w4 no stage");
         launch_roi_corr(a, 0);
     }
     {   // host check of k_roi_corr on a few ROI slots

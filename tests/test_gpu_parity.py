@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 from fastest_image_pattern_matching_amd import synth
+from fastest_image_pattern_matching_amd.matcher import SingleTargetMatch
 from tests import oracle
 
 pytestmark = pytest.mark.gpu
@@ -202,6 +203,35 @@ def test_batch_equals_single(hip, templates):
     batch = hip.match_batch(srcs)
     for k, s in enumerate(srcs):
         assert_same_results(batch[k], o.match(s), f"batch{k}")
+
+
+def test_concurrent_contexts(hip, templates, gpu_matcher_factory):
+    """Two contexts (two HIP streams) with searches in flight at once (fpm_match_staged_launch / _finish) give
+    the oracle's results; staging or a second launch while a search is in flight is refused."""
+    t = templates["Dst10"]
+    srcs = []
+    for k in range(6):
+        s = synth.noise(360, 300, 128, 10, 70 + k)
+        synth.paste_rotated(s, t, 110 + 25 * k, 130 + 8 * k, 35.0 * k - 80)
+        srcs.append(s)
+    o = oracle.OracleMatcher().set(max_pos=3, tolerance_angle=180.0)
+    o.learnPattern(t)
+    ms = [gpu_matcher_factory(max_pos=3, tolerance_angle=180.0) for _ in range(2)]
+    for m, part in zip(ms, (srcs[:3], srcs[3:])):
+        assert m.learnPattern(t)
+        m.stage(part)
+    for rep in range(2):
+        for m in ms:
+            m.match_staged_launch()
+        with pytest.raises(ValueError):
+            ms[0].stage(srcs[:3])
+        with pytest.raises(RuntimeError):
+            ms[1].match_staged_launch()
+        outs = [m.match_staged_finish_array() for m in ms]
+        got = [[SingleTargetMatch.from_row(res[s_, i]) for i in range(cnt[s_])] for cnt, res in outs
+               for s_ in range(len(cnt))]
+        for k, s in enumerate(srcs):
+            assert_same_results(got[k], o.match(s), f"ctx{k // 3} src{k} rep{rep}")
 
 
 def test_error_behaviour(hip, templates):
