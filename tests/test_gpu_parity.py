@@ -187,6 +187,59 @@ def test_constant_template(hip):
     assert_same_results(gpu, orc, "equal1")
 
 
+# ---------------------------------------------------------------------------------------- BASELINE configs
+def test_config2_src10_blockmax(hip, templates):
+    """configs[2] at full size: 3648x3648 Src10 surrogate, Dst10 x 144, TargetNum 100 -> s_BlockMax peaks."""
+    s, t = synth.src10_scene(templates["Dst10"])
+    gpu, orc, ostats, gstats = _run_both(hip, s, t, max_pos=100, score=0.7, tolerance_angle=0.0)
+    assert gstats == ostats
+    assert_same_results(gpu, orc, "src10")
+    assert len(orc) >= 100
+
+
+def test_config2_src10_rotation_sweep(hip, templates):
+    """configs[2] stress (+-180 deg, 47 top angles, TargetNum 100) on the 1824x1824 top-left quarter."""
+    s, t = synth.src10_scene(templates["Dst10"])
+    crop = np.ascontiguousarray(s[:1824, :1824])
+    gpu, orc, ostats, gstats = _run_both(hip, crop, t, max_pos=100, score=0.7, tolerance_angle=180.0)
+    assert gstats == ostats
+    assert_same_results(gpu, orc, "src10_180")
+    assert len(orc) >= 30
+
+
+def test_config3_batch_4096(hip):
+    """configs[3]: 4096x4096 sources searched as one device batch, 512x512 template, +-180 deg (reference step)."""
+    srcs, t = synth.batch_sources(2)
+    o = oracle.OracleMatcher().set(max_pos=1, tolerance_angle=180.0)
+    o.learnPattern(t)
+    hip.resetParams()
+    hip.setMaxPositions(1)
+    hip.setToleranceAngle(180.0)
+    assert hip.learnPattern(t)
+    batch = hip.match_batch(srcs)
+    for k, s in enumerate(srcs):
+        orc = o.match(s)
+        assert_same_results(batch[k], orc, f"batch4096_{k}")
+        assert len(orc) >= 1
+
+
+def test_config4_src5_rotation_set(hip, templates):
+    """configs[4]: the Src5 rotation set (0, 45, ..., 315 deg) with sub-pixel estimation, as one device batch."""
+    srcs, t = synth.src5_set(templates["Dst5"])
+    o = oracle.OracleMatcher().set(max_pos=1, tolerance_angle=180.0, subpixel=1)
+    o.learnPattern(t)
+    hip.resetParams()
+    hip.setMaxPositions(1)
+    hip.setToleranceAngle(180.0)
+    hip.setSubPixelEstimation(True)
+    assert hip.learnPattern(t)
+    batch = hip.match_batch(srcs)
+    for k, s in enumerate(srcs):
+        orc = o.match(s)
+        assert_same_results(batch[k], orc, f"src5_{45 * k}")
+        assert len(orc) == 1
+
+
 def test_batch_equals_single(hip, templates):
     t = templates["Dst10"]
     srcs = []
