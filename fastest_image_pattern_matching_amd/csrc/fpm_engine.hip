@@ -412,7 +412,9 @@ int build_plan(fpm_ctx* ctx) {
         P.roi_pitch = roi_pitch_for(max_w);
         P.tabw = P.roi_pitch;
         P.tabh = round_up((int)max_rows + 6, 4);
-        P.roi_stride = round_up((size_t)P.roi_pitch * (max_rows + 6 + 1), (size_t)256);
+        P.roi_stride = 0;
+        for (int l = 0; l < L; ++l)
+            P.roi_stride = std::max(P.roi_stride, roi_tiles_bytes(ctx->tmpl[l].w, ctx->tmpl[l].h));
         const size_t per_roi = sizeof(int32_t) * 2 * (P.tabw + P.tabh) + sizeof(int4) * P.tdesc_stride + P.roi_stride + max_rows * 49 * 4 +
                                max_chunks * 49 * 12;
         const size_t budget = (size_t)16 << 30;   // of 288 GB HBM; rounds only beyond this

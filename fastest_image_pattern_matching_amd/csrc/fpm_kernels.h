@@ -110,8 +110,8 @@ struct RoiArgs {
     int32_t tabw, tabh;
     int4* tdesc;             // [slot][tdesc_stride] per 32x32 ROI tile: source footprint box + flags
     int32_t tdesc_stride;
-    uint8_t* roi;            // [slot] sampled ROI, (th+6) rows x roi_pitch bytes
-    int32_t roi_pitch;
+    uint8_t* roi;            // [slot] sampled ROI, tile-major: 32 x 32 tiles of 1 KB, row of tiles by row
+    int32_t roi_pitch;       // LDS row pitch of staged ROI rows (k_roi_corr)
     size_t roi_stride;
     uint32_t* rowsum;        // [slot][th][49] exact int32 per-row dot products
     uint32_t* wsum;          // [slot][nchunk][49] window-sum partials of I
@@ -163,6 +163,7 @@ void launch_cand_step(const RoiArgs& a, int max_items, hipStream_t st);
 void launch_pack(const PackArgs& a, hipStream_t st);
 int roi_pick_rc(int tw, int th);
 int roi_pitch_for(int tw);
+size_t roi_tiles_bytes(int tw, int th);
 int roi_tiles_for(int tw, int th);   // 32x32 warp tiles of a (tw+6) x (th+6) ROI
 size_t roi_corr_lds(int roi_pitch, int tw, int rc, bool global_a);
 constexpr int kMmaRows = 16;   // template rows per MFMA correlation chunk (M of v_mfma_i32_16x16x64_i8)

@@ -551,6 +551,9 @@ __host__ __device__ inline int roi_pitch_calc(int tw) {
     return q * 16;
 }
 int roi_pitch_for(int tw) { return roi_pitch_calc(tw); }
+size_t roi_tiles_bytes(int tw, int th) {   // tile-major ROI scratch of one (tw+6) x (th+6) ROI
+    return (size_t)((tw + 6 + ROI_T - 1) / ROI_T) * ((th + 6 + ROI_T - 1) / ROI_T) * ROI_T * ROI_T;
+}
 
 // LDS row pitch of the staged i8 template rows: >= tp8, pitch/16 odd (conflict-free row-strided b128 reads)
 __host__ __device__ inline int tmpl_lds_pitch(int tp8) {
@@ -634,6 +637,26 @@ __device__ __forceinline__ void stage_footprint(uint8_t* FT, int ftw, int wpr, i
         gp += B * gstep;
         lp += B * lstep;
     }
+}
+// (a') the same footprint through LDS-DMA (global_load_lds_dword): dword L of the row-major footprint (pitch wpr
+// words) comes from lane L % 64 of instruction L / 64, whose LDS destination is the wave-uniform FT + 4*64*(L/64);
+// every load of the tile is in flight at once and no VGPR holds data.  Columns past the image edge read the
+// row's pitch slack / next row (never sampled: the box already carries the +2 tap margin).
+typedef __attribute__((address_space(3))) void* fpm_lds_vp;
+typedef __attribute__((address_space(1))) void* fpm_gbl_vp;
+__device__ __forceinline__ void stage_footprint_dma(uint8_t* FT, int wpr, int fth, const uint8_t* gsrc,
+                                                    size_t gpitch, int lane) {
+    const int total = wpr * fth;
+    int r = lane / wpr, c = lane - r * wpr;
+    const int dr = 64 / wpr, dc = 64 - dr * wpr;
+    for (int i0 = 0; i0 < total; i0 += 64) {
+        if (i0 + lane < total)
+            __builtin_amdgcn_global_load_lds((fpm_gbl_vp)(gsrc + (size_t)r * gpitch + 4 * c), (fpm_lds_vp)(FT + 4 * i0), 4, 0, 0);
+        r += dr;
+        c += dc;
+        if (c >= wpr) { c -= wpr; ++r; }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 // (b) a rows x q16 block of 16-byte vectors (workgroup-wide, nthr threads): dst pitch dp, src pitch sp
 __device__ __forceinline__ void stage_block16(uint8_t* dst, int dp, const uint8_t* src, size_t sp, int rows, int q16,
@@ -748,7 +771,9 @@ __global__ __launch_bounds__(256) void k_roi_tables(RoiArgs a) {
 // together; the tile's source footprint is staged into wave-private LDS with dword loads; every lane produces
 // 4 rows x 4 pixels by gathering the bilinear taps from LDS and stores them as dwords.  Interior tiles take a
 // branch-free path; others follow remapBilinear's BORDER_CONSTANT(0) rules per pixel.  No workgroup barrier.
-template <int FB>
+// FB: footprint rows in flight per lane (0 = LDS-DMA); ABL (profiling ablations, product 0): 1 = no footprint
+// staging, 2 = no gathers (stores zeros), 3 = tables + descriptor only
+template <int FB, int ABL = 0>
 __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t ft_all[4][ROI_FT];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -784,11 +809,24 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
         const bool in_lds = (flags & kTileLds) != 0;
         const int wpr = ftw >> 2;
         wave_sync();   // previous task's gathers are done with FT
-        if ((flags & kTileAny) && in_lds) stage_footprint<FB>(FT, ftw, wpr, fth, lvl + (size_t)by0 * a.P + bxa, a.P, bxa, a.P, lane);
+        if (ABL != 1 && ABL != 3 && (flags & kTileAny) && in_lds) {
+            if constexpr (FB == 0) stage_footprint_dma(FT, wpr, fth, lvl + (size_t)by0 * a.P + bxa, a.P, lane);
+            else stage_footprint<FB>(FT, ftw, wpr, fth, lvl + (size_t)by0 * a.P + bxa, a.P, bxa, a.P, lane);
+        }
         wave_sync();
         if (c0 > cx1) continue;
+        // tile-major ROI scratch: tile (ty, tx) is a contiguous 32 x 32 block, so one store instruction of the wave
+        // (8 rows x 8 lanes x 4 bytes) writes 256 contiguous bytes
+        uint8_t* dst = a.roi + (size_t)slot * a.roi_stride + ((size_t)(ty * txn + tx) << 10) + 4 * lg - (size_t)ry0 * ROI_T;
+        if (ABL == 3) continue;
+        if (ABL == 2) {
+            for (int i = 0; i < 4; ++i) {
+                const int r = ry0 + lr + 8 * i;
+                if (r <= ry1) *(uint32_t*)(dst + (size_t)r * ROI_T) = (uint32_t)(X0r[i] ^ Y0r[i] ^ A.x ^ B.w);
+            }
+            continue;
+        }
         const int adv[4] = {A.x, A.y, A.z, A.w}, bdv[4] = {B.x, B.y, B.z, B.w};
-        uint8_t* dst = a.roi + (size_t)slot * a.roi_stride + c0;
         if ((flags & kTileInterior) && in_lds) {
             const uint8_t* base = FT - by0 * ftw - bxa;
 #pragma unroll
@@ -808,7 +846,7 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
                     if (c0 + u >= RW) v = 0;
                     pk |= (uint32_t)v << (8 * u);
                 }
-                *(uint32_t*)(dst + (size_t)r * a.roi_pitch) = pk;
+                *(uint32_t*)(dst + (size_t)r * ROI_T) = pk;
             }
             continue;
         }
@@ -847,7 +885,7 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
                 if (c0 + u >= RW) v = 0;
                 pk |= (uint32_t)v << (8 * u);
             }
-            *(uint32_t*)(dst + (size_t)r * a.roi_pitch) = pk;
+            *(uint32_t*)(dst + (size_t)r * ROI_T) = pk;
         }
     }
 }
@@ -971,7 +1009,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         if (tid < kBandSrc) { rall[tid] = 0; rallq[tid] = 0; }
         __syncthreads();
         if (MODE != 3) {   // stage: wave wv stages rows wv + 4i (kStageBatch rows' loads in flight), bytes ^ 0x80
-            const uint8_t* rsrc = a.roi + (size_t)slot * a.roi_stride + (size_t)T0 * a.roi_pitch;
+            // tile-major ROI scratch (k_roi_warp): row R, 16-byte chunk c lives in tile (R >> 5, c >> 1)
+            const uint8_t* rsrc = a.roi + (size_t)slot * a.roi_stride;
+            const int txn = (RW + ROI_T - 1) / ROI_T;
             for (int c0 = 0; c0 < q4; c0 += 64) {
                 const int c = c0 + lane;
                 for (int i0 = 0; i0 < kStageRows; i0 += kStageBatch) {
@@ -979,8 +1019,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
                     for (int i = 0; i < kStageBatch; ++i) {
                         const int r = wv + 4 * (i0 + i);
-                        v[i] = (r < nsrc && c < q4) ? *(const uint4*)(rsrc + (size_t)r * a.roi_pitch + 16 * c)
-                                                    : make_uint4(0, 0, 0, 0);
+                        const int R = T0 + r;
+                        v[i] = (r < nsrc && c < 2 * txn)
+                                   ? *(const uint4*)(rsrc + ((size_t)((R >> 5) * txn + (c >> 1)) << 10) + (R & 31) * ROI_T + 16 * (c & 1))
+                                   : make_uint4(0, 0, 0, 0);
                     }
 #pragma unroll
                     for (int i = 0; i < kStageBatch; ++i) {

@@ -85,7 +85,7 @@ int main(int argc, char** argv) {
         printf("rois %d rc %d chunks %d corr lds %zu / %zu\n", C * n3, a.rc, a.nchunk, roi_corr_lds(roi_pitch_for(TW), TW, a.rc, false), roi_corr_lds(roi_pitch_for(TW), TW, a.rc, true));
     // ---- product kernels (tables -> warp -> corr -> eval) --------------------------------------------------
     a.tabw = roi_pitch_for(TW); a.tabh = ((TH + 6) + 3) & ~3;
-    a.roi_pitch = roi_pitch_for(TW); a.roi_stride = ((size_t)a.roi_pitch * (TH + 7) + 255) & ~(size_t)255;
+    a.roi_pitch = roi_pitch_for(TW); a.roi_stride = roi_tiles_bytes(TW, TH);
     CK(hipMalloc(&a.tab, (size_t)C * n3 * 2 * (a.tabw + a.tabh) * 4));
     a.tdesc_stride = roi_tiles_for(TW, TH);
     CK(hipMalloc(&a.tdesc, (size_t)C * n3 * a.tdesc_stride * sizeof(int4)));
@@ -104,10 +104,14 @@ int main(int argc, char** argv) {
     {
         const long tiles = (long)a.slot_cap * ((TH + 6 + 31) / 32) * ((TW + 6 + 31) / 32);
         const int grid = (int)std::min<long>((tiles + 3) / 4, 16384);
+        timeit([&] { hipLaunchKernelGGL(k_roi_warp<0>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot LDS-DMA");
         timeit([&] { hipLaunchKernelGGL(k_roi_warp<1>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 1");
         timeit([&] { hipLaunchKernelGGL(k_roi_warp<2>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 2");
         timeit([&] { hipLaunchKernelGGL(k_roi_warp<4>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 4");
         timeit([&] { hipLaunchKernelGGL(k_roi_warp<8>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 8");
+        timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 1>), dim3(grid), dim3(256), 0, 0, a); }, "warp no staging");
+        timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 2>), dim3(grid), dim3(256), 0, 0, a); }, "warp no gathers");
+        timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 3>), dim3(grid), dim3(256), 0, 0, a); }, "warp tables only");
     }
     timeit([&] { launch_roi_corr(a, 0); }, "prod corr");
     timeit([&] { launch_roi_eval(a, 0); }, "prod eval");
@@ -127,10 +131,12 @@ int main(int argc, char** argv) {
         const int RW = TW + 6;
         int bad = 0;
         for (int slot : {0, 1, 131, C * n3 - 1}) {
-            std::vector<uint8_t> roi(a.roi_stride);
+            std::vector<uint8_t> roi_t(a.roi_stride);
+            const int txn = (TW + 6 + 31) / 32;
+            auto roi_at = [&](int r, int c) { return roi_t[((size_t)((r >> 5) * txn + (c >> 5)) << 10) + (r & 31) * 32 + (c & 31)]; };
             std::vector<uint32_t> rs((size_t)TH * 49), ws((size_t)a.nchunk * 49);
             std::vector<uint64_t> wq((size_t)a.nchunk * 49);
-            CK(hipMemcpy(roi.data(), a.roi + (size_t)slot * a.roi_stride, a.roi_stride, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(roi_t.data(), a.roi + (size_t)slot * a.roi_stride, a.roi_stride, hipMemcpyDeviceToHost));
             CK(hipMemcpy(rs.data(), a.rowsum + (size_t)slot * ((TH * 49 + 3) & ~3), rs.size() * 4, hipMemcpyDeviceToHost));
             CK(hipMemcpy(ws.data(), a.wsum + (size_t)slot * a.nchunk * 49, ws.size() * 4, hipMemcpyDeviceToHost));
             CK(hipMemcpy(wq.data(), a.wsq + (size_t)slot * a.nchunk * 49, wq.size() * 8, hipMemcpyDeviceToHost));
@@ -138,7 +144,7 @@ int main(int argc, char** argv) {
                 for (int dy = 0; dy < 7; ++dy)
                     for (int dx = 0; dx < 7; ++dx) {
                         uint32_t ref = 0;
-                        for (int c = 0; c < TW; ++c) ref += (uint32_t)tm[(size_t)t * TP + c] * roi[(size_t)(t + dy) * a.roi_pitch + c + dx];
+                        for (int c = 0; c < TW; ++c) ref += (uint32_t)tm[(size_t)t * TP + c] * roi_at(t + dy, c + dx);
                         if (ref != rs[(size_t)t * 49 + dy * 7 + dx]) ++bad;
                     }
             for (int ch = 0; ch < a.nchunk; ++ch)
@@ -146,7 +152,7 @@ int main(int argc, char** argv) {
                     const int dy = k / 7, dx = k % 7;
                     uint32_t s1 = 0; uint64_t s2 = 0;
                     for (int t = ch * a.rc; t < std::min(TH, (ch + 1) * a.rc); ++t)
-                        for (int c = 0; c < TW; ++c) { const uint32_t v = roi[(size_t)(t + dy) * a.roi_pitch + c + dx]; s1 += v; s2 += v * v; }
+                        for (int c = 0; c < TW; ++c) { const uint32_t v = roi_at(t + dy, c + dx); s1 += v; s2 += v * v; }
                     if (s1 != ws[(size_t)ch * 49 + k] || s2 != wq[(size_t)ch * 49 + k]) ++bad;
                 }
             (void)RW;
