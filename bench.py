@@ -3,7 +3,9 @@
 
 A step is one full TemplateMatcher::match pass (pyramid -> top-layer rotation sweep -> NCC -> peaks -> pyramid
 refinement -> host filters) over a batch of ``--batch`` synthetic Src7 sources per GPU that are already
-resident in HBM (staged before timing; the PCIe upload is not in ``value``).  ``value`` = searches/s over all
+resident in HBM (staged before timing; the PCIe upload is not in ``value``), split over ``--contexts`` contexts
+(one HIP stream each) that run as a stream of passes: a context relaunches as soon as its previous pass is
+finished, so host post-processing overlaps device work.  ``value`` = searches/s over all
 ranks.  Multi-GPU: one process per GPU (torchrun), every rank searches its own sources (weak scaling, no
 data-path collective); barrier + synchronize bracket the K timed steps and the max time over ranks is used.
 
@@ -150,19 +152,23 @@ def main():
     views = [c.match_staged_array() for c in ctxs]
     assert [len(r) for r in ref] == [int(x) for cnt, _ in views for x in cnt]
 
-    def step():
+    def run(k_steps):
+        # K passes per context as a stream: each context relaunches its next pass as soon as it has finished (host
+        # post-processing) the previous one, so the device never waits for the host between steps
         for c in ctxs:
             c.match_staged_launch()
-        return [c.match_staged_finish_array() for c in ctxs]
+        for k in range(k_steps):
+            for c in ctxs:
+                c.match_staged_finish_array()
+                if k + 1 < k_steps:
+                    c.match_staged_launch()
 
-    for _ in range(args.warmup):
-        step()
+    run(args.warmup)
     log(f"[rank {rank}] warm; timing {args.steps} steps x {args.batch} sources over {G} context(s)")
 
     barrier_sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()   # device passes + host finish (C++); results as array views
+    run(args.steps)   # K complete device passes + host finishes (C++) per context
     barrier_sync()
     elapsed = time.perf_counter() - t0
     res = ref

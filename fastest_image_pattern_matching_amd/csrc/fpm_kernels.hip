@@ -773,7 +773,40 @@ __global__ __launch_bounds__(256) void k_roi_tables(RoiArgs a) {
 // branch-free path; others follow remapBilinear's BORDER_CONSTANT(0) rules per pixel.  No workgroup barrier.
 // FB: footprint rows in flight per lane (0 = LDS-DMA); ABL (profiling ablations, product 0): 1 = no footprint
 // staging, 2 = no gathers (stores zeros), 3 = tables + descriptor only
-template <int FB, int ABL = 0>
+// Per-task inputs of k_roi_warp (descriptor, the lane's table entries, the source level), loaded one task ahead.
+struct WarpTask {
+    int4 dsc, A, B;
+    int X0r[4], Y0r[4];
+    const uint8_t* lvl;
+};
+__device__ __forceinline__ void warp_task_load(const RoiArgs& a, int task, int tasks, int per_roi, int txn, int RW,
+                                               int RH, int lr, int lg, WarpTask& w) {
+    if (task >= tasks) return;
+    const int slot = task / per_roi;
+    const int rem = task - slot * per_roi;
+    const int ty = rem / txn, tx = rem - ty * txn;
+    w.dsc = a.tdesc[(size_t)slot * a.tdesc_stride + rem];
+    const int32_t* t = a.tab + (size_t)slot * 2 * (a.tabw + a.tabh);
+    const int cx0 = tx * ROI_T, cx1 = min(cx0 + ROI_T, RW) - 1;
+    const int ry0 = ty * ROI_T, ry1 = min(ry0 + ROI_T, RH) - 1;
+    const int cc = min(cx0 + 4 * lg, cx1 & ~3);   // tables are read in bounds even for idle lanes
+    w.A = *(const int4*)(t + cc);
+    w.B = *(const int4*)(t + a.tabw + cc);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = min(ry0 + lr + 8 * i, ry1);
+        w.X0r[i] = t[2 * a.tabw + r];
+        w.Y0r[i] = t[2 * a.tabw + a.tabh + r];
+    }
+    int id, jj;
+    roi_slot(a, slot, id, jj);
+    w.lvl = a.level + (size_t)(id / a.per_source) * a.level_stride;
+}
+
+// FB: footprint rows in flight per lane (0 = LDS-DMA); ABL (profiling ablations, product 0): 1 = no footprint
+// staging, 2 = no gathers (stores zeros), 3 = tables + descriptor only; PF: load the next task's inputs during
+// the current task's gathers
+template <int FB, int ABL = 0, bool PF = false>
 __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t ft_all[4][ROI_FT];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -783,28 +816,28 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
     const int per_roi = txn * tyn;
     const int tasks = roi_count(a) * per_roi;
     const int lr = lane >> 3, lg = lane & 7;   // lane -> rows lr + 8i, columns 4*lg .. 4*lg+3
-    for (int task = blockIdx.x * 4 + wv; task < tasks; task += gridDim.x * 4) {
+    const int tstride = gridDim.x * 4;
+    WarpTask nxt;
+    if (PF) warp_task_load(a, blockIdx.x * 4 + wv, tasks, per_roi, txn, RW, RH, lr, lg, nxt);
+    for (int task = blockIdx.x * 4 + wv; task < tasks; task += tstride) {
         const int slot = task / per_roi;
         const int rem = task - slot * per_roi;
         const int ty = rem / txn, tx = rem - ty * txn;
-        const int4 dsc = a.tdesc[(size_t)slot * a.tdesc_stride + rem];
-        const int32_t* t = a.tab + (size_t)slot * 2 * (a.tabw + a.tabh);
         const int cx0 = tx * ROI_T, cx1 = min(cx0 + ROI_T, RW) - 1;
         const int ry0 = ty * ROI_T, ry1 = min(ry0 + ROI_T, RH) - 1;
         const int c0 = cx0 + 4 * lg;
-        const int cc = min(c0, cx1 & ~3);   // tables are read in bounds even for idle lanes
-        const int4 A = *(const int4*)(t + cc);
-        const int4 B = *(const int4*)(t + a.tabw + cc);
-        int X0r[4], Y0r[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int r = min(ry0 + lr + 8 * i, ry1);
-            X0r[i] = t[2 * a.tabw + r];
-            Y0r[i] = t[2 * a.tabw + a.tabh + r];
+        WarpTask cur;
+        if (PF) {
+            cur = nxt;
+            warp_task_load(a, task + tstride, tasks, per_roi, txn, RW, RH, lr, lg, nxt);
+            asm volatile("" ::: "memory");   // keep the prefetch here, ahead of this task's work
+        } else {
+            warp_task_load(a, task, tasks, per_roi, txn, RW, RH, lr, lg, cur);
         }
-        int id, jj;
-        roi_slot(a, slot, id, jj);
-        const uint8_t* lvl = a.level + (size_t)(id / a.per_source) * a.level_stride;
+        const int4 dsc = cur.dsc, A = cur.A, B = cur.B;
+        const int* X0r = cur.X0r;
+        const int* Y0r = cur.Y0r;
+        const uint8_t* lvl = cur.lvl;
         const int bxa = dsc.x, by0 = dsc.y, ftw = dsc.z & 0xffff, fth = dsc.z >> 16, flags = dsc.w;
         const bool in_lds = (flags & kTileLds) != 0;
         const int wpr = ftw >> 2;

@@ -109,6 +109,8 @@ int main(int argc, char** argv) {
         timeit([&] { hipLaunchKernelGGL(k_roi_warp<2>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 2");
         timeit([&] { hipLaunchKernelGGL(k_roi_warp<4>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 4");
         timeit([&] { hipLaunchKernelGGL(k_roi_warp<8>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 8");
+        timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 0, true>), dim3(grid), dim3(256), 0, 0, a); }, "warp prefetch b2");
+        timeit([&] { hipLaunchKernelGGL((k_roi_warp<1, 0, true>), dim3(grid), dim3(256), 0, 0, a); }, "warp prefetch b1");
         timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 1>), dim3(grid), dim3(256), 0, 0, a); }, "warp no staging");
         timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 2>), dim3(grid), dim3(256), 0, 0, a); }, "warp no gathers");
         timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 3>), dim3(grid), dim3(256), 0, 0, a); }, "warp tables only");
