@@ -1528,10 +1528,12 @@ __global__ __launch_bounds__(256) void k_cand_step(RoiArgs a) {
 // :329-366: best of the n3 angles, early break below vecLayerScore, back-mapping of ptLT, append to the next live
 // list.  Each wave streams its [th][49] series through wave-private LDS in blocks of kEvalRows rows, the next
 // block's loads in flight while 49 lanes fold the current one in row order.  No workgroup barrier in the loop.
-constexpr int kEvalRows = 64;
-constexpr int kEvalVec = (kEvalRows * 49 / 4 + 63) / 64;   // uint4 per lane per block
+constexpr int kEvalRows = 48;
+constexpr int kEvalDma = (kEvalRows * 49 / 4 + 63) / 64;   // 16-byte LDS-DMA loads per lane per block
+constexpr int kEvalBuf = kEvalDma * 1024;                    // bytes per block buffer
+static_assert(kEvalDma == 10, "the counted s_waitcnt vmcnt(10) in eval_roi assumes 10 loads per block");
 
-__device__ void eval_roi(const RoiArgs& a, int slot, int lane, uint32_t* blk, float* sc, RoiRecord* out,
+__device__ void eval_roi(const RoiArgs& a, int slot, int lane, uint8_t* blk, float* sc, RoiRecord* out,
                          RoiRecord* keep) {
     const int th = a.th;
     if (a.equal1) {   // CCOEFF_Denominator: matResult = 1 everywhere (:529-533)
@@ -1561,26 +1563,35 @@ __device__ void eval_roi(const RoiArgs& a, int slot, int lane, uint32_t* blk, fl
         }
         for (; c < a.nchunk; ++c) { s1 += ws[(size_t)c * 49]; s2 += wq[(size_t)c * 49]; }
     }
+    // the series streams through two wave-private LDS buffers by LDS-DMA: block b + 1 (exactly kEvalDma
+    // 16-byte loads per lane, padded with dummy loads so a counted vmcnt is exact) is in flight while block b folds
     constexpr int BQ = kEvalRows * 49 / 4;   // uint4 per block
     const int nblk = (th + kEvalRows - 1) / kEvalRows;
-    uint4 v[kEvalVec];
-    auto load_block = [&](int b) {
+    auto issue_block = [&](int b, uint8_t* buf) {
 #pragma unroll
-        for (int i = 0; i < kEvalVec; ++i) {
-            const size_t q = (size_t)b * BQ + lane + 64 * i;
-            v[i] = (lane + 64 * i < BQ && q < total4) ? rs[q] : make_uint4(0, 0, 0, 0);
+        for (int i = 0; i < kEvalDma; ++i) {
+            size_t q = (size_t)b * BQ + 64 * i + lane;
+            if (64 * i + lane >= BQ || q >= total4) q = 0;   // dummy: lands past the rows that are read
+            // inline asm: the compiler does not track this LDS-DMA, so it inserts no vmcnt(0) before the fold's
+            // LDS reads; the counted waits below order them (the guide's documented recipe)
+            uint32_t keep;
+            const uint32_t ldsa = (uint32_t)(uintptr_t)(fpm_lds_vp)(buf + 1024 * i);
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                         : "=&s"(keep) : "v"(rs + q), "s"(__builtin_amdgcn_readfirstlane(ldsa)) : "memory");
         }
     };
     float accF = 0.f;
     uint64_t accI = 0;
-    load_block(0);
+    issue_block(0, blk);
     for (int b = 0; b < nblk; ++b) {
-        wave_sync();   // previous block folded
-#pragma unroll
-        for (int i = 0; i < kEvalVec; ++i)
-            if (lane + 64 * i < BQ) ((uint4*)blk)[lane + 64 * i] = v[i];
+        const uint32_t* cb = (const uint32_t*)(blk + (b & 1) * kEvalBuf);
+        if (b + 1 < nblk) {
+            issue_block(b + 1, blk + ((b + 1) & 1) * kEvalBuf);
+            asm volatile("s_waitcnt vmcnt(10)" ::: "memory");   // kEvalDma loads of block b + 1 may stay in flight
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         wave_sync();
-        if (b + 1 < nblk) load_block(b + 1);
         const int rows = min(kEvalRows, th - b * kEvalRows);
         if (lane < 49) {
             if (a.fold) {
@@ -1588,15 +1599,16 @@ __device__ void eval_roi(const RoiArgs& a, int slot, int lane, uint32_t* blk, fl
                 for (; t + 8 <= rows; t += 8) {   // 8 LDS reads in flight, adds in row order (:507)
                     uint32_t x[8];
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) x[u] = blk[(t + u) * 49 + lane];
+                    for (int u = 0; u < 8; ++u) x[u] = cb[(t + u) * 49 + lane];
 #pragma unroll
                     for (int u = 0; u < 8; ++u) accF = accF + (float)(int)x[u];
                 }
-                for (; t < rows; ++t) accF = accF + (float)(int)blk[t * 49 + lane];
+                for (; t < rows; ++t) accF = accF + (float)(int)cb[t * 49 + lane];
             } else {
-                for (int t = 0; t < rows; ++t) accI += blk[t * 49 + lane];
+                for (int t = 0; t < rows; ++t) accI += cb[t * 49 + lane];
             }
         }
+        wave_sync();   // block b folded before its buffer is refilled with block b + 2
     }
     if (lane < 49) {
         const double num = a.fold ? (double)accF : (double)(float)(double)accI;
@@ -1623,7 +1635,7 @@ __device__ void eval_roi(const RoiArgs& a, int slot, int lane, uint32_t* blk, fl
 }
 
 __global__ __launch_bounds__(192) void k_roi_eval(RoiArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t blk_all[3][kEvalRows * 49];
+    __shared__ __attribute__((aligned(16))) uint8_t blk_all[3][2 * kEvalBuf];
     __shared__ float sc_all[3][64];
     __shared__ RoiRecord recs[3];
     const int lane = threadIdx.x & 63, j = threadIdx.x >> 6;   // wave j <-> refinement angle j
