@@ -67,23 +67,62 @@ def make_sources(templ, n, seed0):
     return [synth.src7_scene(templ, seed=seed0 + i)[0] for i in range(n)]
 
 
-def cpu_baseline(templ, src, budget_s):
-    """Oracle (CPU port of the reference, SSE2 IM_Conv, 1 thread) on repeated searches of one Src7 source."""
+def _time_oracle(templ, src, budget_s, lib_path=None, threads=1):
+    """Searches/s of the oracle on repeated searches of one source: `threads` OracleMatcher objects searching
+    concurrently (ctypes releases the GIL around each C call), each until the budget is spent."""
+    import threading
+
     from tests import oracle
 
-    o = oracle.OracleMatcher().set(**PARAMS)
-    o.learnPattern(templ)
-    o.match(src)                       # warm
-    n, t0 = 0, time.perf_counter()
-    while True:
-        o.match(src)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or n >= 200:
-            break
-    return {"value": n / el, "unit": "searches/s", "cores": 1, "kind": "port",
+    path = lib_path or oracle.ORACLE_LIB
+    ms = [oracle.OracleMatcher(path).set(**PARAMS) for _ in range(threads)]
+    counts = [0] * threads
+    start = threading.Barrier(threads + 1)
+
+    def work(i):
+        ms[i].learnPattern(templ)
+        ms[i].match(src)               # warm, outside the timed region
+        start.wait()
+        t0 = time.perf_counter()
+        while True:
+            ms[i].match(src)
+            counts[i] += 1
+            if time.perf_counter() - t0 >= budget_s or counts[i] >= 200:
+                break
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for t in th:
+        t.start()
+    start.wait()
+    t0 = time.perf_counter()
+    for t in th:
+        t.join()
+    el = time.perf_counter() - t0
+    return sum(counts), el
+
+
+def cpu_baseline(templ, src, budget_s):
+    """Oracle (CPU port of the reference, SSE2 IM_Conv) on repeated searches of one Src7 source: the headline is
+    one thread with the parity build's flags (the reference is single-threaded: its OpenMP code is dead); the
+    variants are the reference's release flags (-ffast-math, CMakeLists.txt:67) on one thread and the parity
+    build on every core this process may use (independent searches in parallel, capped at the GPU box's
+    16-core share)."""
+    from tests import oracle
+
+    n, el = _time_oracle(templ, src, 0.5 * budget_s)
+    base = {"value": n / el, "unit": "searches/s", "cores": 1, "kind": "port",
             "sample": f"{n} sequential searches of one Src7 surrogate source ({el:.1f} s), oracle/fpm_oracle.cpp "
                       f"-O3 SSE2, single thread (the reference's OpenMP code is dead)"}
+    variants = []
+    if os.path.exists(oracle.ORACLE_LIB_FAST):
+        n, el = _time_oracle(templ, src, 0.25 * budget_s, oracle.ORACLE_LIB_FAST)
+        variants.append({"value": n / el, "unit": "searches/s", "cores": 1, "flags": "-O3 -ffast-math -msse2",
+                         "sample": f"{n} sequential searches ({el:.1f} s)"})
+    ncores = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    n, el = _time_oracle(templ, src, 0.25 * budget_s, threads=ncores)
+    variants.append({"value": n / el, "unit": "searches/s", "cores": ncores, "flags": "-O3 -msse2 (parity build)",
+                     "sample": f"{n} searches on {ncores} threads, one oracle object each ({el:.1f} s)"})
+    return base, variants
 
 
 def main():
@@ -245,8 +284,8 @@ def main():
         "roofline": roofline,
     }
     if world == 1 and rank == 0 and args.cpu_budget > 0:
-        log("[rank 0] CPU baseline (oracle restatement, 1 thread)")
-        out["cpu_baseline"] = cpu_baseline(templ, sources[0], args.cpu_budget)
+        log("[rank 0] CPU baseline (oracle restatement: 1 thread, fast-math 1 thread, all cores)")
+        out["cpu_baseline"], out["cpu_baseline_variants"] = cpu_baseline(templ, sources[0], args.cpu_budget)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:

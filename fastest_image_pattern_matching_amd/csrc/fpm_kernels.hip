@@ -595,6 +595,42 @@ __device__ __forceinline__ int roi_tap(const uint8_t* __restrict__ src, int sw, 
     return (32 * h0 + fy * (h1 - h0) + 512) >> 10;
 }
 
+// a * b + c on the 24-bit multiplier (|a|, |b| < 2^23): written out because the compiler otherwise re-associates
+// such footprint offsets into the quarter-rate v_mad_u64_u32
+__device__ __forceinline__ int mad24(int a, int b, int c) {
+    int d;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
+// interior bilinear tap from an LDS footprint FT (16-byte aligned; tap (sx, sy) at byte offset off, row pitch
+// ftw): per tap row one aligned dword pair (ds_read2_b32) funnel-shifted to the tap's byte (v_alignbyte uses the
+// offset's low two bits; unaligned 32-bit DS reads measured 2.5x slower than byte gathers), the horizontal passes
+// as u8 dot products with the per-axis weights (32 - fx, fx, 0, 0), the vertical pass as 24-bit multiply-adds:
+// the same integer as roi_tap's (32*h0 + fy*(h1 - h0) + 512) >> 10.  The footprint buffers carry >= 4 bytes of
+// slack after their last row (the pair's second dword).
+__device__ __forceinline__ int ft_tap_interior(const uint8_t* FT, int off, int ftw, int X, int Y) {
+    const uint32_t fx = X & (kInterTab - 1), fy = Y & (kInterTab - 1);
+    const uint32_t* F = (const uint32_t*)FT;
+    const int off1 = off + ftw;
+    const uint32_t* q0 = F + (off >> 2);
+    const uint32_t* q1 = F + (off1 >> 2);
+    const uint32_t r0 = __builtin_amdgcn_alignbyte(q0[1], q0[0], (uint32_t)off);
+    const uint32_t r1 = __builtin_amdgcn_alignbyte(q1[1], q1[0], (uint32_t)off1);
+    const uint32_t wx = 32u + fx * 255u;
+    const uint32_t h0 = __builtin_amdgcn_udot4(r0, wx, 0u, false), h1 = __builtin_amdgcn_udot4(r1, wx, 0u, false);
+    return (int)((__umul24(32u - fy, h0) + __umul24(fy, h1) + 512u) >> 10);
+}
+
+// the same tap by four byte gathers (p = tap (sx, sy))
+__device__ __forceinline__ int ft_tap_bytes(const uint8_t* FT, int off, int ftw, int X, int Y) {
+    const int fx = X & (kInterTab - 1), fy = Y & (kInterTab - 1);
+    const uint8_t* p = FT + off;
+    const int v0 = p[0], v1 = p[1], v2 = p[ftw], v3 = p[ftw + 1];
+    const int h0 = 32 * v0 + __mul24(fx, v1 - v0), h1 = 32 * v2 + __mul24(fx, v3 - v2);
+    return (32 * h0 + __mul24(fy, h1 - h0) + 512) >> 10;
+}
+
 __device__ __forceinline__ void roi_slot(const RoiArgs& a, int slot, int& id, int& jj) {
     const int ri = a.slot_base + slot;
     const int li = ri / a.n3;
@@ -770,9 +806,8 @@ __global__ __launch_bounds__(256) void k_roi_tables(RoiArgs a) {
 // ---- K6b: ROI sampling.  One wave = one 32x32 ROI tile: its descriptor and the lane's table entries are loaded
 // together; the tile's source footprint is staged into wave-private LDS with dword loads; every lane produces
 // 4 rows x 4 pixels by gathering the bilinear taps from LDS and stores them as dwords.  Interior tiles take a
-// branch-free path; others follow remapBilinear's BORDER_CONSTANT(0) rules per pixel.  No workgroup barrier.
-// FB: footprint rows in flight per lane (0 = LDS-DMA); ABL (profiling ablations, product 0): 1 = no footprint
-// staging, 2 = no gathers (stores zeros), 3 = tables + descriptor only
+// branch-free path (ft_tap_interior); others follow remapBilinear's BORDER_CONSTANT(0) rules per pixel.  No
+// workgroup barrier.
 // Per-task inputs of k_roi_warp (descriptor, the lane's table entries, the source level), loaded one task ahead.
 struct WarpTask {
     int4 dsc, A, B;
@@ -804,13 +839,13 @@ __device__ __forceinline__ void warp_task_load(const RoiArgs& a, int task, int t
 }
 
 // FB: footprint rows in flight per lane (0 = LDS-DMA); ABL (profiling ablations, product 0): 1 = no footprint
-// staging, 2 = no gathers (stores zeros), 3 = tables + descriptor only; PF: load the next task's inputs during
+// staging, 2 = no gathers (stores zeros), 3 = tables + descriptor only, 4 = dot-product interior taps (ft_tap_interior); PF: load the next task's inputs during
 // the current task's gathers
 template <int FB, int ABL = 0, bool PF = false>
 __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t ft_all[4][ROI_FT];
+    __shared__ __attribute__((aligned(16))) uint8_t ft_all[4 * ROI_FT + 16];   // + slack for ft_tap_interior
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint8_t* FT = ft_all[wv];
+    uint8_t* FT = ft_all + wv * ROI_FT;
     const int RW = a.tw + 6, RH = a.th + 6, W = a.W, H = a.H;
     const int txn = (RW + ROI_T - 1) / ROI_T, tyn = (RH + ROI_T - 1) / ROI_T;
     const int per_roi = txn * tyn;
@@ -861,7 +896,10 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
         }
         const int adv[4] = {A.x, A.y, A.z, A.w}, bdv[4] = {B.x, B.y, B.z, B.w};
         if ((flags & kTileInterior) && in_lds) {
-            const uint8_t* base = FT - by0 * ftw - bxa;
+            const int obase = by0 * ftw + bxa;
+            // columns past the ROI's right edge are zero: one byte mask per lane instead of a select per pixel
+            const int nvalid = RW - c0;
+            const uint32_t colmask = nvalid >= 4 ? 0xffffffffu : (1u << (8 * nvalid)) - 1u;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int r = ry0 + lr + 8 * i;
@@ -871,15 +909,11 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
                 for (int u = 0; u < 4; ++u) {
                     const int X = (X0r[i] + adv[u]) >> (kAbBits - kInterBits);
                     const int Y = (Y0r[i] + bdv[u]) >> (kAbBits - kInterBits);
-                    const int fx = X & (kInterTab - 1), fy = Y & (kInterTab - 1);
-                    const uint8_t* p = base + __mul24(Y >> kInterBits, ftw) + (X >> kInterBits);
-                    const int v0 = p[0], v1 = p[1], v2 = p[ftw], v3 = p[ftw + 1];
-                    const int h0 = 32 * v0 + __mul24(fx, v1 - v0), h1 = 32 * v2 + __mul24(fx, v3 - v2);
-                    int v = (32 * h0 + __mul24(fy, h1 - h0) + 512) >> 10;
-                    if (c0 + u >= RW) v = 0;
+                    const int off = mad24(Y >> kInterBits, ftw, (X >> kInterBits) - obase);
+                    const int v = ABL == 4 ? ft_tap_interior(FT, off, ftw, X, Y) : ft_tap_bytes(FT, off, ftw, X, Y);
                     pk |= (uint32_t)v << (8 * u);
                 }
-                *(uint32_t*)(dst + (size_t)r * ROI_T) = pk;
+                *(uint32_t*)(dst + (size_t)r * ROI_T) = pk & colmask;
             }
             continue;
         }
@@ -1203,7 +1237,8 @@ bool roi_small_fits(int tw, int th) { return small_layout(tw, th).total <= kSmal
 size_t roi_small_lds(int tw, int th) { return (size_t)small_layout(tw, th).total; }
 
 // MODE (profiling ablations in scripts/roi_microbench.hip; the product uses 0): 1 = tables + sampling only,
-// 2 = + row / window sums, 3 = + bands without the fold, 9 = full with per-phase s_memtime stamps (a.stamps)
+// 2 = + row / window sums, 3 = + bands without the fold, 5 = full with byte-gather taps, 9 = full with per-phase
+// s_memtime stamps (a.stamps)
 template <int MODE>
 __global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1273,11 +1308,13 @@ __global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
         const int gbxa = gbx0 & ~3;
         const int gftw = g_any ? ((gbx1 - gbxa + 4) & ~3) + 4 : 4;   // +4: odd-ish pitch vs banks
         const int gfth = g_any ? gby1 - gby0 + 1 : 0;
+        const int gobase = gby0 * gftw + gbxa;
         if (g_any && gftw * gfth <= LY.tab - LY.u) {   // wave-uniform (same values in every thread)
             uint8_t* FT = FTall;
             const int wpr = gftw >> 2;
             stage_block4(FT, gftw, lvl + (size_t)gby0 * a.P + gbxa, a.P, gfth, wpr, gbxa, a.P, tid, 256);
             __syncthreads();
+            STAMP(8);
             const int ngrp = (RW + 3) >> 2;
             for (int i = tid; i < RH * ngrp; i += 256) {   // thread -> (row, 4 columns)
                 const int r = i / ngrp, c0 = 4 * (i - r * ngrp);
@@ -1289,11 +1326,8 @@ __global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
                     const int Y = (Y0 + lbd[c0 + u]) >> (kAbBits - kInterBits);
                     int v;
                     if (g_interior) {
-                        const int fx = X & (kInterTab - 1), fy = Y & (kInterTab - 1);
-                        const uint8_t* p = FT + __mul24((Y >> kInterBits) - gby0, gftw) + ((X >> kInterBits) - gbxa);
-                        const int v0 = p[0], v1 = p[1], v2 = p[gftw], v3 = p[gftw + 1];
-                        const int h0 = 32 * v0 + __mul24(fx, v1 - v0), h1 = 32 * v2 + __mul24(fx, v3 - v2);
-                        v = (32 * h0 + __mul24(fy, h1 - h0) + 512) >> 10;
+                        const int off = mad24(Y >> kInterBits, gftw, (X >> kInterBits) - gobase);
+                        v = MODE == 5 ? ft_tap_bytes(FT, off, gftw, X, Y) : ft_tap_interior(FT, off, gftw, X, Y);
                     } else {
                         v = ft_tap_general(FT, gftw, gbxa, gby0, W, H, X, Y);
                     }
@@ -1302,6 +1336,7 @@ __global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
                 }
                 *(uint32_t*)(SB + r * SBp + c0) = pk;
             }
+            STAMP(9);
         } else if (!g_any) {   // the ROI lies entirely outside the image: all zero (BORDER_CONSTANT 0)
             for (int i = tid; i < RH * (SBp >> 2); i += 256) ((uint32_t*)SB)[i] = 0u;
         } else {   // footprint too large: one 32x32 tile per wave at a time
@@ -1345,11 +1380,8 @@ __global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
                         const int Y = (Y0 + lbd[c0 + u]) >> (kAbBits - kInterBits);
                         int v;
                         if (interior && in_lds) {
-                            const int fx = X & (kInterTab - 1), fy = Y & (kInterTab - 1);
-                            const uint8_t* p = FT + __mul24((Y >> kInterBits) - by0, ftw) + ((X >> kInterBits) - bxa);
-                            const int v0 = p[0], v1 = p[1], v2 = p[ftw], v3 = p[ftw + 1];
-                            const int h0 = 32 * v0 + __mul24(fx, v1 - v0), h1 = 32 * v2 + __mul24(fx, v3 - v2);
-                            v = (32 * h0 + __mul24(fy, h1 - h0) + 512) >> 10;
+                            const int off = mad24(Y >> kInterBits, ftw, (X >> kInterBits) - (by0 * ftw + bxa));
+                            v = MODE == 5 ? ft_tap_bytes(FT, off, ftw, X, Y) : ft_tap_interior(FT, off, ftw, X, Y);
                         } else {
                             v = in_lds ? ft_tap_general(FT, ftw, bxa, by0, W, H, X, Y) : roi_tap(lvl, W, H, a.P, X, Y);
                         }

@@ -113,6 +113,7 @@ int main(int argc, char** argv) {
         timeit([&] { hipLaunchKernelGGL((k_roi_warp<1, 0, true>), dim3(grid), dim3(256), 0, 0, a); }, "warp prefetch b1");
         timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 1>), dim3(grid), dim3(256), 0, 0, a); }, "warp no staging");
         timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 2>), dim3(grid), dim3(256), 0, 0, a); }, "warp no gathers");
+        timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 4>), dim3(grid), dim3(256), 0, 0, a); }, "warp dot4 taps");
         timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 3>), dim3(grid), dim3(256), 0, 0, a); }, "warp tables only");
     }
     timeit([&] { launch_roi_corr(a, 0); }, "prod corr");
@@ -198,6 +199,7 @@ int main(int argc, char** argv) {
         timeit([&] { hipLaunchKernelGGL(k_roi_small<2>, dim3(7872), dim3(256), lds, 0, b); }, "small +sums");
         timeit([&] { hipLaunchKernelGGL(k_roi_small<3>, dim3(7872), dim3(256), lds, 0, b); }, "small +bands nofold");
         timeit([&] { hipLaunchKernelGGL(k_roi_small<0>, dim3(C3 * n3), dim3(256), lds, 0, b); }, "small exact grid");
+        timeit([&] { hipLaunchKernelGGL(k_roi_small<5>, dim3(C3 * n3), dim3(256), lds, 0, b); }, "small byte-gather taps");
         {   // per-phase s_memtime stamps of the first 64 workgroups
             uint64_t* d_stamps;
             CK(hipMalloc(&d_stamps, 64 * 16 * 8));
@@ -214,6 +216,17 @@ int main(int argc, char** argv) {
             printf("small L3 phases (cycles, mean of 64 WGs):");
             for (int k = 0; k < 7; ++k) printf(" %s %.0f", names[k], acc[k] / 64);
             printf("\n");
+            double st = 0, ga = 0, tail = 0;
+            int ng = 0;
+            for (int w = 0; w < 64; ++w)
+                if (hs[w * 16 + 8] && hs[w * 16 + 9]) {   // whole-footprint path: staging / gathers / barrier tail
+                    st += (double)(hs[w * 16 + 8] - hs[w * 16 + 1]);
+                    ga += (double)(hs[w * 16 + 9] - hs[w * 16 + 8]);
+                    tail += (double)(hs[w * 16 + 2] - hs[w * 16 + 9]);
+                    ++ng;
+                }
+            if (ng) printf("  sampling split over %d whole-footprint WGs: stage %.0f gathers %.0f barrier %.0f\n", ng,
+                           st / ng, ga / ng, tail / ng);
             b.stamps = nullptr;
         }
     }

@@ -16,17 +16,18 @@ from fastest_image_pattern_matching_amd._lib import Params, Result
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(REPO, "oracle")
 ORACLE_LIB = os.path.join(ORACLE_DIR, "build", "liboracle_fpm.so")
+# -ffast-math build of the same source: bench.py's CPU timing variant only, never a parity checker
+ORACLE_LIB_FAST = os.path.join(ORACLE_DIR, "build", "liboracle_fpm_fast.so")
 _U8P = C.POINTER(C.c_uint8)
-_lib = None
+_libs = {}
 
 
-def load():
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(ORACLE_LIB):
+def load(path: str = ORACLE_LIB):
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
         subprocess.check_call(["make", "-C", ORACLE_DIR])
-    lib = C.CDLL(ORACLE_LIB)
+    lib = C.CDLL(path)
     lib.orc_create.restype = C.c_void_p
     lib.orc_destroy.argtypes = [C.c_void_p]
     lib.orc_set_params.argtypes = [C.c_void_p, C.POINTER(Params)]
@@ -49,7 +50,7 @@ def load():
     lib.orc_rotrect_overlap.argtypes = [C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_double),
                                         C.POINTER(C.c_int)]
     lib.fpm_params_default.argtypes = [C.POINTER(Params)]
-    _lib = lib
+    _libs[path] = lib
     return lib
 
 
@@ -93,8 +94,8 @@ def rotrect_overlap(a, b):
 class OracleMatcher:
     """Same surface as fastest_image_pattern_matching_amd.TemplateMatcher (setters, learnPattern, match)."""
 
-    def __init__(self):
-        self._lib = load()
+    def __init__(self, lib_path: str = ORACLE_LIB):
+        self._lib = load(lib_path)
         self._h = C.c_void_p(self._lib.orc_create())
         self._p = Params()
         self._lib.fpm_params_default(C.byref(self._p))
