@@ -631,6 +631,28 @@ __device__ __forceinline__ int ft_tap_bytes(const uint8_t* FT, int off, int ftw,
     return (32 * h0 + __mul24(fy, h1 - h0) + 512) >> 10;
 }
 
+// One bilinear ROI pixel from a staged footprint, BORDER_CONSTANT(0) rules of remapBilinear (general path).
+__device__ __forceinline__ int ft_tap_general(const uint8_t* FT, int ftw, int bxa, int by0, int W, int H, int X, int Y) {
+    const int sx = sat_s16(X >> kInterBits), sy = sat_s16(Y >> kInterBits);
+    const int fx = X & (kInterTab - 1), fy = Y & (kInterTab - 1);
+    const uint8_t* p = FT + (sy - by0) * ftw + (sx - bxa);
+    int v0, v1, v2, v3;
+    if ((unsigned)sx < (unsigned)(W - 1) && (unsigned)sy < (unsigned)(H - 1)) {
+        v0 = p[0]; v1 = p[1]; v2 = p[ftw]; v3 = p[ftw + 1];
+    } else if (sx >= W || sx + 1 < 0 || sy >= H || sy + 1 < 0) {
+        return 0;
+    } else {
+        const bool x0 = sx >= 0 && sx < W, x1 = sx + 1 >= 0 && sx + 1 < W;
+        const bool y0 = sy >= 0 && sy < H, y1 = sy + 1 >= 0 && sy + 1 < H;
+        v0 = x0 && y0 ? p[0] : 0;
+        v1 = x1 && y0 ? p[1] : 0;
+        v2 = x0 && y1 ? p[ftw] : 0;
+        v3 = x1 && y1 ? p[ftw + 1] : 0;
+    }
+    const int h0 = 32 * v0 + fx * (v1 - v0), h1 = 32 * v2 + fx * (v3 - v2);
+    return (32 * h0 + fy * (h1 - h0) + 512) >> 10;
+}
+
 __device__ __forceinline__ void roi_slot(const RoiArgs& a, int slot, int& id, int& jj) {
     const int ri = a.slot_base + slot;
     const int li = ri / a.n3;
@@ -839,7 +861,8 @@ __device__ __forceinline__ void warp_task_load(const RoiArgs& a, int task, int t
 }
 
 // FB: footprint rows in flight per lane (0 = LDS-DMA); ABL (profiling ablations, product 0): 1 = no footprint
-// staging, 2 = no gathers (stores zeros), 3 = tables + descriptor only, 4 = dot-product interior taps (ft_tap_interior); PF: load the next task's inputs during
+// staging, 2 = no gathers (stores zeros), 3 = tables + descriptor only, 4 = dot-product interior taps
+// (ft_tap_interior), 9 = per-wave phase cycles into a.stamps (task loads / footprint staging / gathers + stores); PF: load the next task's inputs during
 // the current task's gathers
 template <int FB, int ABL = 0, bool PF = false>
 __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
@@ -853,8 +876,16 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
     const int lr = lane >> 3, lg = lane & 7;   // lane -> rows lr + 8i, columns 4*lg .. 4*lg+3
     const int tstride = gridDim.x * 4;
     WarpTask nxt;
+    uint64_t st_acc[3] = {0, 0, 0}, st_t = 0;   // ABL 9: per-wave cycles in task loads / staging / gathers
+    int st_n = 0;
     if (PF) warp_task_load(a, blockIdx.x * 4 + wv, tasks, per_roi, txn, RW, RH, lr, lg, nxt);
     for (int task = blockIdx.x * 4 + wv; task < tasks; task += tstride) {
+        if (ABL == 9) {   // the previous task's gathers + stores end here
+            const uint64_t t = __builtin_readcyclecounter();
+            if (st_n > 0) st_acc[2] += t - st_t;
+            st_t = t;
+            ++st_n;
+        }
         const int slot = task / per_roi;
         const int rem = task - slot * per_roi;
         const int ty = rem / txn, tx = rem - ty * txn;
@@ -876,12 +907,23 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
         const int bxa = dsc.x, by0 = dsc.y, ftw = dsc.z & 0xffff, fth = dsc.z >> 16, flags = dsc.w;
         const bool in_lds = (flags & kTileLds) != 0;
         const int wpr = ftw >> 2;
+        if (ABL == 9) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint64_t t = __builtin_readcyclecounter();
+            st_acc[0] += t - st_t;
+            st_t = t;
+        }
         wave_sync();   // previous task's gathers are done with FT
         if (ABL != 1 && ABL != 3 && (flags & kTileAny) && in_lds) {
             if constexpr (FB == 0) stage_footprint_dma(FT, wpr, fth, lvl + (size_t)by0 * a.P + bxa, a.P, lane);
             else stage_footprint<FB>(FT, ftw, wpr, fth, lvl + (size_t)by0 * a.P + bxa, a.P, bxa, a.P, lane);
         }
         wave_sync();
+        if (ABL == 9) {
+            const uint64_t t = __builtin_readcyclecounter();
+            st_acc[1] += t - st_t;
+            st_t = t;
+        }
         if (c0 > cx1) continue;
         // tile-major ROI scratch: tile (ty, tx) is a contiguous 32 x 32 block, so one store instruction of the wave
         // (8 rows x 8 lanes x 4 bytes) writes 256 contiguous bytes
@@ -954,6 +996,11 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
             }
             *(uint32_t*)(dst + (size_t)r * ROI_T) = pk;
         }
+    }
+    if (ABL == 9 && lane == 0 && blockIdx.x < 64) {
+        if (st_n > 0) st_acc[2] += __builtin_readcyclecounter() - st_t;
+        uint64_t* o = a.stamps + (size_t)(blockIdx.x * 4 + wv) * 4;
+        o[0] = st_acc[0]; o[1] = st_acc[1]; o[2] = st_acc[2]; o[3] = (uint64_t)st_n;
     }
 }
 
@@ -1185,28 +1232,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             }
         }
     }
-}
-
-// One bilinear ROI pixel from a staged footprint, BORDER_CONSTANT(0) rules of remapBilinear (general path).
-__device__ __forceinline__ int ft_tap_general(const uint8_t* FT, int ftw, int bxa, int by0, int W, int H, int X, int Y) {
-    const int sx = sat_s16(X >> kInterBits), sy = sat_s16(Y >> kInterBits);
-    const int fx = X & (kInterTab - 1), fy = Y & (kInterTab - 1);
-    const uint8_t* p = FT + (sy - by0) * ftw + (sx - bxa);
-    int v0, v1, v2, v3;
-    if ((unsigned)sx < (unsigned)(W - 1) && (unsigned)sy < (unsigned)(H - 1)) {
-        v0 = p[0]; v1 = p[1]; v2 = p[ftw]; v3 = p[ftw + 1];
-    } else if (sx >= W || sx + 1 < 0 || sy >= H || sy + 1 < 0) {
-        return 0;
-    } else {
-        const bool x0 = sx >= 0 && sx < W, x1 = sx + 1 >= 0 && sx + 1 < W;
-        const bool y0 = sy >= 0 && sy < H, y1 = sy + 1 >= 0 && sy + 1 < H;
-        v0 = x0 && y0 ? p[0] : 0;
-        v1 = x1 && y0 ? p[1] : 0;
-        v2 = x0 && y1 ? p[ftw] : 0;
-        v3 = x1 && y1 ? p[ftw + 1] : 0;
-    }
-    const int h0 = 32 * v0 + fx * (v1 - v0), h1 = 32 * v2 + fx * (v3 - v2);
-    return (32 * h0 + fy * (h1 - h0) + 512) >> 10;
 }
 
 // ---- K6-K8 for small templates: one workgroup per ROI does the whole refinement of the ROI in LDS (tables,

@@ -64,7 +64,7 @@ int main(int argc, char** argv) {
     a.tmpl = d_tm; a.tw = TW; a.th = TH; a.tp = TP;
     {   // MFMA operands: T ^ 0x80 with zero padding, per-row sums
         const int p8 = 64 * ((TW + 63) / 64), rows8 = (TH + kMmaRows - 1) / kMmaRows * kMmaRows;
-        std::vector<int8_t> t8((size_t)p8 * rows8, 0);
+        std::vector<int8_t> t8((size_t)p8 * rows8 + 512, 0);
         std::vector<int32_t> ts(rows8, 0);
         for (int y = 0; y < TH; ++y)
             for (int x = 0; x < TW; ++x) { t8[(size_t)y * p8 + x] = (int8_t)(tm[(size_t)y * TP + x] ^ 0x80); ts[y] += tm[(size_t)y * TP + x]; }
@@ -114,6 +114,22 @@ int main(int argc, char** argv) {
         timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 1>), dim3(grid), dim3(256), 0, 0, a); }, "warp no staging");
         timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 2>), dim3(grid), dim3(256), 0, 0, a); }, "warp no gathers");
         timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 4>), dim3(grid), dim3(256), 0, 0, a); }, "warp dot4 taps");
+        {   // per-wave phase cycles of the product warp (ABL 9): first 64 workgroups
+            uint64_t* d_st;
+            CK(hipMalloc(&d_st, 256 * 4 * 8));
+            CK(hipMemset(d_st, 0, 256 * 4 * 8));
+            RoiArgs b = a;
+            b.stamps = d_st;
+            for (int rep = 0; rep < 3; ++rep) hipLaunchKernelGGL((k_roi_warp<2, 9>), dim3(grid), dim3(256), 0, 0, b);
+            CK(hipDeviceSynchronize());
+            std::vector<uint64_t> h(256 * 4);
+            CK(hipMemcpy(h.data(), d_st, h.size() * 8, hipMemcpyDeviceToHost));
+            double acc[3] = {0, 0, 0}, nt = 0;
+            for (int w = 0; w < 256; ++w) { for (int k = 0; k < 3; ++k) acc[k] += (double)h[w * 4 + k]; nt += (double)h[w * 4 + 3]; }
+            printf("warp phases (cycles per task, %0.f tasks in 256 waves): loads %.0f staging %.0f gathers+stores %.0f\n",
+                   nt, acc[0] / nt, acc[1] / nt, acc[2] / nt);
+            CK(hipFree(d_st));
+        }
         timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 3>), dim3(grid), dim3(256), 0, 0, a); }, "warp tables only");
     }
     timeit([&] { launch_roi_corr(a, 0); }, "prod corr");
@@ -128,6 +144,8 @@ int main(int argc, char** argv) {
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 4>), dim3(grid), dim3(256), lds1, 0, a); }, "corr globA w4");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<2, true, 4>), dim3(grid), dim3(256), lds1, 0, a); }, "corr globA w4 no mfma");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<3, true, 4>), dim3(grid), dim3(256), lds1, 0, a); }, "corr globA w4 no stage");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<3, true, 3>), dim3(grid), dim3(256), lds1, 0, a); }, "corr globA w3 no stage");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<2, true, 3>), dim3(grid), dim3(256), lds1, 0, a); }, "corr globA w3 no mfma");
         launch_roi_corr(a, 0);
     }
     {   // host check of k_roi_corr on a few ROI slots
@@ -168,7 +186,7 @@ int main(int argc, char** argv) {
         RoiArgs b = a;
         b.W = W3; b.H = H3; b.tw = TW3; b.th = TH3;
         const int p8 = 128, rows8 = 80;
-        std::vector<int8_t> t8((size_t)p8 * rows8 + 64, 0);
+        std::vector<int8_t> t8((size_t)p8 * rows8 + 512, 0);
         std::vector<int32_t> ts(rows8, 0);
         for (int y = 0; y < TH3; ++y)
             for (int x = 0; x < TW3; ++x) { t8[(size_t)y * p8 + x] = (int8_t)(tm[(size_t)y * TP + x] ^ 0x80); ts[y] += tm[(size_t)y * TP + x]; }
