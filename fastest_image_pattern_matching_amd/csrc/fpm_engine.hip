@@ -96,8 +96,9 @@ struct Plan {
     std::vector<size_t> canvas_off, map_off, blk_off;
     std::vector<int> canvas_pitch, map_w, map_h, nblk;
     size_t canvas_bytes = 0, map_floats = 0, blk_count = 0;
-    int max_canvas = 0, max_map = 0;
+    int max_canvas = 0, max_map = 0, max_nblk = 0;
     // device buffers owned by the plan
+    DevBuf d_ncand, d_ncnt;                    // s_BlockMax candidate lists (k_nms_blocks -> k_nms_fast)
     DevBuf d_canvas, d_map, d_bmax, d_bloc, d_jobs, d_nodes, d_top, d_topn, d_peaks, d_counts, d_state,
         d_live, d_livecnt, d_rec, d_rowsum, d_wsum, d_wsq, d_tab, d_roi, d_tdesc;
     int tabw = 0, tabh = 0, roi_pitch = 0, tdesc_stride = 1;
@@ -108,7 +109,7 @@ struct Plan {
     size_t h_counts = 0, h_peaks = 0, h_live = 0, h_live0 = 0, h_state = 0, h_rec = 0, h_total = 0;
     char* h_dev = nullptr;   // device-side address of h_out (k_pack writes it over PCIe)
     void release() {
-        for (DevBuf* b : {&d_canvas, &d_map, &d_bmax, &d_bloc, &d_jobs, &d_nodes, &d_top, &d_topn, &d_peaks,
+        for (DevBuf* b : {&d_ncand, &d_ncnt, &d_canvas, &d_map, &d_bmax, &d_bloc, &d_jobs, &d_nodes, &d_top, &d_topn, &d_peaks,
                           &d_counts, &d_state, &d_live, &d_livecnt, &d_rec, &d_rowsum, &d_wsum, &d_wsq, &d_tab, &d_roi, &d_tdesc})
             b->release();
         h_out.release();
@@ -320,7 +321,7 @@ int build_plan(fpm_ctx* ctx) {
     P.canvas_pitch.resize(P.nang); P.map_w.resize(P.nang); P.map_h.resize(P.nang); P.nblk.resize(P.nang);
     std::vector<std::array<double, 6>> mats(P.nang);
     size_t co = 0, mo = 0, bo = 0;
-    P.max_canvas = 0; P.max_map = 0;
+    P.max_canvas = 0; P.max_map = 0; P.max_nblk = 0;
     for (int a = 0; a < P.nang; ++a) {
         int bw, bh;
         best_rotation_size(top.w, top.h, tt.w, tt.h, P.angles[a], &bw, &bh);
@@ -351,6 +352,7 @@ int build_plan(fpm_ctx* ctx) {
             nb = ncol * nrow + (rw > 0) + (rh > 0) + (rw > 0 && rh > 0);
         }
         P.nblk[a] = nb;
+        P.max_nblk = std::max(P.max_nblk, nb);
         P.blk_off[a] = bo;
         bo += round_up((size_t)nb, (size_t)64);
         P.max_canvas = std::max(P.max_canvas, bw * bh);
@@ -394,6 +396,10 @@ int build_plan(fpm_ctx* ctx) {
     HIP_TRY(P.d_topn.ensure(sizeof(AngleNode) * P.nang));
     HIP_TRY(P.d_peaks.ensure(sizeof(Peak) * (size_t)P.C));
     HIP_TRY(P.d_counts.ensure(sizeof(int32_t) * J));
+    if (P.by_block) {
+        HIP_TRY(P.d_ncand.ensure(sizeof(int32_t) * (size_t)kNmsCandCap * J));
+        HIP_TRY(P.d_ncnt.ensure(sizeof(int32_t) * J));
+    }
     HIP_TRY(P.d_state.ensure(sizeof(CandState) * (size_t)P.C));
     HIP_TRY(P.d_live.ensure(sizeof(int32_t) * (size_t)P.C * 2));
     HIP_TRY(P.d_livecnt.ensure(sizeof(int32_t) * (L + 2)));
@@ -568,7 +574,15 @@ int enqueue_search(fpm_ctx* ctx) {
         na.counts = P.d_counts.as<int32_t>();
         na.tw = tt.w; na.th = tt.h; na.cap = P.cap; na.by_block = P.by_block ? 1 : 0;
         na.thr = P.layer_score[L]; na.overlap = ctx->prm.max_overlap;
-        launch_nms(na, J, P.max_map, st);
+        na.lds_blocks = 0;
+        na.cand = nullptr; na.cand_cnt = nullptr; na.cand_cap = 0; na.cand_lds = 0; na.stamps = nullptr;
+        if (P.by_block) {
+            HIP_TRY(hipMemsetAsync(P.d_ncnt.p, 0, sizeof(int32_t) * J, st));
+            na.cand = P.d_ncand.as<int32_t>(); na.cand_cnt = P.d_ncnt.as<int32_t>(); na.cand_cap = kNmsCandCap;
+        }
+        int mdim = 0;
+        for (int a = 0; a < P.nang; ++a) mdim = std::max(mdim, std::max(P.map_w[a], P.map_h[a]));
+        launch_nms(na, J, P.max_nblk, mdim, st);
     }
     HIP_TRY(hipMemsetAsync(P.d_livecnt.p, 0, sizeof(int32_t) * (L + 2), st));
     int32_t* live[2] = {P.d_live.as<int32_t>(), P.d_live.as<int32_t>() + P.C};

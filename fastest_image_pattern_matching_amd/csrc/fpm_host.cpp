@@ -173,10 +173,27 @@ void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
     if (v.empty()) return;
     const int n = (int)v.size();
     std::vector<F2> pts;
+    // corner bounding boxes: pairs whose boxes are > 1 px apart cannot have an edge crossing or a contained corner,
+    // so rrect_intersection would return INTERSECT_NONE; skipping them keeps the reference's O(n^2) loop order
+    // and deletions exactly while avoiding the exact test for far-apart detections
+    std::vector<float> box((size_t)4 * n);
+    for (int i = 0; i < n; ++i) {
+        F2 c[4];
+        rrect_corners(v[i].rect, c);
+        float x0 = c[0].x, x1 = c[0].x, y0 = c[0].y, y1 = c[0].y;
+        for (int k = 1; k < 4; ++k) {
+            x0 = std::min(x0, c[k].x); x1 = std::max(x1, c[k].x);
+            y0 = std::min(y0, c[k].y); y1 = std::max(y1, c[k].y);
+        }
+        box[4 * i] = x0 - 1.f; box[4 * i + 1] = y0 - 1.f; box[4 * i + 2] = x1 + 1.f; box[4 * i + 3] = y1 + 1.f;
+    }
     for (int i = 0; i + 1 < n; ++i) {
         if (v[i].del) continue;
+        const float* bi = &box[4 * i];
         for (int j = i + 1; j < n; ++j) {
             if (v[j].del) continue;
+            const float* bj = &box[4 * j];
+            if (bj[0] > bi[2] || bj[2] < bi[0] || bj[1] > bi[3] || bj[3] < bi[1]) continue;
             const int kind = rrect_intersection(v[i].rect, v[j].rect, pts);
             if (kind == 0) continue;
             bool drop = kind == 2;

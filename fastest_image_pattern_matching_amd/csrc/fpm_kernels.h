@@ -52,8 +52,14 @@ struct NmsArgs {
     int32_t tw, th;          // top template size
     int32_t cap;             // max_pos + MATCH_CANDIDATE_NUM
     int32_t by_block;
+    int32_t lds_blocks;      // block-maxima capacity in LDS (set by launch_nms; 0 = global scratch)
+    int32_t* cand;           // s_BlockMax mode: indices of the map pixels >= thr, [job][cand_cap] (k_nms_blocks)
+    int32_t* cand_cnt;       // [job], zeroed before the launch
+    int32_t cand_cap;        // kNmsCandCap
+    int32_t cand_lds;        // candidate capacity in LDS (set by launch_nms)
     double thr;              // vecLayerScore[top]
     double overlap;
+    uint64_t* stamps;        // profiling only (scripts/nms_probe.hip): k_nms_fast phase cycles of job 0, else null
 };
 
 // Angle-tree node: the reference's refinement angle for one path, with glibc trig of angle*D2R.
@@ -150,7 +156,9 @@ void launch_warp(const WarpJob* jobs, int njobs, int max_pixels, hipStream_t st)
 void launch_ncc_map(const NccJob* jobs, int njobs, int max_out, int tmpl_bytes, hipStream_t st);
 bool ncc_tile_fits(int tw, int th);   // LDS-tiled variant applies (templates up to 128 x 64)
 void launch_ncc_tile(const NccJob* jobs, int njobs, int max_ow, int max_oh, hipStream_t st);
-void launch_nms(const NmsArgs& a, int njobs, int max_map, hipStream_t st);
+constexpr int kNmsCandCap = 8192;   // s_BlockMax candidates (pixels >= the top-layer score) kept per map
+// max_blocks: s_BlockMax blocks of the largest map (block mode); max_map_dim: largest map width or height
+void launch_nms(const NmsArgs& a, int njobs, int max_blocks, int max_map_dim, hipStream_t st);
 void launch_cand_init(const CandInitArgs& a, hipStream_t st);
 void launch_roi_tables(const RoiArgs& a, hipStream_t st);
 void launch_roi_warp(const RoiArgs& a, hipStream_t st);

@@ -414,12 +414,116 @@ struct BlockGeom {
     }
 };
 
+// wave argmax (value, key) with lowest-key tie-break, by DPP steps (no LDS round trip per step): quad swaps, row
+// half-mirror, row mirror, then row_bcast15 / row_bcast31 fold the rows into lane 63, read back to every lane
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void dpp_better(float& v, int& b) {
+    const float ov = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(-INFINITY), __float_as_int(v), CTRL,
+                                                                ROWS, 0xf, false));
+    const int ob = __builtin_amdgcn_update_dpp(INT_MAX, b, CTRL, ROWS, 0xf, false);
+    better(v, b, ov, ob);
+}
+__device__ __forceinline__ void wave_better_reduce(float& v, int& b) {
+    dpp_better<0xb1, 0xf>(v, b);    // quad_perm [1,0,3,2]
+    dpp_better<0x4e, 0xf>(v, b);    // quad_perm [2,3,0,1]
+    dpp_better<0x141, 0xf>(v, b);   // row_half_mirror
+    dpp_better<0x140, 0xf>(v, b);   // row_mirror
+    dpp_better<0x142, 0xa>(v, b);   // row_bcast15 into rows 1 and 3
+    dpp_better<0x143, 0xc>(v, b);   // row_bcast31 into rows 2 and 3
+    v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+    b = __builtin_amdgcn_readlane(b, 63);
+}
+
+// minMaxLoc over a sub-rectangle by one wave: first max in row-major order (rect_max), result in every lane
+__device__ __forceinline__ void wave_rect_max(const float* m, int mw, int x0, int y0, int w, int h, int lane,
+                                              float& bv, int& bi) {
+    const int n = w * h;
+    if (n <= 0) {   // empty rectangle (a zero-width strip): its origin pixel, as rect_max / the oracle's max_loc
+        bi = y0 * mw + x0;
+        bv = m[bi];
+        return;
+    }
+    float v = -INFINITY;
+    int i = INT_MAX;
+    int r = lane / w, c = lane - (lane / w) * w;   // element e = lane + 64k -> (r, c), advanced incrementally
+    const int dr = 64 / w, dc = 64 - (64 / w) * w;
+#pragma unroll 4
+    for (int e = lane; e < n; e += 64) {
+        const int idx = (y0 + r) * mw + x0 + c;
+        const float x = m[idx];
+        if (x > v) { v = x; i = idx; }   // a lane visits increasing indices: strict > keeps the first
+        r += dr;
+        c += dc;
+        if (c >= w) { c -= w; ++r; }
+    }
+    wave_better_reduce(v, i);
+    bv = v;
+    bi = i;
+}
+
+// K5a: the s_BlockMax constructor (DataStructures.h:150-213) for every top-layer map at once, one wave per block;
+// with a.cand it also lists the map's pixels >= thr (the only ones the peak loop can accept), each pixel once (the
+// corner block, which repeats the right strip's pixels, emits none)
+__global__ __launch_bounds__(256) void k_nms_blocks(NmsArgs a) {
+    const NmsJob& j = a.jobs[blockIdx.y];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    BlockGeom g;
+    g.init(j.mw, j.mh, a.tw, a.th);
+    if (j.mw <= 0 || j.mh <= 0) return;
+    const int corner = (g.rw > 0 && g.rh > 0) ? g.nb - 1 : -1;
+    int32_t* cand = a.cand ? a.cand + (size_t)blockIdx.y * a.cand_cap : nullptr;
+    for (int b = blockIdx.x * 4 + wv; b < g.nb; b += gridDim.x * 4) {
+        int x, y, w, h;
+        g.rect(b, j.mw, j.mh, a.tw, a.th, x, y, w, h);
+        float v;
+        int i;
+        wave_rect_max(j.map, j.mw, x, y, w, h, lane, v, i);
+        if (lane == 0) { j.bmax[b] = v; j.bloc[b] = i; }
+        if (cand && b != corner && w * h > 0) {
+            const int n = w * h;
+            int r = lane / w, c = lane - (lane / w) * w;
+            const int dr = 64 / w, dc = 64 - (64 / w) * w;
+            for (int e0 = 0; e0 < n; e0 += 64) {
+                const int idx = (y + r) * j.mw + x + c;
+                const bool take = e0 + lane < n && (double)j.map[idx] >= a.thr;
+                const uint64_t mk = __ballot(take);
+                if (mk) {
+                    int base = 0;
+                    if (lane == 0) base = atomicAdd(&a.cand_cnt[blockIdx.y], __popcll(mk));
+                    base = __shfl(base, 0);
+                    const int pos = base + __popcll(mk & ((1ull << lane) - 1));
+                    if (take && pos < a.cand_cap) cand[pos] = idx;
+                }
+                r += dr;
+                c += dc;
+                if (c >= w) { c -= w; ++r; }
+            }
+        }
+    }
+}
+
+// argmax over the block maxima (GetMaxValueLoc: max_element, first block on ties), broadcast to every thread
+__device__ __forceinline__ void block_argmax(const float* bm, const int* bl, int nb, float* sv, int* si, float& v,
+                                             int& i) {
+    v = -INFINITY;
+    i = INT_MAX;
+    for (int b = threadIdx.x; b < nb; b += 256) better(v, i, bm[b], b);
+    wg_argmax(v, i, sv, si);
+    i = bl[i];
+}
+
+// K5: peak extraction of one map per workgroup: getNextMaxLoc (plain: painted rectangle + full-map argmax) or its
+// s_BlockMax form when k_nms_fast's LDS cannot hold the map's blocks (block maxima from k_nms_blocks in global
+// scratch; after each painted rectangle the intersecting blocks are re-scanned one wave per block,
+// TemplateMatcher.cpp:1208-1221, DataStructures.h:215-246)
 __global__ __launch_bounds__(256) void k_nms(NmsArgs a) {
     __shared__ float sv[4];
     __shared__ int si[4];
+    __shared__ int naff;
+    __shared__ int aff[256];
     const NmsJob& j = a.jobs[blockIdx.x];
     float* m = j.map;
-    const int mw = j.mw, mh = j.mh, n = mw * mh, tid = threadIdx.x;
+    const int mw = j.mw, mh = j.mh, n = mw * mh, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     Peak* out = a.peaks + (size_t)blockIdx.x * a.cap;
     const double ov = a.overlap;
     BlockGeom g;
@@ -427,16 +531,10 @@ __global__ __launch_bounds__(256) void k_nms(NmsArgs a) {
     float v = -INFINITY;
     int i = INT_MAX;
     if (n <= 0) { if (tid == 0) a.counts[blockIdx.x] = 0; return; }
+    float* bm = j.bmax;
+    int* bl = j.bloc;
     if (a.by_block) {
-        for (int b = tid; b < g.nb; b += 256) {
-            int x, y, w, h;
-            g.rect(b, mw, mh, a.tw, a.th, x, y, w, h);
-            rect_max(m, mw, x, y, w, h, &j.bmax[b], &j.bloc[b]);
-        }
-        __syncthreads();
-        for (int b = tid; b < g.nb; b += 256) better(v, i, j.bmax[b], b);
-        wg_argmax(v, i, sv, si);
-        i = j.bloc[i];
+        block_argmax(bm, bl, g.nb, sv, si, v, i);
     } else {
         for (int k = tid; k < n; k += 256) { const float x = m[k]; if (x > v) { v = x; i = k; } }
         wg_argmax(v, i, sv, si);
@@ -457,22 +555,46 @@ __global__ __launch_bounds__(256) void k_nms(NmsArgs a) {
             if (cw > 0 && ch > 0)
                 for (int k = tid; k < cw * ch; k += 256) m[(size_t)(y1 + k / cw) * mw + x1 + k % cw] = -1.f;
         }
+        if (tid == 0) naff = 0;
         __syncthreads();
-        v = -INFINITY;
-        i = INT_MAX;
         if (a.by_block) {
+            // blocks whose rectangle intersects the painted one (UpdateMax), listed, then re-scanned per wave
             for (int b = tid; b < g.nb; b += 256) {
                 int x, y, w, h;
                 g.rect(b, mw, mh, a.tw, a.th, x, y, w, h);
                 const int ix1 = max(x, sx), iy1 = max(y, sy);
                 const int iw = min(x + w, sx + rw) - ix1, ih = min(y + h, sy + rh) - iy1;
-                if (iw > 0 && ih > 0) rect_max(m, mw, x, y, w, h, &j.bmax[b], &j.bloc[b]);
+                if (iw > 0 && ih > 0) {
+                    const int k = atomicAdd(&naff, 1);
+                    if (k < 256) aff[k] = b;
+                }
             }
             __syncthreads();
-            for (int b = tid; b < g.nb; b += 256) better(v, i, j.bmax[b], b);
-            wg_argmax(v, i, sv, si);
-            i = j.bloc[i];
+            const int na = naff;
+            if (na <= 256) {
+                for (int k = wv; k < na; k += 4) {
+                    const int b = aff[k];
+                    int x, y, w, h;
+                    g.rect(b, mw, mh, a.tw, a.th, x, y, w, h);
+                    float bv;
+                    int bi;
+                    wave_rect_max(m, mw, x, y, w, h, lane, bv, bi);
+                    if (lane == 0) { bm[b] = bv; bl[b] = bi; }
+                }
+            } else {   // (a painted rectangle spanning > 256 blocks: overlap < 0 with tiny blocks) one per thread
+                for (int b = tid; b < g.nb; b += 256) {
+                    int x, y, w, h;
+                    g.rect(b, mw, mh, a.tw, a.th, x, y, w, h);
+                    const int ix1 = max(x, sx), iy1 = max(y, sy);
+                    const int iw = min(x + w, sx + rw) - ix1, ih = min(y + h, sy + rh) - iy1;
+                    if (iw > 0 && ih > 0) rect_max(m, mw, x, y, w, h, &bm[b], &bl[b]);
+                }
+            }
+            __syncthreads();
+            block_argmax(bm, bl, g.nb, sv, si, v, i);
         } else {
+            v = -INFINITY;
+            i = INT_MAX;
             for (int k = tid; k < n; k += 256) { const float x = m[k]; if (x > v) { v = x; i = k; } }
             wg_argmax(v, i, sv, si);
         }
@@ -483,8 +605,434 @@ __global__ __launch_bounds__(256) void k_nms(NmsArgs a) {
     if (tid == 0) a.counts[blockIdx.x] = cnt;
 }
 
-void launch_nms(const NmsArgs& a, int njobs, int /*max_map*/, hipStream_t st) {
+// K5 (s_BlockMax, fast form): the same sequence of peaks as k_nms's block mode with the map left untouched.  A
+// pixel inside an accepted peak's rectangle reads as -1 (the value getNextMaxLoc paints), so an iteration is: the
+// blocks the new rectangle intersects (from the grid arithmetic, UpdateMax), their maxima re-scanned one wave per
+// block, the maxima of their 64-block groups, and one wave's argmax over the group maxima (GetMaxValueLoc: first
+// block on ties).  Block / group maxima and the accepted peaks live in LDS.  Sparse mode (thr > -1 and the
+// map's candidate list fits): a block's maximum only matters while it is >= thr, and every pixel >= thr is in
+// the candidate list, so a block re-scan reads its few candidates from LDS instead of the map (a block left with
+// none reads -inf: the loop then stops exactly where the reference's maximum drops below thr).
+
+// s_BlockMax block(s) holding map pixel (x, y): grid block or strip; b2 = the corner block (repeats the right strip)
+__device__ __forceinline__ int nms_block_of(const BlockGeom& g, int x, int y, int tw, int th, int& b2) {
+    const int gw = g.ncol * tw, gh = g.nrow * th, base = g.ncol * g.nrow;
+    b2 = -1;
+    if (x < gw && y < gh) return (y / th) * g.ncol + x / tw;
+    if (x >= gw) {
+        if (y >= gh) b2 = base + 2;   // rw > 0 and rh > 0: right strip, bottom strip, corner
+        return base;
+    }
+    return base + (g.rw > 0 ? 1 : 0);
+}
+
+__global__ __launch_bounds__(256) void k_nms_fast(NmsArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t nms_lds[];
+    __shared__ int wsum[4];
+    __shared__ int sparse_s;
+    const NmsJob& j = a.jobs[blockIdx.x];
+    const float* m = j.map;
+    const int mw = j.mw, mh = j.mh, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    Peak* out = a.peaks + (size_t)blockIdx.x * a.cap;
+    if (a.cand && a.cand_cnt[blockIdx.x] < 0) return;   // taken by k_nms_greedy
+    if (mw <= 0 || mh <= 0) { if (tid == 0) a.counts[blockIdx.x] = 0; return; }
+    const bool stamp = a.stamps && blockIdx.x == 0 && tid == 0;
+    uint64_t st_t = stamp ? __builtin_readcyclecounter() : 0, st_acc[6] = {0, 0, 0, 0, 0, 0};
+    auto STAMP = [&](int k) {
+        if (stamp) { const uint64_t t = __builtin_readcyclecounter(); st_acc[k] += t - st_t; st_t = t; }
+    };
+    const double ov = a.overlap;
+    const int tw = a.tw, th = a.th;
+    BlockGeom g;
+    g.init(mw, mh, tw, th);
+    const int nb = g.nb, ng = (nb + 63) >> 6, LB = a.lds_blocks;
+    // positions are kept as keys (y << 16) | x (maps are < 65536 wide and high): key order = row-major order, so
+    // ties resolve exactly as on map indices, and no division is needed in the loop
+    float* bm = (float*)nms_lds;                  // [LB] block maxima
+    int* bl = (int*)(bm + LB);                    // [LB] their keys
+    int* st = bl + LB;                            // [LB + 1] candidate ranges (sparse mode)
+    float* gm = (float*)(st + LB + 1);            // [LB / 64 + 1] group maxima
+    int* gb = (int*)(gm + (LB >> 6) + 1);         // their block indices
+    float* cv = (float*)(gb + (LB >> 6) + 1);     // [cand_lds] candidate values, grouped by block
+    int* ci = (int*)(cv + a.cand_lds);            // [cand_lds] candidate keys
+    for (int b = tid; b < nb; b += 256) {
+        const int idx = j.bloc[b];
+        bm[b] = j.bmax[b];
+        bl[b] = ((idx / mw) << 16) | (idx % mw);
+    }
+    // ---- sparse mode setup: counting sort of the candidate list by block into LDS
+    const int K = a.cand ? a.cand_cnt[blockIdx.x] : 0;
+    bool sparse = a.cand && a.thr > -1.0 && K <= a.cand_cap && K <= a.cand_lds;
+    if (sparse) {
+        const int32_t* cand = a.cand + (size_t)blockIdx.x * a.cand_cap;
+        for (int b = tid; b <= nb; b += 256) st[b] = 0;
+        __syncthreads();
+        for (int k = tid; k < K; k += 256) {
+            const int idx = cand[k];
+            int b2;
+            const int b = nms_block_of(g, idx % mw, idx / mw, tw, th, b2);
+            atomicAdd(&st[b], 1);
+            if (b2 >= 0) atomicAdd(&st[b2], 1);
+        }
+        __syncthreads();
+        // exclusive scan of st[0 .. nb): per-thread chunk sums, wave prefix by shuffles, wave totals, chunk re-walk
+        const int chunk = (nb + 255) / 256, c0 = tid * chunk, c1 = min(nb, c0 + chunk);
+        int sum = 0;
+        for (int b = c0; b < c1; ++b) sum += st[b];
+        int incl = sum;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(incl, off);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        int run = incl - sum;
+        for (int w = 0; w < wv; ++w) run += wsum[w];
+        if (tid == 255) sparse_s = run + sum <= a.cand_lds;   // the corner's repeats must fit too
+        for (int b = c0; b < c1; ++b) { const int x = st[b]; st[b] = run; run += x; }
+        __syncthreads();
+        sparse = sparse_s != 0;
+        if (sparse) {
+            for (int k = tid; k < K; k += 256) {   // scatter; afterwards st[b] = end of block b = start of b + 1
+                const int idx = cand[k];
+                const float val = m[idx];
+                const int x = idx % mw, y = idx / mw, key = (y << 16) | x;
+                int b2;
+                const int b = nms_block_of(g, x, y, tw, th, b2);
+                const int p = atomicAdd(&st[b], 1);
+                cv[p] = val; ci[p] = key;
+                if (b2 >= 0) { const int p2 = atomicAdd(&st[b2], 1); cv[p2] = val; ci[p2] = key; }
+            }
+        }
+    }
+    __syncthreads();
+    auto group_max = [&](int gi) {   // one wave
+        const int b = gi * 64 + lane;
+        float v = b < nb ? bm[b] : -INFINITY;
+        int bb = b < nb ? b : INT_MAX;
+        wave_better_reduce(v, bb);
+        if (lane == 0) { gm[gi] = v; gb[gi] = bb; }
+    };
+    for (int gi = wv; gi < ng; gi += 4) group_max(gi);
+    __syncthreads();
+    // the peak loop runs in wave 0 alone (no barriers): the state is in LDS and the work per peak is a few blocks
+    if (wv != 0) return;
+    int nres = 0;   // (profiling) blocks re-scanned
+    auto final_max = [&](float& v, int& key) {
+        float fv = -INFINITY;
+        int bb = INT_MAX;
+        for (int k = lane; k < ng; k += 64) better(fv, bb, gm[k], gb[k]);
+        wave_better_reduce(fv, bb);
+        v = fv;
+        key = bl[bb];
+    };
+    float v;
+    int key;
+    final_max(v, key);
+    STAMP(0);   // setup
+    // rectangle of getNextMaxLoc (TemplateMatcher.cpp:1198-1201 / :1211-1214): int truncation of f64
+    const int rw = (int)(2 * tw * (1 - ov)), rh = (int)(2 * th * (1 - ov));
+    const int gw = g.ncol * tw, gh = g.nrow * th, ngrid = g.ncol * g.nrow;
+    int qx[4] = {0, 0, 0, 0}, qy[4] = {0, 0, 0, 0};   // accepted rectangles' origins: rectangle k in lane k % 64
+    int cnt = 0;
+    for (;;) {
+        if ((double)v < a.thr) break;
+        const int px = key & 0xffff, py = key >> 16;
+        const int sx = (int)(px - tw * (1 - ov)), sy = (int)(py - th * (1 - ov));
+        if (lane == 0) { out[cnt].x = px; out[cnt].y = py; out[cnt].score = v; }
+        if (lane == (cnt & 63)) {
+            const int hw = cnt >> 6;
+            if (hw == 0) { qx[0] = sx; qy[0] = sy; }
+            else if (hw == 1) { qx[1] = sx; qy[1] = sy; }
+            else if (hw == 2) { qx[2] = sx; qy[2] = sy; }
+            else { qx[3] = sx; qy[3] = sy; }
+        }
+        ++cnt;
+        if (cnt >= a.cap) break;
+        if (rw <= 0 || rh <= 0) continue;   // nothing painted: the same peak again (as the reference finds it)
+        // blocks intersecting [sx, sx + rw) x [sy, sy + rh) (UpdateMax), one candidate per lane: lanes 0-8 the <= 3x3
+        // grid blocks, lanes 9-11 the right strip, bottom strip and corner
+        int lb = -1, lx = 0, ly = 0, lw = 0, lh = 0;
+        if (lane < 9) {
+            if (g.ncol > 0 && g.nrow > 0 && sx < gw && sx + rw > 0 && sy < gh && sy + rh > 0) {
+                const int c0 = max(sx, 0) / tw, c1 = min(sx + rw - 1, gw - 1) / tw;
+                const int r0 = max(sy, 0) / th, r1 = min(sy + rh - 1, gh - 1) / th;
+                const int r = r0 + lane / 3, c = c0 + lane % 3;
+                if (r <= r1 && c <= c1) { lb = r * g.ncol + c; lx = c * tw; ly = r * th; lw = tw; lh = th; }
+            }
+        } else if (lane == 9) {
+            if (g.rw > 0) { lb = ngrid; lx = gw; ly = 0; lw = g.rw; lh = mh; }
+        } else if (lane == 10) {
+            if (g.rh > 0) { lb = ngrid + (g.rw > 0 ? 1 : 0); lx = 0; ly = gh; lw = gw; lh = g.rh; }
+        } else if (lane == 11) {
+            if (g.rw > 0 && g.rh > 0) { lb = ngrid + 2; lx = gw; ly = gh; lw = g.rw; lh = g.rh; }
+        }
+        bool upd = lb >= 0 && min(lx + lw, sx + rw) - max(lx, sx) > 0 && min(ly + lh, sy + rh) - max(ly, sy) > 0;
+        // painting only lowers values: a block whose current maximum lies outside the new rectangle keeps it (value
+        // and first position), so only blocks whose maximum was painted are re-scanned
+        if (upd) {
+            const int k = bl[lb], kx = k & 0xffff, ky = k >> 16;
+            upd = kx >= sx && kx < sx + rw && ky >= sy && ky < sy + rh;
+        }
+        const uint64_t umask = __ballot(upd);
+        STAMP(1);   // enumeration + the painted-maximum test
+        for (uint64_t mk = umask; mk;) {
+            const int l = __builtin_ctzll(mk);
+            mk &= mk - 1;
+            const int b = __builtin_amdgcn_readlane(lb, l);
+            const int x = __builtin_amdgcn_readlane(lx, l), y = __builtin_amdgcn_readlane(ly, l);
+            const int w = __builtin_amdgcn_readlane(lw, l), h = __builtin_amdgcn_readlane(lh, l);
+            // accepted rectangles that meet this block
+            uint64_t hit[4];
+#pragma unroll
+            for (int hw = 0; hw < 4; ++hw) {
+                const int k = hw * 64 + lane;
+                hit[hw] = __ballot(k < cnt && min(x + w, qx[hw] + rw) > max(x, qx[hw]) &&
+                                   min(y + h, qy[hw] + rh) > max(y, qy[hw]));
+            }
+            auto painted = [&](int X, int Y) {
+                bool p = false;
+#pragma unroll
+                for (int hw = 0; hw < 4; ++hw) {
+                    uint64_t hm = hit[hw];
+                    while (hm) {
+                        const int hl = __builtin_ctzll(hm);
+                        hm &= hm - 1;
+                        const int ax = __builtin_amdgcn_readlane(qx[hw], hl), ay = __builtin_amdgcn_readlane(qy[hw], hl);
+                        p |= X >= ax && X < ax + rw && Y >= ay && Y < ay + rh;
+                    }
+                }
+                return p;
+            };
+            float bv = -INFINITY;
+            int bk = INT_MAX;
+            if (sparse) {
+                const int e0 = b == 0 ? 0 : st[b - 1], e1 = st[b];
+                for (int e = e0 + lane; e < e1; e += 64) {
+                    const int ck = ci[e];
+                    const float cval = cv[e];
+                    if (!painted(ck & 0xffff, ck >> 16)) better(bv, bk, cval, ck);
+                }
+                wave_better_reduce(bv, bk);
+                if (bk == INT_MAX) bk = (y << 16) | x;   // no candidate left: below thr (any valid position)
+            } else {
+                const int n = w * h;
+                int r = lane / w, cc = lane - (lane / w) * w;
+                const int dr = 64 / w, dc = 64 - (64 / w) * w;
+                for (int e = lane; e < n; e += 64) {
+                    const int X = x + cc, Y = y + r;
+                    const float val = painted(X, Y) ? -1.f : m[Y * mw + X];
+                    if (val > bv) { bv = val; bk = (Y << 16) | X; }
+                    r += dr;
+                    cc += dc;
+                    if (cc >= w) { cc -= w; ++r; }
+                }
+                wave_better_reduce(bv, bk);   // ties: lowest key = first in the block's row-major order
+            }
+            if (lane == 0) { bm[b] = bv; bl[b] = bk; }
+            ++nres;
+        }
+        STAMP(2);   // block re-scans
+        // the re-scanned blocks' 64-block groups (unique)
+        const int lg = upd ? (lb >> 6) : -1;
+        bool first = upd;
+        for (int u = 0; u < 12; ++u) {
+            const int gu = __builtin_amdgcn_readlane(lg, u);
+            if (u < lane && gu == lg) first = false;
+        }
+        for (uint64_t gmask = __ballot(first); gmask;) {
+            const int l = __builtin_ctzll(gmask);
+            gmask &= gmask - 1;
+            group_max(__builtin_amdgcn_readlane(lg, l));
+        }
+        STAMP(3);   // group maxima
+        final_max(v, key);
+        STAMP(4);   // final argmax
+    }
+    if (tid == 0) a.counts[blockIdx.x] = cnt;
+    if (stamp) {
+        for (int k = 0; k < 5; ++k) a.stamps[k] = st_acc[k];
+        a.stamps[5] = (uint64_t)cnt;
+        a.stamps[6] = (uint64_t)(sparse ? 1 : 0);
+        a.stamps[7] = (uint64_t)nres;
+    }
+}
+
+// K5 (s_BlockMax, greedy form).  With every painted rectangle the reference takes the maximum of the remaining
+// pixels, ordered by value (descending), then block (first in s_BlockMax order: max_element), then row-major
+// position inside the block (minMaxLoc).  Only pixels >= thr can be taken and the values never change except by
+// painting, so the peak sequence is the greedy pass over the pixels >= thr sorted by that key: a pixel is taken
+// iff no earlier taken pixel's rectangle covers it.  Here: bitonic sort of the candidate list in LDS, then one
+// wave walks it 64 candidates at a time; coverage is looked up in per-cell lists (cells of template size) of the
+// taken rectangles.  Maps this form does not take (candidate list too long, thr <= -1, an empty painted
+// rectangle, a zero-width strip) are left to k_nms_fast; a taken map is marked by cand_cnt = -1.
+constexpr int kGreedyMax = 4096;   // candidates sorted in LDS
+constexpr int kCellIds = 6;        // taken rectangles listed per cell before the cell falls back to a full scan
+
+__device__ __forceinline__ bool greedy_before(float va, uint64_t ka, float vb, uint64_t kb) {
+    return va > vb || (va == vb && ka < kb);
+}
+
+__global__ __launch_bounds__(256) void k_nms_greedy(NmsArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t nms_lds[];
+    const NmsJob& j = a.jobs[blockIdx.x];
+    const float* m = j.map;
+    const int mw = j.mw, mh = j.mh, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const double ov = a.overlap;
+    const int tw = a.tw, th = a.th;
+    const int rw = (int)(2 * tw * (1 - ov)), rh = (int)(2 * th * (1 - ov));
+    BlockGeom g;
+    g.init(mw, mh, tw, th);
+    const int K = a.cand_cnt[blockIdx.x];
+    const int cxn = (mw + tw - 1) / tw, cyn = (mh + th - 1) / th, ncell = cxn * cyn;
+    if (!(mw > 0 && mh > 0 && g.ncol > 0 && g.nrow > 0 && rw > 0 && rh > 0 && a.thr > -1.0 && K >= 0 &&
+          K <= a.cand_cap && K <= kGreedyMax && ncell <= a.lds_blocks))
+        return;
+    int P = 64;
+    while (P < K) P <<= 1;
+    float* sv = (float*)nms_lds;                       // [kGreedyMax] values
+    uint64_t* sk = (uint64_t*)(sv + kGreedyMax);       // [kGreedyMax] (block << 32) | (y << 16) | x
+    uint8_t* ccnt = (uint8_t*)(sk + kGreedyMax);       // [cells] taken rectangles per cell
+    uint8_t* cids = ccnt + a.lds_blocks;               // [cells][kCellIds]
+    int* accx = (int*)(cids + (size_t)a.lds_blocks * kCellIds + 16 - ((a.lds_blocks * (1 + kCellIds)) & 15));
+    int* accy = accx + 256;
+    const int32_t* cand = a.cand + (size_t)blockIdx.x * a.cand_cap;
+    for (int i = tid; i < P; i += 256) {
+        if (i < K) {
+            const int idx = cand[i], x = idx % mw, y = idx / mw;
+            int b2;
+            const int b = nms_block_of(g, x, y, tw, th, b2);
+            sv[i] = m[idx];
+            sk[i] = ((uint64_t)b << 32) | (uint32_t)((y << 16) | x);
+        } else {
+            sv[i] = -INFINITY;
+            sk[i] = ~0ull;
+        }
+    }
+    for (int c = tid; c < ncell; c += 256) ccnt[c] = 0;
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1)   // bitonic sort into greedy order
+        for (int jj = k >> 1; jj > 0; jj >>= 1) {
+            for (int i = tid; i < P; i += 256) {
+                const int l = i ^ jj;
+                if (l > i) {
+                    const float vi = sv[i], vl = sv[l];
+                    const uint64_t ki = sk[i], kl = sk[l];
+                    const bool asc = (i & k) == 0;
+                    if (asc ? greedy_before(vl, kl, vi, ki) : greedy_before(vi, ki, vl, kl)) {
+                        sv[i] = vl; sv[l] = vi; sk[i] = kl; sk[l] = ki;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    if (wv != 0) return;
+    Peak* out = a.peaks + (size_t)blockIdx.x * a.cap;
+    int cnt = 0;
+    for (int base = 0; base < K && cnt < a.cap; base += 64) {
+        const int i = base + lane;
+        const bool valid = i < K;
+        const uint32_t pk = valid ? (uint32_t)sk[i] : 0u;
+        const int x = pk & 0xffff, y = pk >> 16;
+        const float v = valid ? sv[i] : -INFINITY;
+        bool covered = !valid;
+        if (valid) {
+            const int c = (y / th) * cxn + x / tw;
+            const int nc = ccnt[c];
+            if (nc <= kCellIds) {
+                for (int r = 0; r < nc; ++r) {
+                    const int id = cids[c * kCellIds + r];
+                    const int qx = accx[id], qy = accy[id];
+                    covered |= x >= qx && x < qx + rw && y >= qy && y < qy + rh;
+                }
+            } else {
+                for (int id = 0; id < cnt; ++id) {
+                    const int qx = accx[id], qy = accy[id];
+                    covered |= x >= qx && x < qx + rw && y >= qy && y < qy + rh;
+                }
+            }
+        }
+        uint64_t fre = __ballot(!covered);
+        while (fre && cnt < a.cap) {
+            const int l = __builtin_ctzll(fre);
+            const int tx = __builtin_amdgcn_readlane(x, l), ty = __builtin_amdgcn_readlane(y, l);
+            const float tv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+            const int sx = (int)(tx - tw * (1 - ov)), sy = (int)(ty - th * (1 - ov));
+            if (lane == 0) {
+                out[cnt].x = tx; out[cnt].y = ty; out[cnt].score = tv;
+                accx[cnt] = sx; accy[cnt] = sy;
+            }
+            // register the rectangle in the <= 3 x 3 cells it covers (lanes 0-8)
+            const int cx0 = max(sx, 0) / tw, cx1 = min(sx + rw - 1, mw - 1) / tw;
+            const int cy0 = max(sy, 0) / th, cy1 = min(sy + rh - 1, mh - 1) / th;
+            if (lane < 9) {
+                const int cx = cx0 + lane % 3, cy = cy0 + lane / 3;
+                if (cx <= cx1 && cy <= cy1 && sx + rw > 0 && sy + rh > 0) {
+                    const int c = cy * cxn + cx;
+                    const int nc = ccnt[c];
+                    if (nc < kCellIds) cids[c * kCellIds + nc] = (uint8_t)cnt;
+                    ccnt[c] = (uint8_t)(nc < 255 ? nc + 1 : 255);
+                }
+            }
+            ++cnt;
+            // this chunk's later candidates: covered by the new rectangle?
+            const bool hit = lane > l && x >= sx && x < sx + rw && y >= sy && y < sy + rh;
+            fre &= ~__ballot(hit);
+            fre &= fre - 1;   // lane l taken
+        }
+    }
+    if (lane == 0) {
+        a.counts[blockIdx.x] = cnt;
+        a.cand_cnt[blockIdx.x] = -1;   // taken by this form: k_nms_fast skips the map
+    }
+}
+
+static size_t nms_greedy_lds(int cells) {
+    return (size_t)12 * kGreedyMax + (size_t)cells * (1 + kCellIds) + 16 + 8 * 256;
+}
+
+// LDS bytes of k_nms_fast for a block capacity, peak capacity and candidate capacity
+static size_t nms_fast_lds(int blocks, int /*cap*/, int cands) {
+    return (size_t)12 * blocks + 4 + (size_t)8 * ((blocks >> 6) + 1) + (size_t)8 * cands;
+}
+
+constexpr int kNmsLdsBlocksMax = 12 * 1024;   // block maxima kept in LDS up to this many blocks
+constexpr int kNmsLdsBytes = 160 * 1024 - 4096;   // k_nms_fast dynamic LDS budget (statics take the rest)
+
+void launch_nms(const NmsArgs& a0, int njobs, int max_blocks, int max_map_dim, hipStream_t st) {
     if (njobs <= 0) return;
+    NmsArgs a = a0;
+    if (a.by_block && max_blocks > 0) {
+        hipLaunchKernelGGL(k_nms_blocks, dim3((max_blocks + 3) / 4 < 1024 ? (max_blocks + 3) / 4 : 1024, njobs),
+                           dim3(256), 0, st, a);
+        const size_t fixed = nms_fast_lds(max_blocks, a.cap, 0);
+        if (max_blocks <= kNmsLdsBlocksMax && a.cap <= 256 && a.overlap >= 0.0 && max_map_dim < 65536 &&
+            fixed <= (size_t)kNmsLdsBytes) {
+            a.lds_blocks = max_blocks;
+            const long room = ((long)kNmsLdsBytes - (long)fixed) / 8;
+            a.cand_lds = a.cand ? (int)(room < kNmsCandCap ? room : kNmsCandCap) : 0;
+            const size_t lds = nms_fast_lds(max_blocks, a.cap, a.cand_lds);
+            static bool attr = false;
+            if (!attr) {
+                (void)hipFuncSetAttribute((const void*)k_nms_fast, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          kNmsLdsBytes);
+                (void)hipFuncSetAttribute((const void*)k_nms_greedy, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          kNmsLdsBytes);
+                attr = true;
+            }
+            // cells of template size cover the map: (ceil(mw / tw) * ceil(mh / th)) <= max_blocks + ncol + nrow + 1
+            const int cells = max_blocks + max_map_dim / (a.tw > 0 ? a.tw : 1) + max_map_dim / (a.th > 0 ? a.th : 1) + 2;
+            if (a.cand && !a.stamps && nms_greedy_lds(cells) <= (size_t)kNmsLdsBytes) {
+                NmsArgs gA = a;
+                gA.lds_blocks = cells;
+                hipLaunchKernelGGL(k_nms_greedy, dim3(njobs), dim3(256), nms_greedy_lds(cells), st, gA);
+            }
+            hipLaunchKernelGGL(k_nms_fast, dim3(njobs), dim3(256), lds, st, a);
+            return;
+        }
+    }
+    a.lds_blocks = 0;
     hipLaunchKernelGGL(k_nms, dim3(njobs), dim3(256), 0, st, a);
 }
 

@@ -1,0 +1,72 @@
+"""Timing of the BASELINE configs other than the headline one (bench.py measures configs[1], Src7, batched):
+per config the device-resident ms per search on one GPU (sources staged in HBM, median over repeated passes of
+the staged batch) next to one oracle search on the host (the CPU restatement, one thread), plus the result
+count of each.  Writes one JSON line per config.  usage: python scripts/bench_configs.py [reps] [--no-cpu] [--only=K ...]"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fastest_image_pattern_matching_amd import TemplateMatcher, synth  # noqa: E402
+from tests import oracle  # noqa: E402  (timed CPU baseline only)
+
+REPS = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 10
+CPU = "--no-cpu" not in sys.argv
+ONLY = [int(a.split("=")[1]) for a in sys.argv if a.startswith("--only=")]   # config positions to run
+
+
+def configs():
+    T = synth.load_templates()
+    s10, t10 = synth.src10_scene(T["Dst10"])
+    yield ("configs[2] Src10 3648x3648 / Dst10 54x54, Tol 0, TargetNum 100 (s_BlockMax)", [s10], t10,
+           dict(max_pos=100, score=0.7, tolerance_angle=0.0))
+    yield ("configs[2] stress: Src10 3648x3648, +-180 deg, TargetNum 100", [s10], t10,
+           dict(max_pos=100, score=0.7, tolerance_angle=180.0))
+    srcs, t = synth.batch_sources(8)
+    yield ("configs[3] 8 x 4096x4096 / 512x512 crop, +-180 deg (reference step), TargetNum 1", srcs, t,
+           dict(max_pos=1, tolerance_angle=180.0))
+    srcs5, t5 = synth.src5_set(T["Dst5"])
+    yield ("configs[4] Src5 rotation set 8 x 640x480 / Dst5 160x159, +-180 deg, sub-pixel", srcs5, t5,
+           dict(max_pos=1, tolerance_angle=180.0, subpixel=1))
+    s7, t7 = synth.src7_scene(T["Dst7"])
+    yield ("configs[1] single Src7 source (latency view of the headline config)", [s7], t7,
+           dict(max_pos=3, tolerance_angle=180.0, score=0.7, min_reduce_area=256, max_overlap=0.0, use_simd=1))
+
+
+def main():
+    for pos, (name, srcs, t, prm) in enumerate(configs()):
+        if ONLY and pos not in ONLY:
+            continue
+        m = TemplateMatcher(0)
+        for k, v in prm.items():
+            setattr(m._params, k, v)
+        assert m.learnPattern(t)
+        m.stage(srcs)
+        cnt, _ = m.match_staged_array()          # warm: plan + graph
+        ts = []
+        for _ in range(REPS):
+            t0 = time.perf_counter()
+            m.match_staged_array()
+            ts.append(time.perf_counter() - t0)
+        ms = float(np.median(ts)) * 1e3
+        out = {"config": name, "sources": len(srcs), "gpu_ms_per_pass": round(ms, 3),
+               "gpu_ms_per_search": round(ms / len(srcs), 3), "gpu_searches_per_s": round(1e3 * len(srcs) / ms, 1),
+               "matches": [int(x) for x in cnt]}
+        if CPU:
+            o = oracle.OracleMatcher().set(**prm)
+            o.learnPattern(t)
+            t0 = time.perf_counter()
+            r = o.match(srcs[0])
+            cpu = time.perf_counter() - t0
+            out.update({"cpu_oracle_ms_per_search": round(cpu * 1e3, 1), "cpu_matches_src0": len(r),
+                        "gpu_vs_cpu": round(cpu * 1e3 / (ms / len(srcs)), 1)})
+            assert len(r) == int(cnt[0]), (name, len(r), int(cnt[0]))
+        print(json.dumps(out), flush=True)
+        del m
+
+
+if __name__ == "__main__":
+    main()

@@ -197,6 +197,17 @@ def test_config2_src10_blockmax(hip, templates):
     assert len(orc) >= 100
 
 
+def test_blockmax_overlap(hip, templates):
+    """s_BlockMax mode (map / template area > 500, MaxPos > 10) with MaxOverlap 0.4: painted rectangles smaller
+    than two template sizes, so peaks sit close together and rectangles straddle block borders and strips."""
+    s, t = synth.src10_scene(templates["Dst10"])
+    crop = np.ascontiguousarray(s[:1824, :1830])
+    for ov, n in ((0.4, 60), (0.8, 40)):
+        gpu, orc, ostats, gstats = _run_both(hip, crop, t, max_pos=n, score=0.5, tolerance_angle=0.0, max_overlap=ov)
+        assert gstats == ostats
+        assert_same_results(gpu, orc, f"blockmax_ov{ov}")
+
+
 def test_config2_src10_rotation_sweep(hip, templates):
     """configs[2] stress (+-180 deg, 47 top angles, TargetNum 100) on the 1824x1824 top-left quarter."""
     s, t = synth.src10_scene(templates["Dst10"])
