@@ -559,7 +559,7 @@ int enqueue_search(fpm_ctx* ctx) {
         if (ncc_tile_fits(tt.w, tt.h)) {
             int mw = 0, mh = 0;
             for (int a = 0; a < P.nang; ++a) { mw = std::max(mw, P.map_w[a]); mh = std::max(mh, P.map_h[a]); }
-            launch_ncc_tile(P.d_jobs.as<NccJob>(P.off_ncc), J, mw, mh, st);
+            launch_ncc_tile(P.d_jobs.as<NccJob>(P.off_ncc), J, mw, mh, tt.w, tt.h, st);
         } else {
             launch_ncc_map(P.d_jobs.as<NccJob>(P.off_ncc), J, P.max_map, tt.w * tt.h, st);
         }
@@ -691,7 +691,16 @@ int enqueue_search(fpm_ctx* ctx) {
 
 // host finish for source s (TemplateMatcher.cpp:214-432)
 // pos[id] = index of candidate id in the layer-0 live list (k_pack's compact states / records), -1 if absent
+#ifdef FPM_HOST_TIMING   // diagnostic build only: per-stage host finish times to stderr
+#define HT(k) const auto ht_##k = std::chrono::steady_clock::now()
+#define HT_PRINT(a, b, name) \
+    fprintf(stderr, "host %-10s %8.3f ms\n", name, std::chrono::duration<double, std::milli>(ht_##b - ht_##a).count())
+#else
+#define HT(k)
+#define HT_PRINT(a, b, name)
+#endif
 void finish_source(fpm_ctx* ctx, int s, std::vector<fpm_result>& out, const std::vector<int>& pos) {
+    HT(0);
     Plan& P = ctx->plan;
     const int L = P.L;
     const char* h = P.h_out.as<char>();
@@ -711,8 +720,11 @@ void finish_source(fpm_ctx* ctx, int s, std::vector<fpm_result>& out, const std:
         for (int r = 0; r < counts[job]; ++r) order.push_back({(double)peaks[job * P.cap + r].score, job * P.cap + r, a});
     }
     std::sort(order.begin(), order.end(), [](const Key& l, const Key& r) { return l.score > r.score; });
+    HT(1);
     std::vector<HostMatch> all;
     const TmplLevel& t0 = ctx->tmpl[0];
+    std::vector<HostMatch> nm(P.n3);   // one candidate's n3 angle results, reused
+    const double astep = std::atan(2.0 / std::max(t0.w, t0.h)) * kR2D;   // layer 0's angle step (:283)
     for (const Key& k : order) {
         const int id = k.id;
         if (L == 0) {   // iTopLayer <= iStopLayer (:272-276)
@@ -732,9 +744,7 @@ void finish_source(fpm_ctx* ctx, int s, std::vector<fpm_result>& out, const std:
         const CandState& cs = state[li];
         // layer 0 (:282-358) from the device's ROI records
         const int d = L - 1;
-        const double astep = std::atan(2.0 / std::max(t0.w, t0.h)) * kR2D;
         const SrcLevel& lv = ctx->src[0];
-        std::vector<HostMatch> nm(P.n3);
         int imax = 0;
         double big = -1;
         for (int j = 0; j < P.n3; ++j) {
@@ -767,7 +777,9 @@ void finish_source(fpm_ctx* ctx, int s, std::vector<fpm_result>& out, const std:
         nm[imax].ptx = p.x; nm[imax].pty = p.y;
         all.push_back(nm[imax]);
     }
+    HT(2);
     filter_with_score(all, ctx->prm.score);
+    HT(3);
     const int dstW = t0.w, dstH = t0.h;
     for (HostMatch& m : all) {   // :380-390
         const double rad = -m.angle * kD2R;
@@ -777,7 +789,16 @@ void finish_source(fpm_ctx* ctx, int s, std::vector<fpm_result>& out, const std:
         m.rect = rrect_from3(lt, rt, rb);
         m.del = false;
     }
+    HT(4);
     filter_with_rotated_rect(all, ctx->prm.max_overlap);
+    HT(5);
+    HT_PRINT(0, 1, "sort");
+    HT_PRINT(1, 2, "collect");
+    HT_PRINT(2, 3, "score");
+    HT_PRINT(4, 5, "rotrect");
+#ifdef FPM_HOST_TIMING
+    fprintf(stderr, "host n=%zu order=%zu\n", all.size(), order.size());
+#endif
     std::sort(all.begin(), all.end(), score_big2small);
     out.clear();
     for (const HostMatch& m : all) {   // :406-432
@@ -1246,7 +1267,7 @@ int fpm_op_ncc_map(fpm_ctx* ctx, const uint8_t* src, int32_t w, int32_t h, size_
     j.mean = t.mean; j.norm = t.norm; j.inv_area = t.inv_area;
     HIP_TRY(hipMemcpyAsync(ctx->d_op_job.p, &j, sizeof(j), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpy2DAsync(ctx->d_op_a.p, sp, src, ss, w, h, hipMemcpyHostToDevice, ctx->stream));
-    if (ncc_tile_fits(t.w, t.h)) launch_ncc_tile(ctx->d_op_job.as<NccJob>(), 1, ow, oh, ctx->stream);
+    if (ncc_tile_fits(t.w, t.h)) launch_ncc_tile(ctx->d_op_job.as<NccJob>(), 1, ow, oh, t.w, t.h, ctx->stream);
     else launch_ncc_map(ctx->d_op_job.as<NccJob>(), 1, ow * oh, t.w * t.h, ctx->stream);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(out, ctx->d_op_b.p, sizeof(float) * (size_t)ow * oh, hipMemcpyDeviceToHost, ctx->stream));

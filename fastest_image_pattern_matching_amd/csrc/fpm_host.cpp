@@ -40,11 +40,19 @@ static void rrect_corners(const RRect& r, F2 pt[4]) {
 }
 
 // returns 0 = INTERSECT_NONE, 1 = INTERSECT_PARTIAL, 2 = INTERSECT_FULL
+// the same on precomputed corners (rrect_corners of ra / rb)
+static int rrect_intersection_c(const RRect& ra, const RRect& rb, const F2* A, const F2* B, std::vector<F2>& pts);
+
 int rrect_intersection(const RRect& ra, const RRect& rb, std::vector<F2>& pts) {
-    pts.clear();
-    F2 A[4], B[4], eA[4], eB[4];
+    F2 A[4], B[4];
     rrect_corners(ra, A);
     rrect_corners(rb, B);
+    return rrect_intersection_c(ra, rb, A, B, pts);
+}
+
+static int rrect_intersection_c(const RRect& ra, const RRect& rb, const F2* A, const F2* B, std::vector<F2>& pts) {
+    pts.clear();
+    F2 eA[4], eB[4];
     float eps = 1e-6f * std::max(ra.w * ra.h, rb.w * rb.h);
     bool coincident = true;
     for (int i = 0; i < 4 && coincident; ++i)
@@ -96,9 +104,11 @@ int rrect_intersection(const RRect& ra, const RRect& rb, std::vector<F2>& pts) {
     int n = (int)pts.size();
     if (n == 0) return 0;
     // drop near-duplicates (swap-with-last), remembering pairwise distances for the > 8 pass
+    // (n <= 16 edge crossings + 8 corners)
     const int stride = n;
-    std::vector<float> dist((size_t)n * n, 0.f);
-    std::vector<int> slot(n);
+    float dist[24 * 24];
+    int slot[24];
+    for (int i = 0; i < n * n; ++i) dist[i] = 0.f;
     for (int i = 0; i < n; ++i) {
         slot[i] = i;
         const F2 p = pts[i];
@@ -119,7 +129,7 @@ int rrect_intersection(const RRect& ra, const RRect& rb, std::vector<F2>& pts) {
         int bj = 1;
         float bd = dist[1];
         for (int i = 0; i < n - 1; ++i) {
-            const float* row = dist.data() + (size_t)stride * slot[i];
+            const float* row = dist + (size_t)stride * slot[i];
             for (int j = i + 1; j < n; ++j)
                 if (row[slot[j]] < bd) { bd = row[slot[j]]; bj = j; }
         }
@@ -136,7 +146,7 @@ void sort_pt_with_center(std::vector<F2>& pts) {
     for (const F2& p : pts) { ctr.x += p.x; ctr.y += p.y; }
     ctr.x = ctr.x / n;
     ctr.y = ctr.y / n;
-    std::vector<std::pair<F2, double>> keyed(n);
+    std::pair<F2, double> keyed[24];   // n <= 24 (rrect_intersection)
     for (int i = 0; i < n; ++i) {
         const F2 d = f2(pts[i].x - ctr.x, pts[i].y - ctr.y);
         const float nn = d.x * d.x + d.y * d.y;   // (squared norm: reference behaviour)
@@ -146,7 +156,7 @@ void sort_pt_with_center(std::vector<F2>& pts) {
         else key = (d.x - ctr.x > 0) ? 0 : 180;
         keyed[i] = std::make_pair(pts[i], key);
     }
-    std::sort(keyed.begin(), keyed.end(),
+    std::sort(keyed, keyed + n,
               [](const std::pair<F2, double> l, const std::pair<F2, double> r) { return l.second < r.second; });
     for (int i = 0; i < n; ++i) pts[i] = keyed[i].first;
 }
@@ -164,9 +174,18 @@ double contour_area(const std::vector<F2>& pts) {
 }
 
 void filter_with_score(std::vector<HostMatch>& v, double score) {
-    std::sort(v.begin(), v.end(), score_big2small);
-    for (size_t i = 0; i < v.size(); ++i)
-        if (v[i].score < score) { v.erase(v.begin() + (long)i, v.end()); return; }
+    // std::sort's permutation depends only on the comparison results, so sorting light (score, index) keys with
+    // the same comparator reproduces the reference's order of equal scores; the heavy records move once
+    struct K { double score; int i; };
+    std::vector<K> k(v.size());
+    for (size_t i = 0; i < v.size(); ++i) k[i] = {v[i].score, (int)i};
+    std::sort(k.begin(), k.end(), [](const K& a, const K& b) { return a.score > b.score; });
+    size_t n = 0;
+    while (n < k.size() && !(k[n].score < score)) ++n;
+    std::vector<HostMatch> out;
+    out.reserve(n);
+    for (size_t i = 0; i < n; ++i) out.push_back(v[k[i].i]);
+    v.swap(out);
 }
 
 void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
@@ -177,8 +196,9 @@ void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
     // so rrect_intersection would return INTERSECT_NONE; skipping them keeps the reference's O(n^2) loop order
     // and deletions exactly while avoiding the exact test for far-apart detections
     std::vector<float> box((size_t)4 * n);
+    std::vector<F2> corners((size_t)4 * n);
     for (int i = 0; i < n; ++i) {
-        F2 c[4];
+        F2* c = &corners[(size_t)4 * i];
         rrect_corners(v[i].rect, c);
         float x0 = c[0].x, x1 = c[0].x, y0 = c[0].y, y1 = c[0].y;
         for (int k = 1; k < 4; ++k) {
@@ -187,23 +207,58 @@ void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
         }
         box[4 * i] = x0 - 1.f; box[4 * i + 1] = y0 - 1.f; box[4 * i + 2] = x1 + 1.f; box[4 * i + 3] = y1 + 1.f;
     }
-    for (int i = 0; i + 1 < n; ++i) {
-        if (v[i].del) continue;
+    auto pair = [&](int i, int j) {   // the reference's inner-loop body for (i, j), boxes overlapping
+        const int kind = rrect_intersection_c(v[i].rect, v[j].rect, &corners[(size_t)4 * i], &corners[(size_t)4 * j], pts);
+        if (kind == 0) return;
+        bool drop = kind == 2;
+        if (kind == 1) {
+            if (pts.size() < 3) return;
+            sort_pt_with_center(pts);
+            const double ratio = contour_area(pts) / (v[i].rect.w * v[i].rect.h);
+            drop = ratio > max_overlap;
+        }
+        if (drop) v[(v[i].score >= v[j].score) ? j : i].del = true;
+    };
+    auto overlap = [&](int i, int j) {
         const float* bi = &box[4 * i];
-        for (int j = i + 1; j < n; ++j) {
-            if (v[j].del) continue;
-            const float* bj = &box[4 * j];
-            if (bj[0] > bi[2] || bj[2] < bi[0] || bj[1] > bi[3] || bj[3] < bi[1]) continue;
-            const int kind = rrect_intersection(v[i].rect, v[j].rect, pts);
-            if (kind == 0) continue;
-            bool drop = kind == 2;
-            if (kind == 1) {
-                if (pts.size() < 3) continue;
-                sort_pt_with_center(pts);
-                const double ratio = contour_area(pts) / (v[i].rect.w * v[i].rect.h);
-                drop = ratio > max_overlap;
-            }
-            if (drop) v[(v[i].score >= v[j].score) ? j : i].del = true;
+        const float* bj = &box[4 * j];
+        return !(bj[0] > bi[2] || bj[2] < bi[0] || bj[1] > bi[3] || bj[3] < bi[1]);
+    };
+    if (n <= 64) {
+        for (int i = 0; i + 1 < n; ++i) {
+            if (v[i].del) continue;
+            for (int j = i + 1; j < n; ++j)
+                if (!v[j].del && overlap(i, j)) pair(i, j);
+        }
+    } else {
+        // uniform grid over the boxes (cell = the largest box extent): for each i only the j > i whose boxes
+        // overlap its box, in ascending order -- the same (i, j) sequence as the full loop minus no-op pairs
+        float gx0 = box[0], gy0 = box[1], gx1 = box[2], gy1 = box[3], cs = 1.f;
+        for (int i = 0; i < n; ++i) {
+            gx0 = std::min(gx0, box[4 * i]); gy0 = std::min(gy0, box[4 * i + 1]);
+            gx1 = std::max(gx1, box[4 * i + 2]); gy1 = std::max(gy1, box[4 * i + 3]);
+            cs = std::max(cs, std::max(box[4 * i + 2] - box[4 * i], box[4 * i + 3] - box[4 * i + 1]));
+        }
+        const int gnx = std::min(1024, (int)((gx1 - gx0) / cs) + 1), gny = std::min(1024, (int)((gy1 - gy0) / cs) + 1);
+        const float sx = gnx / std::max(gx1 - gx0, 1e-3f), sy = gny / std::max(gy1 - gy0, 1e-3f);
+        auto cell = [&](float x, float s_, float o, int nmax) { return std::min(nmax - 1, std::max(0, (int)((x - o) * s_))); };
+        std::vector<std::vector<int>> grid((size_t)gnx * gny);
+        for (int i = 0; i < n; ++i)
+            for (int cy = cell(box[4 * i + 1], sy, gy0, gny); cy <= cell(box[4 * i + 3], sy, gy0, gny); ++cy)
+                for (int cx = cell(box[4 * i], sx, gx0, gnx); cx <= cell(box[4 * i + 2], sx, gx0, gnx); ++cx)
+                    grid[(size_t)cy * gnx + cx].push_back(i);
+        std::vector<int> nb;
+        for (int i = 0; i + 1 < n; ++i) {
+            if (v[i].del) continue;
+            nb.clear();
+            for (int cy = cell(box[4 * i + 1], sy, gy0, gny); cy <= cell(box[4 * i + 3], sy, gy0, gny); ++cy)
+                for (int cx = cell(box[4 * i], sx, gx0, gnx); cx <= cell(box[4 * i + 2], sx, gx0, gnx); ++cx)
+                    for (int j : grid[(size_t)cy * gnx + cx])
+                        if (j > i) nb.push_back(j);
+            std::sort(nb.begin(), nb.end());
+            nb.erase(std::unique(nb.begin(), nb.end()), nb.end());
+            for (int j : nb)
+                if (!v[j].del && overlap(i, j)) pair(i, j);
         }
     }
     v.erase(std::remove_if(v.begin(), v.end(), [](const HostMatch& m) { return m.del; }), v.end());

@@ -155,7 +155,7 @@ void launch_pyr_down(const uint8_t* src, int sw, int sh, int sp, size_t s_img, u
 void launch_warp(const WarpJob* jobs, int njobs, int max_pixels, hipStream_t st);
 void launch_ncc_map(const NccJob* jobs, int njobs, int max_out, int tmpl_bytes, hipStream_t st);
 bool ncc_tile_fits(int tw, int th);   // LDS-tiled variant applies (templates up to 128 x 64)
-void launch_ncc_tile(const NccJob* jobs, int njobs, int max_ow, int max_oh, hipStream_t st);
+void launch_ncc_tile(const NccJob* jobs, int njobs, int max_ow, int max_oh, int tw, int th, hipStream_t st);
 constexpr int kNmsCandCap = 8192;   // s_BlockMax candidates (pixels >= the top-layer score) kept per map
 // max_blocks: s_BlockMax blocks of the largest map (block mode); max_map_dim: largest map width or height
 void launch_nms(const NmsArgs& a, int njobs, int max_blocks, int max_map_dim, hipStream_t st);

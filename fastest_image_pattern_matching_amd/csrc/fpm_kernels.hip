@@ -257,25 +257,34 @@ __global__ __launch_bounds__(256) void k_ncc_map(const NccJob* __restrict__ jobs
 
 // LDS-tiled NCC for small templates (the top layer: area <= MinReduceArea by construction).  A 256-thread
 // workgroup computes a 64 x 16 tile of one map; its canvas window ((16 + th - 1) rows x (64 + 4*ntw + 4) bytes)
-// and the template (rows of ntw words, zero beyond tw) are staged in LDS.  A thread owns 4 adjacent outputs of
-// one row: per template word it funnel-shifts two canvas words into the 4 byte alignments and accumulates the
-// correlation (v_dot4_u32_u8 with the template word), the window sum (with a 0x01 mask word) and the window sum of
-// squares (masked word with itself).  Exact u32 row sums, then the same f32 fold / TM_CCORR rounding and f64
-// normalisation as k_ncc_map.
+// and the template (rows of ntw words, zero beyond tw) are staged in LDS.  The window sums of I and I^2 depend on
+// the canvas row and the output column only, so they are formed once per staged row (h1 / h2: sums over the
+// template width, v_dot4_u32_u8 with a byte mask) and summed over th rows per output.  A thread owns 4 adjacent
+// outputs of one row: per template word it funnel-shifts two canvas words into the 4 byte alignments and
+// accumulates the correlation with one v_dot4_u32_u8 each.  Exact u32 row sums, then the same f32 fold /
+// TM_CCORR rounding and f64 normalisation as k_ncc_map.  Dynamic LDS: ncc_tile_lds(tw, th).
 constexpr int NT_W = 64, NT_H = 16;
 constexpr int NT_MAXW = 32;                 // template words per row (tw <= 128)
 constexpr int NT_MAXH = 64;                 // template rows
 
+static size_t ncc_tile_lds(int tw, int th) {
+    const int ntw = (tw + 3) >> 2, iwq = NT_W / 4 + ntw + 1, irows = NT_H + th - 1;
+    return (size_t)4 * (th * ntw + ntw + irows * iwq) + (size_t)8 * irows * NT_W;
+}
+
 __global__ __launch_bounds__(256) void k_ncc_tile(const NccJob* __restrict__ jobs, int tiles_x) {
-    __shared__ uint32_t Tw[NT_MAXH * NT_MAXW];
-    __shared__ uint32_t Mw[NT_MAXW];
-    __shared__ uint32_t Iw[(NT_H + NT_MAXH) * (NT_W / 4 + NT_MAXW + 2)];
+    extern __shared__ __attribute__((aligned(16))) uint32_t nt_lds[];
     const NccJob& j = jobs[blockIdx.y];
     const int tx0 = (blockIdx.x % tiles_x) * NT_W, ty0 = (blockIdx.x / tiles_x) * NT_H;
     if (tx0 >= j.ow || ty0 >= j.oh) return;   // uniform: this map has fewer tiles
     const int tw = j.tw, th = j.th, ntw = (tw + 3) >> 2;
     const int iwq = NT_W / 4 + ntw + 1;        // canvas words per staged row
     const int irows = NT_H + th - 1;
+    uint32_t* H1 = nt_lds;                     // [irows][64] window row sums of I (16-byte aligned: first)
+    uint32_t* H2 = H1 + irows * NT_W;          // [irows][64] of I^2
+    uint32_t* Tw = H2 + irows * NT_W;          // [th][ntw]
+    uint32_t* Mw = Tw + th * ntw;              // [ntw] byte masks of the template width
+    uint32_t* Iw = Mw + ntw;                   // [irows][iwq]
     const int tid = threadIdx.x;
     for (int i = tid; i < th * ntw; i += 256) {
         const int r = i / ntw, k = i - r * ntw;
@@ -305,6 +314,28 @@ __global__ __launch_bounds__(256) void k_ncc_tile(const NccJob* __restrict__ job
         }
         return;
     }
+    // window row sums: item (staged row r, 4 output columns q)
+    for (int it = tid; it < irows * (NT_W / 4); it += 256) {
+        const int r = it >> 4, q = it & 15;
+        const uint32_t* ir = Iw + r * iwq + q;
+        uint32_t s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+        uint32_t w0 = ir[0];
+        for (int k = 0; k < ntw; ++k) {
+            const uint32_t w1 = ir[k + 1];
+            const uint32_t m = Mw[k], mff = m * 0xffu;
+            const uint32_t sh[4] = {w0, __builtin_amdgcn_alignbyte(w1, w0, 1), __builtin_amdgcn_alignbyte(w1, w0, 2),
+                                    __builtin_amdgcn_alignbyte(w1, w0, 3)};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                s1[u] = __builtin_amdgcn_udot4(m, sh[u], s1[u], false);
+                s2[u] = __builtin_amdgcn_udot4(sh[u] & mff, sh[u], s2[u], false);
+            }
+            w0 = w1;
+        }
+        *(uint4*)(H1 + r * NT_W + 4 * q) = make_uint4(s1[0], s1[1], s1[2], s1[3]);
+        *(uint4*)(H2 + r * NT_W + 4 * q) = make_uint4(s2[0], s2[1], s2[2], s2[3]);
+    }
+    __syncthreads();
     const int ly = tid >> 4, lx = (tid & 15) * 4;   // outputs (tx0 + lx .. +3, ty0 + ly)
     float accF[4] = {0.f, 0.f, 0.f, 0.f};
     uint64_t accI[4] = {0, 0, 0, 0};
@@ -316,18 +347,16 @@ __global__ __launch_bounds__(256) void k_ncc_tile(const NccJob* __restrict__ job
         uint32_t w0 = ir[0];
         for (int k = 0; k < ntw; ++k) {
             const uint32_t w1 = ir[k + 1];
-            const uint32_t t = tr[k], m = Mw[k];
-            const uint32_t mff = m * 0xffu;
-            const uint32_t sh[4] = {w0, __builtin_amdgcn_alignbyte(w1, w0, 1), __builtin_amdgcn_alignbyte(w1, w0, 2),
-                                    __builtin_amdgcn_alignbyte(w1, w0, 3)};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                d[q] = __builtin_amdgcn_udot4(t, sh[q], d[q], false);
-                sI[q] = __builtin_amdgcn_udot4(m, sh[q], sI[q], false);
-                sQ[q] = __builtin_amdgcn_udot4(sh[q] & mff, sh[q], sQ[q], false);
-            }
+            const uint32_t t = tr[k];
+            d[0] = __builtin_amdgcn_udot4(t, w0, d[0], false);
+            d[1] = __builtin_amdgcn_udot4(t, __builtin_amdgcn_alignbyte(w1, w0, 1), d[1], false);
+            d[2] = __builtin_amdgcn_udot4(t, __builtin_amdgcn_alignbyte(w1, w0, 2), d[2], false);
+            d[3] = __builtin_amdgcn_udot4(t, __builtin_amdgcn_alignbyte(w1, w0, 3), d[3], false);
             w0 = w1;
         }
+        const uint4 h1 = *(const uint4*)(H1 + (ly + r) * NT_W + lx), h2 = *(const uint4*)(H2 + (ly + r) * NT_W + lx);
+        sI[0] += h1.x; sI[1] += h1.y; sI[2] += h1.z; sI[3] += h1.w;
+        sQ[0] += h2.x; sQ[1] += h2.y; sQ[2] += h2.z; sQ[3] += h2.w;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             if (j.fold) accF[q] = accF[q] + (float)(int)d[q];   // TemplateMatcher.cpp:507
@@ -355,10 +384,17 @@ void launch_ncc_map(const NccJob* jobs, int njobs, int max_out, int tmpl_bytes, 
 
 bool ncc_tile_fits(int tw, int th) { return tw <= 4 * NT_MAXW && th <= NT_MAXH; }
 
-void launch_ncc_tile(const NccJob* jobs, int njobs, int max_ow, int max_oh, hipStream_t st) {
+void launch_ncc_tile(const NccJob* jobs, int njobs, int max_ow, int max_oh, int tw, int th, hipStream_t st) {
     if (njobs <= 0 || max_ow <= 0 || max_oh <= 0) return;
     const int tiles_x = (max_ow + NT_W - 1) / NT_W, tiles_y = (max_oh + NT_H - 1) / NT_H;
-    hipLaunchKernelGGL(k_ncc_tile, dim3(tiles_x * tiles_y, njobs), dim3(256), 0, st, jobs, tiles_x);
+    const size_t lds = ncc_tile_lds(tw, th);
+    static bool attr = false;
+    if (lds > 65536 && !attr) {
+        (void)hipFuncSetAttribute((const void*)k_ncc_tile, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)ncc_tile_lds(4 * NT_MAXW, NT_MAXH));
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_ncc_tile, dim3(tiles_x * tiles_y, njobs), dim3(256), lds, st, jobs, tiles_x);
 }
 
 // ============================================================================================== K5
@@ -1004,7 +1040,7 @@ void launch_nms(const NmsArgs& a0, int njobs, int max_blocks, int max_map_dim, h
     if (njobs <= 0) return;
     NmsArgs a = a0;
     if (a.by_block && max_blocks > 0) {
-        hipLaunchKernelGGL(k_nms_blocks, dim3((max_blocks + 3) / 4 < 1024 ? (max_blocks + 3) / 4 : 1024, njobs),
+        hipLaunchKernelGGL(k_nms_blocks, dim3((max_blocks + 3) / 4 < 16384 ? (max_blocks + 3) / 4 : 16384, njobs),
                            dim3(256), 0, st, a);
         const size_t fixed = nms_fast_lds(max_blocks, a.cap, 0);
         if (max_blocks <= kNmsLdsBlocksMax && a.cap <= 256 && a.overlap >= 0.0 && max_map_dim < 65536 &&

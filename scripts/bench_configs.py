@@ -52,7 +52,9 @@ def main():
             m.match_staged_array()
             ts.append(time.perf_counter() - t0)
         ms = float(np.median(ts)) * 1e3
+        dev_ms, host_ms, _ = m.profile_last()   # the last pass: device span and host post-processing
         out = {"config": name, "sources": len(srcs), "gpu_ms_per_pass": round(ms, 3),
+               "last_pass_device_ms": round(dev_ms, 3), "last_pass_host_ms": round(host_ms, 3),
                "gpu_ms_per_search": round(ms / len(srcs), 3), "gpu_searches_per_s": round(1e3 * len(srcs) / ms, 1),
                "matches": [int(x) for x in cnt]}
         if CPU:

@@ -208,6 +208,35 @@ def test_blockmax_overlap(hip, templates):
         assert_same_results(gpu, orc, f"blockmax_ov{ov}")
 
 
+def test_blockmax_ties_across_blocks(hip, templates):
+    """Identical windows at many sites (the template pasted at 4-aligned positions of a flat background, so the
+    top-layer windows are equal) give exactly equal scores in different s_BlockMax blocks: the peak order must
+    follow the block order (max_element's first block), then the row-major position inside the block."""
+    t = templates["Dst10"]
+    s = np.full((1824, 1824), 90, np.uint8)
+    for gy in range(9):
+        for gx in range(9):
+            synth.paste(s, t, 96 + 192 * gx, 96 + 192 * gy)
+    gpu, orc, ostats, gstats = _run_both(hip, s, t, max_pos=50, score=0.7, tolerance_angle=0.0)
+    assert gstats == ostats
+    assert_same_results(gpu, orc, "blockmax_ties")
+
+
+@pytest.mark.parametrize("prm", [dict(max_overlap=1.0), dict(score=0.05), dict(score=-0.5)],
+                         ids=["empty_rect", "many_candidates", "negative_score"])
+def test_blockmax_fallback_paths(hip, templates, prm):
+    """s_BlockMax peak extraction off the greedy form's path: an empty painted rectangle (MaxOverlap 1: the same
+    peak again, as the reference finds it), candidate lists too long for the sorted form, a threshold below the
+    painted value's reach."""
+    s, t = synth.src10_scene(templates["Dst10"])
+    crop = np.ascontiguousarray(s[:1824, :1824])
+    base = dict(max_pos=30, score=0.7, tolerance_angle=0.0)
+    base.update(prm)
+    gpu, orc, ostats, gstats = _run_both(hip, crop, t, **base)
+    assert gstats == ostats
+    assert_same_results(gpu, orc, f"blockmax_{prm}")
+
+
 def test_config2_src10_rotation_sweep(hip, templates):
     """configs[2] stress (+-180 deg, 47 top angles, TargetNum 100) on the 1824x1824 top-left quarter."""
     s, t = synth.src10_scene(templates["Dst10"])
