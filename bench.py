@@ -125,6 +125,33 @@ def cpu_baseline(templ, src, budget_s):
     return base, variants
 
 
+def kernel_pass(m, sources, steps, L):
+    """Kernel-level pass: one context over the whole batch, eager launches with HIP events around each kernel on the
+    library's stream (the kernels' own durations, not time shared with another context's stream).  Returns the
+    per-kernel table and the roofline object of the dominant kernel."""
+    m.stage(sources)
+    m.match_staged_array()
+    m.profile(True)
+    m.profile_reset()
+    for _ in range(steps):
+        m.match_staged_array()
+    m.profile(False)
+    kern = {}
+    for k, name in enumerate(L.KERNEL_NAMES):
+        ms, launches, b = m.profile_get(k)
+        if launches:
+            kern[name] = {"ms_total": ms, "launches": launches, "bytes": b}
+    dom = max(kern, key=lambda k: kern[k]["ms_total"])
+    d = kern[dom]
+    avg_s = d["ms_total"] / d["launches"] * 1e-3
+    bytes_per_launch = d["bytes"] / d["launches"]
+    achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
+    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic(dom), "kernel": dom,
+                "avg_launch_us": round(avg_s * 1e6, 3), "algorithmic_bytes_per_launch": int(bytes_per_launch)}
+    return kern, roofline
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -135,6 +162,10 @@ def main():
     ap.add_argument("--contexts", type=int, default=2, help="concurrent contexts (HIP streams) per GPU")
     ap.add_argument("--skip-latency", action="store_true",
                     help="skip the single-search latency probe (PMC runs: only batch dispatches)")
+    ap.add_argument("--kernel-pass-only", action="store_true",
+                    help="run only the per-kernel pass (one context, the whole batch, K eager steps) and print its "
+                         "kernel table + roofline: the command whose rocprofv3 --kernel-trace --stats averages are "
+                         "directly comparable to roofline.avg_launch_us")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -166,6 +197,11 @@ def main():
         setattr(m._params, k, v)
     assert m.learnPattern(templ)
     # single-search latency (host upload included) for the record, after one warm call builds the plan
+    if args.kernel_pass_only:
+        kern, roofline = kernel_pass(m, sources, args.steps, L)
+        print(json.dumps({"kernel_pass_only": True, "steps": args.steps, "sources_per_step": args.batch,
+                          "kernels": kern, "roofline": roofline}), flush=True)
+        return
     lat_e2e = None
     if not args.skip_latency:
         m.match(sources[0])
@@ -226,28 +262,7 @@ def main():
     else:
         n_matches = [len(r) for r in res]
 
-    # kernel-level pass: one context over the whole batch, eager launches with HIP events around each kernel (the
-    # kernels' own durations, not time shared with another context's stream)
-    m.stage(sources)
-    m.match_staged_array()
-    m.profile(True)
-    m.profile_reset()
-    for _ in range(args.steps):
-        m.match_staged_array()
-    m.profile(False)
-    kern = {}
-    for k, name in enumerate(L.KERNEL_NAMES):
-        ms, launches, b = m.profile_get(k)
-        if launches:
-            kern[name] = {"ms_total": ms, "launches": launches, "bytes": b}
-    dom = max(kern, key=lambda k: kern[k]["ms_total"])
-    d = kern[dom]
-    avg_s = d["ms_total"] / d["launches"] * 1e-3
-    bytes_per_launch = d["bytes"] / d["launches"]
-    achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
-    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic(dom), "kernel": dom,
-                "avg_launch_us": round(avg_s * 1e6, 3), "algorithmic_bytes_per_launch": int(bytes_per_launch)}
+    kern, roofline = kernel_pass(m, sources, args.steps, L)
 
     searches = world * args.batch * args.steps
     value = searches / elapsed

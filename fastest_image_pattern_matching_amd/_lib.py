@@ -57,6 +57,14 @@ class Result(C.Structure):
         "lt_x", "lt_y", "rt_x", "rt_y", "rb_x", "rb_y", "lb_x", "lb_y", "cx", "cy", "angle", "score")]
 
 
+class Candidate(C.Structure):
+    """fpm_candidate — one top-layer candidate (s_MatchParameter, DataStructures.h:58-94) and its refinement."""
+
+    _fields_ = [("top_score", C.c_double), ("x", C.c_double), ("y", C.c_double), ("score", C.c_double),
+                ("angle", C.c_double), ("angle_index", C.c_int32), ("peak_rank", C.c_int32), ("source", C.c_int32),
+                ("kept", C.c_int32)]
+
+
 # every symbol include/fpm.h declares, with (restype, argtypes)
 _P = C.c_void_p
 _U8P = C.POINTER(C.c_uint8)
@@ -86,6 +94,11 @@ SIGNATURES = {
     "fpm_template_level": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                      C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double),
                                      C.POINTER(C.c_int32), _U8P, C.c_size_t]),
+    "fpm_set_angle_shard": (C.c_int, [_P, C.c_int32, C.c_int32]),
+    "fpm_get_angle_shard": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "fpm_last_candidates": (C.c_int, [_P, C.c_int32, C.POINTER(Candidate), C.c_int32, C.POINTER(C.c_int32)]),
+    "fpm_merge_candidates": (C.c_int, [C.POINTER(Params), C.c_int32, C.c_int32, C.POINTER(Candidate), C.c_int32,
+                                       C.POINTER(Result), C.c_int32, C.POINTER(C.c_int32)]),
     "fpm_search_stats": (C.c_int, [_P, C.POINTER(C.c_int64), C.c_int32]),
     "fpm_profile_enable": (C.c_int, [_P, C.c_int32]),
     "fpm_profile_reset": (C.c_int, [_P]),

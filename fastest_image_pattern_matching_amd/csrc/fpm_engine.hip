@@ -85,6 +85,8 @@ struct Plan {
     int sw = 0, sh = 0, S = 0, L = 0;
     fpm_params prm{};
     int nang = 0, cap = 0, n3 = 1, C = 0;      // C = S * nang * cap candidate slots
+    int a0 = 0, nang_all = 0;                  // this plan's angles = [a0, a0 + nang) of the full top-layer list
+    int shard = 0, shards = 1;                 // angle shard the plan was built for (fpm_set_angle_shard)
     bool by_block = false;
     std::vector<double> angles, layer_score;
     std::vector<TopAngle> top;
@@ -139,6 +141,8 @@ struct fpm_ctx {
     uint64_t tmpl_gen = 0;
     // staged sources
     int S = 0, sw = 0, sh = 0, src_L = -1;
+    // angle shard (fpm_set_angle_shard): this context's slice of the top-layer angle list
+    int shard = 0, shards = 1;
     std::vector<SrcLevel> src;
     DevBuf d_src;
     // plan
@@ -161,6 +165,8 @@ struct fpm_ctx {
     double last_device_ms = 0, last_host_ms = 0, last_call_ms = 0;
     std::chrono::steady_clock::time_point t_call0;
     bool pending = false;    // a staged search is in flight (fpm_match_staged_launch)
+    // per-source candidate records of the last search (collect_candidates; fpm_match_*candidates)
+    std::vector<std::vector<fpm_candidate>> cands;
 };
 
 #define HIP_TRY(expr)                                                                   \
@@ -290,10 +296,11 @@ int build_plan(fpm_ctx* ctx) {
     Plan& P = ctx->plan;
     const int L = ctx->src_L;
     if (P.valid && ctx->plan_gen == ctx->tmpl_gen && P.sw == ctx->sw && P.sh == ctx->sh && P.S == ctx->S &&
-        P.L == L && same_search_params(P.prm, ctx->prm))
+        P.L == L && same_search_params(P.prm, ctx->prm) && P.shard == ctx->shard && P.shards == ctx->shards)
         return FPM_OK;
     P.valid = false;
     P.sw = ctx->sw; P.sh = ctx->sh; P.S = ctx->S; P.L = L; P.prm = ctx->prm;
+    P.shard = ctx->shard; P.shards = ctx->shards;
     const fpm_params& prm = ctx->prm;
     const TmplLevel& tt = ctx->tmpl[L];
     // angle list (TemplateMatcher.cpp:130-144)
@@ -305,6 +312,12 @@ int build_plan(fpm_ctx* ctx) {
         for (double a = 0; a < prm.tolerance_angle + step; a += step) P.angles.push_back(a);
         for (double a = -step; a > -prm.tolerance_angle - step; a -= step) P.angles.push_back(a);
     }
+    // angle shard: a contiguous block [a0, a1) of the reference's list, so the concatenation of the shards' candidate
+    // lists in shard order is the reference's push order (angle-major, TemplateMatcher.cpp:157-211)
+    P.nang_all = (int)P.angles.size();
+    P.a0 = (int)((int64_t)P.nang_all * P.shard / P.shards);
+    const int a1 = (int)((int64_t)P.nang_all * (P.shard + 1) / P.shards);
+    P.angles = std::vector<double>(P.angles.begin() + P.a0, P.angles.begin() + a1);
     P.nang = (int)P.angles.size();
     P.layer_score.assign(L + 1, prm.score);
     for (int l = 1; l <= L; ++l) P.layer_score[l] = P.layer_score[l - 1] * 0.9;
@@ -689,124 +702,130 @@ int enqueue_search(fpm_ctx* ctx) {
     return FPM_OK;
 }
 
-// host finish for source s (TemplateMatcher.cpp:214-432)
-// pos[id] = index of candidate id in the layer-0 live list (k_pack's compact states / records), -1 if absent
-#ifdef FPM_HOST_TIMING   // diagnostic build only: per-stage host finish times to stderr
-#define HT(k) const auto ht_##k = std::chrono::steady_clock::now()
-#define HT_PRINT(a, b, name) \
-    fprintf(stderr, "host %-10s %8.3f ms\n", name, std::chrono::duration<double, std::milli>(ht_##b - ht_##a).count())
-#else
-#define HT(k)
-#define HT_PRINT(a, b, name)
-#endif
-void finish_source(fpm_ctx* ctx, int s, std::vector<fpm_result>& out, const std::vector<int>& pos) {
-    HT(0);
+// Host half of the search, split at the one point where a search can be sharded by angle:
+//   collect_candidates: every top-layer candidate of source s in the reference's push order (angle-major, then
+//     peak order, TemplateMatcher.cpp:157-211) with its own refinement outcome (:262-371) — each candidate's
+//     descent is independent of every other candidate's, so a shard of the angle list yields exactly the
+//     records of its angles;
+//   merge_candidates: everything after that which couples candidates — the std::sort of the top list (:214),
+//     vecAllResult in sorted order, filterWithScore, filterWithRotatedRect, the final sort and the
+//     s_SingleTargetMatch conversion (:373-432).  It needs the complete push-order sequence, i.e. the shards'
+//     records concatenated in shard order.
+// pos[id] = index of candidate id in the layer-0 live list (k_pack's compact states / records), -1 if absent.
+void collect_candidates(fpm_ctx* ctx, int s, const std::vector<int>& pos, std::vector<fpm_candidate>& out) {
     Plan& P = ctx->plan;
     const int L = P.L;
+    out.clear();
+    if (P.nang == 0) return;
     const char* h = P.h_out.as<char>();
     const int32_t* counts = (const int32_t*)(h + P.h_counts);
     const Peak* peaks = (const Peak*)(h + P.h_peaks);
     const CandState* state = (const CandState*)(h + P.h_state);
     const RoiRecord* rec = (const RoiRecord*)(h + P.h_rec);
-    // std::sort(vecMatchParameter, compareScoreBig2Small) (:214) over the top candidates in the reference's
-    // insertion order (angle-major, then peak order).  The permutation std::sort produces depends only on the
-    // sequence of comparison results, so sorting light (score, id) keys with the same comparator reproduces the
-    // reference's order of equal scores exactly.
-    struct Key { double score; int id; int a; };
-    std::vector<Key> order;
-    order.reserve(64);
-    for (int a = 0; a < P.nang; ++a) {
-        const int job = s * P.nang + a;
-        for (int r = 0; r < counts[job]; ++r) order.push_back({(double)peaks[job * P.cap + r].score, job * P.cap + r, a});
-    }
-    std::sort(order.begin(), order.end(), [](const Key& l, const Key& r) { return l.score > r.score; });
-    HT(1);
-    std::vector<HostMatch> all;
     const TmplLevel& t0 = ctx->tmpl[0];
     std::vector<HostMatch> nm(P.n3);   // one candidate's n3 angle results, reused
     const double astep = std::atan(2.0 / std::max(t0.w, t0.h)) * kR2D;   // layer 0's angle step (:283)
-    for (const Key& k : order) {
-        const int id = k.id;
-        if (L == 0) {   // iTopLayer <= iStopLayer (:272-276)
+    const SrcLevel& lv = ctx->src[0];
+    const F2 sc = f2((lv.w - 1) / 2.0f, (lv.h - 1) / 2.0f);
+    for (int a = 0; a < P.nang; ++a) {
+        const int job = s * P.nang + a;
+        for (int r = 0; r < counts[job]; ++r) {
+            const int id = job * P.cap + r;
             const Peak& pk = peaks[id];
-            HostMatch c{};
-            const F2 pt = f2((float)pk.x - P.top[k.a].tx, (float)pk.y - P.top[k.a].ty);
-            c.score = pk.score;
-            c.angle = P.angles[k.a];
-            const double rad = -c.angle * kD2R;
-            const F2 lt = rotate_pt(f2(pt.x, pt.y), P.center, std::cos(rad), std::sin(rad));
-            c.ptx = lt.x; c.pty = lt.y;
-            all.push_back(c);
-            continue;
+            fpm_candidate c{};
+            c.top_score = (double)pk.score;
+            c.angle_index = P.a0 + a;
+            c.peak_rank = r;
+            c.source = s;
+            if (L == 0) {   // iTopLayer <= iStopLayer (:272-276)
+                const F2 pt = f2((float)pk.x - P.top[a].tx, (float)pk.y - P.top[a].ty);
+                const double rad = -P.angles[a] * kD2R;
+                const F2 lt = rotate_pt(f2(pt.x, pt.y), P.center, std::cos(rad), std::sin(rad));
+                c.x = lt.x; c.y = lt.y; c.score = pk.score; c.angle = P.angles[a]; c.kept = 1;
+                out.push_back(c);
+                continue;
+            }
+            const int li = pos[id];
+            if (li < 0) { out.push_back(c); continue; }   // broke out at a layer > 0 (:331-332)
+            const CandState& cs = state[li];
+            // layer 0 (:282-358) from the device's ROI records
+            const int d = L - 1;
+            int imax = 0;
+            double big = -1;
+            for (int j = 0; j < P.n3; ++j) {
+                const RoiRecord& rr = rec[(size_t)li * P.n3 + j];
+                HostMatch m{};
+                m.ptx = rr.mx; m.pty = rr.my;
+                m.score = rr.score;
+                m.angle = P.nodes[d][(size_t)cs.node * P.n3 + j].angle;
+                m.on_border = rr.on_border != 0;
+                for (int x = 0; x < 3; ++x)
+                    for (int y = 0; y < 3; ++y) m.vec[x][y] = rr.vec[x * 3 + y];
+                nm[j] = m;
+                if (nm[j].score > big) { imax = j; big = nm[j].score; }
+            }
+            if (nm[imax].score < P.layer_score[0]) { out.push_back(c); continue; }
+            if (ctx->prm.subpixel && !nm[imax].on_border && imax != 0 && imax != 2) {
+                double nx = 0, ny = 0, na = 0;
+                subpix_estimation(nm, &nx, &ny, &na, astep, imax);
+                nm[imax].ptx = nx; nm[imax].pty = ny;
+                nm[imax].angle = na;
+            }
+            const double nang = nm[imax].angle;
+            const double rad = nang * kD2R;
+            const F2 r0 = rotate_pt(f2(cs.lt.x * 2, cs.lt.y * 2), sc, std::cos(rad), std::sin(rad));
+            const F2 pad = f2(r0.x - 3, r0.y - 3);
+            F2 p = f2((float)(nm[imax].ptx + pad.x), (float)(nm[imax].pty + pad.y));
+            const double nrad = -nang * kD2R;
+            p = rotate_pt(p, sc, std::cos(nrad), std::sin(nrad));
+            c.x = p.x; c.y = p.y; c.score = nm[imax].score; c.angle = nang; c.kept = 1;
+            out.push_back(c);
         }
-        const int li = pos[id];
-        if (li < 0) continue;           // broke out at a layer > 0 (:331-332)
-        const CandState& cs = state[li];
-        // layer 0 (:282-358) from the device's ROI records
-        const int d = L - 1;
-        const SrcLevel& lv = ctx->src[0];
-        int imax = 0;
-        double big = -1;
-        for (int j = 0; j < P.n3; ++j) {
-            const RoiRecord& r = rec[(size_t)li * P.n3 + j];
-            HostMatch m{};
-            m.ptx = r.mx; m.pty = r.my;
-            m.score = r.score;
-            m.angle = P.nodes[d][(size_t)cs.node * P.n3 + j].angle;
-            m.on_border = r.on_border != 0;
-            for (int x = 0; x < 3; ++x)
-                for (int y = 0; y < 3; ++y) m.vec[x][y] = r.vec[x * 3 + y];
-            nm[j] = m;
-            if (nm[j].score > big) { imax = j; big = nm[j].score; }
-        }
-        if (nm[imax].score < P.layer_score[0]) continue;
-        if (ctx->prm.subpixel && !nm[imax].on_border && imax != 0 && imax != 2) {
-            double nx = 0, ny = 0, na = 0;
-            subpix_estimation(nm, &nx, &ny, &na, astep, imax);
-            nm[imax].ptx = nx; nm[imax].pty = ny;
-            nm[imax].angle = na;
-        }
-        const double nang = nm[imax].angle;
-        const F2 sc = f2((lv.w - 1) / 2.0f, (lv.h - 1) / 2.0f);
-        const double rad = nang * kD2R;
-        const F2 r0 = rotate_pt(f2(cs.lt.x * 2, cs.lt.y * 2), sc, std::cos(rad), std::sin(rad));
-        const F2 pad = f2(r0.x - 3, r0.y - 3);
-        F2 p = f2((float)(nm[imax].ptx + pad.x), (float)(nm[imax].pty + pad.y));
-        const double nrad = -nang * kD2R;
-        p = rotate_pt(p, sc, std::cos(nrad), std::sin(nrad));
-        nm[imax].ptx = p.x; nm[imax].pty = p.y;
-        all.push_back(nm[imax]);
     }
-    HT(2);
-    filter_with_score(all, ctx->prm.score);
-    HT(3);
-    const int dstW = t0.w, dstH = t0.h;
+}
+
+// Returns false when `cand` is not in push order (angle_index ascending, peak_rank 0, 1, ... within an angle).
+bool merge_candidates(const fpm_params& prm, int t0w, int t0h, const fpm_candidate* cand, int n,
+                      std::vector<fpm_result>& out) {
+    out.clear();
+    for (int i = 0; i < n; ++i) {
+        const bool first = i == 0 || cand[i].angle_index != cand[i - 1].angle_index;
+        if (first ? (cand[i].peak_rank != 0 || (i > 0 && cand[i].angle_index < cand[i - 1].angle_index))
+                  : cand[i].peak_rank != cand[i - 1].peak_rank + 1)
+            return false;
+    }
+    // std::sort(vecMatchParameter, compareScoreBig2Small) (:214) over the push-order sequence.  The permutation
+    // std::sort produces depends only on the sequence of comparison results, so sorting light (score, index) keys
+    // with the same comparator reproduces the reference's order of equal scores exactly.
+    struct Key { double score; int i; };
+    std::vector<Key> order(n);
+    for (int i = 0; i < n; ++i) order[i] = {cand[i].top_score, i};
+    std::sort(order.begin(), order.end(), [](const Key& l, const Key& r) { return l.score > r.score; });
+    std::vector<HostMatch> all;
+    for (const Key& k : order) {   // vecAllResult in sorted-candidate order (:262-358)
+        const fpm_candidate& c = cand[k.i];
+        if (!c.kept) continue;
+        HostMatch m{};
+        m.ptx = c.x; m.pty = c.y; m.score = c.score; m.angle = c.angle;
+        all.push_back(m);
+    }
+    filter_with_score(all, prm.score);
     for (HostMatch& m : all) {   // :380-390
         const double rad = -m.angle * kD2R;
         const F2 lt = f2((float)m.ptx, (float)m.pty);
-        const F2 rt = f2(lt.x + dstW * (float)std::cos(rad), lt.y - dstW * (float)std::sin(rad));
-        const F2 rb = f2(rt.x + dstH * (float)std::sin(rad), rt.y + dstH * (float)std::cos(rad));
+        const F2 rt = f2(lt.x + t0w * (float)std::cos(rad), lt.y - t0w * (float)std::sin(rad));
+        const F2 rb = f2(rt.x + t0h * (float)std::sin(rad), rt.y + t0h * (float)std::cos(rad));
         m.rect = rrect_from3(lt, rt, rb);
         m.del = false;
     }
-    HT(4);
-    filter_with_rotated_rect(all, ctx->prm.max_overlap);
-    HT(5);
-    HT_PRINT(0, 1, "sort");
-    HT_PRINT(1, 2, "collect");
-    HT_PRINT(2, 3, "score");
-    HT_PRINT(4, 5, "rotrect");
-#ifdef FPM_HOST_TIMING
-    fprintf(stderr, "host n=%zu order=%zu\n", all.size(), order.size());
-#endif
+    filter_with_rotated_rect(all, prm.max_overlap);
     std::sort(all.begin(), all.end(), score_big2small);
-    out.clear();
     for (const HostMatch& m : all) {   // :406-432
         const double rad = -m.angle * kD2R;
         const F2 lt = f2((float)m.ptx, (float)m.pty);
-        const F2 rt = f2(lt.x + t0.w * (float)std::cos(rad), lt.y - t0.w * (float)std::sin(rad));
-        const F2 lb = f2(lt.x + t0.h * (float)std::sin(rad), lt.y + t0.h * (float)std::cos(rad));
-        const F2 rb = f2(rt.x + t0.h * (float)std::sin(rad), rt.y + t0.h * (float)std::cos(rad));
+        const F2 rt = f2(lt.x + t0w * (float)std::cos(rad), lt.y - t0w * (float)std::sin(rad));
+        const F2 lb = f2(lt.x + t0h * (float)std::sin(rad), lt.y + t0h * (float)std::cos(rad));
+        const F2 rb = f2(rt.x + t0h * (float)std::sin(rad), rt.y + t0h * (float)std::cos(rad));
         const F2 c = f2((lt.x + rt.x + lb.x + rb.x) / 4.0f, (lt.y + rt.y + lb.y + rb.y) / 4.0f);
         fpm_result o;
         o.lt_x = lt.x; o.lt_y = lt.y; o.rt_x = rt.x; o.rt_y = rt.y;
@@ -814,6 +833,7 @@ void finish_source(fpm_ctx* ctx, int s, std::vector<fpm_result>& out, const std:
         o.cx = c.x; o.cy = c.y; o.angle = m.angle; o.score = m.score;
         out.push_back(o);
     }
+    return true;
 }
 
 // Launch the search: replay the captured graph (every pointer and launch shape is fixed by the plan and the
@@ -848,8 +868,10 @@ int start_staged(fpm_ctx* ctx) {
         HIP_TRY(hipEventCreate(&ctx->t_ev[1]));
     }
     HIP_TRY(hipEventRecord(ctx->t_ev[0], ctx->stream));
-    rc = launch_search(ctx);
-    if (rc != FPM_OK) return rc;
+    if (ctx->plan.nang > 0) {   // an angle shard with no angles has no device work (and no candidates)
+        rc = launch_search(ctx);
+        if (rc != FPM_OK) return rc;
+    }
     HIP_TRY(hipEventRecord(ctx->t_ev[1], ctx->stream));
     ctx->pending = true;
     return FPM_OK;
@@ -870,23 +892,29 @@ int complete_staged(fpm_ctx* ctx, std::vector<std::vector<fpm_result>>& results)
     Plan& P = ctx->plan;
     results.assign(P.S, {});
     std::vector<int> pos;
-    if (P.L > 0) {
+    if (P.L > 0 && P.nang > 0) {
         const char* hb = P.h_out.as<char>();
         const int n0 = ((const int32_t*)(hb + P.h_live))[P.L - 1];
         const int32_t* ids = (const int32_t*)(hb + P.h_live0);
         pos.assign(P.C, -1);
         for (int li = 0; li < n0; ++li) pos[ids[li]] = li;
     }
-    for (int s = 0; s < P.S; ++s) finish_source(ctx, s, results[s], pos);
+    ctx->cands.assign(P.S, {});
+    for (int s = 0; s < P.S; ++s) {
+        collect_candidates(ctx, s, pos, ctx->cands[s]);
+        merge_candidates(ctx->prm, ctx->tmpl[0].w, ctx->tmpl[0].h, ctx->cands[s].data(), (int)ctx->cands[s].size(),
+                         results[s]);
+    }
     // stats: [angles, top candidates, live entering layer L-1 .. 0] (totals over the batch)
     const char* h = P.h_out.as<char>();
     const int32_t* counts = (const int32_t*)(h + P.h_counts);
     int64_t topc = 0;
     for (int k = 0; k < P.S * P.nang; ++k) topc += counts[k];
     ctx->stats.assign({(int64_t)P.nang, topc});
-    const int32_t* lc = (const int32_t*)(h + P.h_live);
+    static const int32_t zeros[64] = {};
+    const int32_t* lc = P.nang > 0 ? (const int32_t*)(h + P.h_live) : zeros;
     for (int d = 0; d < P.L; ++d) ctx->stats.push_back(lc[d]);
-    if (ctx->prof) {   // refinement bytes need the live counts
+    if (ctx->prof && P.nang > 0) {   // refinement bytes need the live counts
         for (int d = 0; d < P.L; ++d) {
             const int l = P.L - 1 - d;
             const TmplLevel& t = ctx->tmpl[l];
@@ -1167,6 +1195,44 @@ int fpm_match(fpm_ctx* ctx, const uint8_t* gray, int32_t w, int32_t h, size_t st
     if (!r.empty() && seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
     for (int i = 0; i < (int)r.size() && i < cap && out; ++i) out[i] = r[i];
     return (int)r.size() > cap ? FPM_E_CAPACITY : FPM_OK;
+}
+
+// --- angle sharding of one search ---------------------------------------------------------
+int fpm_set_angle_shard(fpm_ctx* ctx, int32_t shard, int32_t shards) {
+    if (!ctx) return FPM_E_INVALID_ARG;
+    if (shards < 1 || shard < 0 || shard >= shards) { ctx->err = "bad angle shard"; return FPM_E_INVALID_ARG; }
+    if (ctx->pending) { ctx->err = "a search is in flight (fpm_match_staged_finish first)"; return FPM_E_INVALID_ARG; }
+    ctx->shard = shard;
+    ctx->shards = shards;
+    return FPM_OK;
+}
+
+int fpm_get_angle_shard(const fpm_ctx* ctx, int32_t* shard, int32_t* shards) {
+    if (!ctx || !shard || !shards) return FPM_E_INVALID_ARG;
+    *shard = ctx->shard;
+    *shards = ctx->shards;
+    return FPM_OK;
+}
+
+int fpm_last_candidates(const fpm_ctx* ctx, int32_t source, fpm_candidate* out, int32_t cap, int32_t* n) {
+    if (!ctx || !n) return FPM_E_INVALID_ARG;
+    *n = 0;
+    if (source < 0 || source >= (int)ctx->cands.size()) return FPM_E_INVALID_ARG;
+    const std::vector<fpm_candidate>& c = ctx->cands[source];
+    *n = (int32_t)c.size();
+    for (int i = 0; i < (int)c.size() && i < cap && out; ++i) out[i] = c[i];
+    return (int)c.size() > cap ? FPM_E_CAPACITY : FPM_OK;
+}
+
+int fpm_merge_candidates(const fpm_params* p, int32_t tmpl_w, int32_t tmpl_h, const fpm_candidate* cand, int32_t n,
+                         fpm_result* out, int32_t cap, int32_t* n_results) {
+    if (!p || !n_results || tmpl_w <= 0 || tmpl_h <= 0 || n < 0 || (n > 0 && !cand)) return FPM_E_INVALID_ARG;
+    *n_results = 0;
+    std::vector<fpm_result> res;
+    if (!merge_candidates(*p, tmpl_w, tmpl_h, cand, n, res)) return FPM_E_INVALID_ARG;
+    *n_results = (int32_t)res.size();
+    for (int i = 0; i < (int)res.size() && i < cap && out; ++i) out[i] = res[i];
+    return (int)res.size() > cap ? FPM_E_CAPACITY : FPM_OK;
 }
 
 int fpm_search_stats(const fpm_ctx* ctx, int64_t* stats, int32_t cap) {

@@ -51,6 +51,27 @@ class SingleTargetMatch:
                 self.dMatchScore)
 
 
+# fpm_candidate as a numpy record (include/fpm.h), 56 bytes
+CANDIDATE_DTYPE = np.dtype([("top_score", "<f8"), ("x", "<f8"), ("y", "<f8"), ("score", "<f8"), ("angle", "<f8"),
+                            ("angle_index", "<i4"), ("peak_rank", "<i4"), ("source", "<i4"), ("kept", "<i4")])
+assert CANDIDATE_DTYPE.itemsize == C.sizeof(L.Candidate)
+
+
+def merge_candidates(params: "L.Params", tmpl_w: int, tmpl_h: int, cands: np.ndarray) -> List[SingleTargetMatch]:
+    """fpm_merge_candidates: the coupled tail of TemplateMatcher::match (TemplateMatcher.cpp:214, 262-432) over one
+    source's candidate records in push order (all shards concatenated in shard order).  Host only (no device)."""
+    lib = L.load()
+    c = np.ascontiguousarray(cands, CANDIDATE_DTYPE)
+    cap = max(16, len(c))
+    out = (L.Result * cap)()
+    n = C.c_int32()
+    rc = lib.fpm_merge_candidates(C.byref(params), int(tmpl_w), int(tmpl_h),
+                                  c.ctypes.data_as(C.POINTER(L.Candidate)), len(c), out, cap, C.byref(n))
+    if rc != L.FPM_OK:
+        raise ValueError(f"fpm_merge_candidates failed with {rc} (records not in push order?)")
+    return [SingleTargetMatch.from_c(out[i]) for i in range(n.value)]
+
+
 def _gray(img) -> np.ndarray:
     a = np.asarray(img)
     if a.ndim != 2 or a.dtype != np.uint8:
@@ -187,6 +208,30 @@ class TemplateMatcher:
             if rc != L.FPM_OK:
                 raise RuntimeError(f"fpm_match_staged_finish failed with {rc}: {self.last_error()}")
             return views
+
+    # -- angle sharding of one search (fpm_set_angle_shard / fpm_last_candidates; sharding.match_angle_sharded) ----
+    def setAngleShard(self, shard: int, shards: int):
+        """Restrict searches to shard `shard` of `shards` contiguous blocks of the top-layer angle list."""
+        rc = self._lib.fpm_set_angle_shard(self._ctx, int(shard), int(shards))
+        if rc != L.FPM_OK:
+            raise ValueError(f"fpm_set_angle_shard({shard}, {shards}) failed with {rc}: {self.last_error()}")
+
+    def getAngleShard(self) -> Tuple[int, int]:
+        a, b = C.c_int32(), C.c_int32()
+        self._lib.fpm_get_angle_shard(self._ctx, C.byref(a), C.byref(b))
+        return a.value, b.value
+
+    def last_candidates(self, source: int = 0) -> np.ndarray:
+        """Candidate records (CANDIDATE_DTYPE, push order) of `source` in the last search."""
+        n = C.c_int32()
+        rc = self._lib.fpm_last_candidates(self._ctx, int(source), None, 0, C.byref(n))
+        if rc not in (L.FPM_OK, L.FPM_E_CAPACITY):
+            raise ValueError(f"fpm_last_candidates({source}) failed with {rc}")
+        out = np.zeros(n.value, CANDIDATE_DTYPE)
+        if n.value:
+            self._lib.fpm_last_candidates(self._ctx, int(source), out.ctypes.data_as(C.POINTER(L.Candidate)),
+                                          n.value, C.byref(n))
+        return out
 
     def search_stats(self) -> List[int]:
         buf = (C.c_int64 * 64)()

@@ -1,4 +1,5 @@
-"""Multi-GPU layer: one process per GPU, sources sharded across ranks (batch config).
+"""Multi-GPU layer: one process per GPU; sources sharded across ranks (batch config), or the
+angles of one search sharded across ranks with an all_gather of candidate records (single-image configs).
 
 Every source image is an independent ``TemplateMatcher::match`` call (TemplateMatcher.cpp:97-437), so the path
 partitions by source with no data-path collective: rank r searches the contiguous slice
@@ -96,3 +97,70 @@ def match_sharded(matcher, sources: Sequence[np.ndarray], cap: int = 256, group=
     mine = matcher.match_batch(list(sources[a:b])) if b > a else []
     local = [[r.as_tuple() for r in res] for res in mine]
     return gather_results(local, len(sources), cap, group=group, device=device)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# Angle sharding of ONE search (SURVEY.md §8(e), configs 2-±180 / 3-±180 / 5): every rank runs the top-layer sweep
+# and the pyramid descent for a contiguous block of the angle list (fpm_set_angle_shard), the candidate records
+# (fpm_candidate: top score, angle index, peak rank, refined pose) are all-gathered in rank order — which is the
+# reference's push order of vecMatchParameter (TemplateMatcher.cpp:157-211) — and every rank runs the coupled
+# tail (sort :214, filters and conversion :373-432) on the full list with fpm_merge_candidates.
+# ---------------------------------------------------------------------------------------------------------------
+def angle_block(n_angles: int, shard: int, shards: int) -> Tuple[int, int]:
+    """The block [a0, a1) of the top-layer angle list that fpm_set_angle_shard(shard, shards) searches (the same
+    integer formula as the engine's build_plan)."""
+    if shards < 1 or not 0 <= shard < shards or n_angles < 0:
+        raise ValueError(f"bad angle shard {shard}/{shards} of {n_angles}")
+    return n_angles * shard // shards, n_angles * (shard + 1) // shards
+
+
+def gather_candidates(local: np.ndarray, group=None, device=None) -> np.ndarray:
+    """all_gather variable-length candidate record arrays (CANDIDATE_DTYPE); returns the rank-order concatenation
+    on every rank.  Two collectives: the counts, then the records as bytes padded to the largest count."""
+    import torch
+    import torch.distributed as dist
+
+    from .matcher import CANDIDATE_DTYPE
+
+    local = np.ascontiguousarray(local, CANDIDATE_DTYPE)
+    world = dist.get_world_size(group)
+    cnt = torch.tensor([len(local)], dtype=torch.int64)
+    if device is not None:
+        cnt = cnt.to(device)
+    counts = [torch.empty_like(cnt) for _ in range(world)]
+    dist.all_gather(counts, cnt, group=group)
+    counts = [int(c.item()) for c in counts]
+    width = max(max(counts), 1) * CANDIDATE_DTYPE.itemsize
+    buf = np.zeros(width, np.uint8)
+    raw = local.view(np.uint8)
+    buf[:raw.size] = raw
+    mine = torch.from_numpy(buf)
+    if device is not None:
+        mine = mine.to(device)
+    parts = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(parts, mine, group=group)
+    out = [parts[k].cpu().numpy()[:counts[k] * CANDIDATE_DTYPE.itemsize].view(CANDIDATE_DTYPE) for k in range(world)]
+    return np.concatenate(out) if out else np.zeros(0, CANDIDATE_DTYPE)
+
+
+def merge_gathered(params, tmpl_w: int, tmpl_h: int, cands: np.ndarray):
+    """fpm_merge_candidates over gathered records (host only): the search's final s_SingleTargetMatch list."""
+    from .matcher import merge_candidates
+
+    return merge_candidates(params, tmpl_w, tmpl_h, cands)
+
+
+def match_angle_sharded(matcher, source: np.ndarray, group=None, device=None):
+    """One search of `source` split by angle over the ranks of `group`: this rank's matcher (bound to its GPU)
+    searches its angle block, the candidate records are all-gathered, and every rank returns the full result
+    list — identical to matcher.match(source) on one GPU."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    matcher.setAngleShard(rank, world)
+    matcher.match(source)
+    local = matcher.last_candidates(0)
+    full = gather_candidates(local, group=group, device=device)
+    tw, th = matcher.template_level(0)[0].shape[::-1]
+    return merge_gathered(matcher._params, tw, th, full)

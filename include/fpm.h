@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define FPM_ABI_VERSION 5
+#define FPM_ABI_VERSION 6
 
 /* status codes */
 #define FPM_OK 0
@@ -104,6 +104,41 @@ int fpm_match_staged(fpm_ctx* ctx, fpm_result* out, int32_t cap_per_source, int3
  * can have searches in flight at once; the staged sources must not be re-staged in between. */
 int fpm_match_staged_launch(fpm_ctx* ctx);
 int fpm_match_staged_finish(fpm_ctx* ctx, fpm_result* out, int32_t cap_per_source, int32_t* n_results);
+
+/* --- angle sharding of one search (no reference equivalent: the reference loops over the
+ * whole angle list on one thread, TemplateMatcher.cpp:157-211) ----------------------------------------------
+ * A search splits at the reference's own seam: the top-layer sweep and every candidate's pyramid descent
+ * (:157-371) are independent per angle, while the std::sort of the top candidates (:214) and the result
+ * filters (:373-432) need all of them.  So: every rank runs the search restricted to its shard of the angle
+ * list, exports its candidate records, the records are all-gathered in shard order (RCCL over xGMI on a node),
+ * and fpm_merge_candidates runs the coupled tail.  The merged results equal the unsharded search's bit for bit.
+ *
+ * One top-layer candidate (an s_MatchParameter of vecMatchParameter, DataStructures.h:58-94) and the outcome of
+ * its refinement. */
+typedef struct fpm_candidate {
+    double top_score;     /* dMatchScore at the top layer: the key of std::sort(compareScoreBig2Small) (:214) */
+    double x, y;          /* refined ptLT at layer 0 (the vecAllResult entry's pt, :346-356), when kept     */
+    double score;         /* refined dMatchScore (:312), when kept                                         */
+    double angle;         /* refined dMatchAngle (sub-pixel estimate applied, :334-344), when kept          */
+    int32_t angle_index;  /* index of the candidate's angle in the full top-layer angle list (:130-144)    */
+    int32_t peak_rank;    /* push order of the peak within its angle (0 = the minMaxLoc / s_BlockMax max)  */
+    int32_t source;       /* source index within a staged batch (0 for fpm_match)                           */
+    int32_t kept;         /* 1: reaches vecAllResult; 0: left the descent at a layer score (:331-332)       */
+} fpm_candidate;
+
+/* Restrict this context's searches to shard `shard` of `shards`: the contiguous block
+ * [n*shard/shards, n*(shard+1)/shards) of the n top-layer angles.  (0, 1) = the whole list (default).  fpm_match /
+ * fpm_match_staged on a sharded context return the results of that block alone. */
+int fpm_set_angle_shard(fpm_ctx* ctx, int32_t shard, int32_t shards);
+int fpm_get_angle_shard(const fpm_ctx* ctx, int32_t* shard, int32_t* shards);
+/* Candidate records of source `source` of the last fpm_match / fpm_match_staged* call, in push order
+ * (angle_index ascending, then peak_rank), every top-layer candidate of the context's shard included. */
+int fpm_last_candidates(const fpm_ctx* ctx, int32_t source, fpm_candidate* out, int32_t cap, int32_t* n);
+/* The coupled tail of TemplateMatcher::match (:214, :262-432) over the candidate records of ONE source: `cand` is
+ * the concatenation of every shard's records in shard order (push order; FPM_E_INVALID_ARG otherwise).  Host
+ * only, no context or device needed; tmpl_w/tmpl_h = the learned template's level-0 size. */
+int fpm_merge_candidates(const fpm_params* p, int32_t tmpl_w, int32_t tmpl_h, const fpm_candidate* cand, int32_t n,
+                         fpm_result* out, int32_t cap, int32_t* n_results);
 
 /* --- pixel operators (L1 kernels exposed for parity tests and standalone use) ----------------------- */
 /* cv::pyrDown (8U, 5x5 Gaussian, reflect-101), as called by cv::buildPyramid (TemplateMatcher.cpp:55,124).

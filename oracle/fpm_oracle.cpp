@@ -381,6 +381,7 @@ struct MatchParam {
     bool del = false;
     double vecResult[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
     bool on_border = false;
+    int origin = -1;   // not in the reference: push index into vecMatchParameter, to export candidate records
     MatchParam() {}
     MatchParam(P2f p, double s, double a) : pt(p.x, p.y), score(s), angle(a) {}
 };
@@ -430,6 +431,7 @@ struct SearchStats {
     int top_angles = 0, top_candidates = 0;
     std::vector<int> live_per_layer;  // entering layer L-1 .. 0
     std::vector<MatchParam> top_list; // vecMatchParameter before the sort (reference push order)
+    std::vector<fpm_candidate> cands; // per push-order candidate: top score, angle index, peak rank, refined pose
 };
 
 class Matcher {
@@ -792,6 +794,21 @@ public:
     }
 
     // TemplateMatcher::match (TemplateMatcher.cpp:97-437)
+    // candidate-record export (test infrastructure for the angle-sharded merge; no reference counterpart)
+    void note_candidate(MatchParam& m, int angle_index, int peak_rank) {
+        m.origin = (int)stats.cands.size();
+        fpm_candidate c;
+        std::memset(&c, 0, sizeof(c));
+        c.top_score = m.score;
+        c.angle_index = angle_index;
+        c.peak_rank = peak_rank;
+        stats.cands.push_back(c);
+    }
+    void note_kept(int origin, const MatchParam& m) {
+        fpm_candidate& c = stats.cands[origin];
+        c.x = m.pt.x; c.y = m.pt.y; c.score = m.score; c.angle = m.angle; c.kept = 1;
+    }
+
     int match(const Mat8& src, std::vector<fpm_result>& out) {
         out.clear();
         stats = SearchStats();
@@ -842,19 +859,23 @@ public:
                 bm.get_max(&vmax, &px, &py);
                 if (vmax < layer_score[L]) continue;
                 cand.push_back(MatchParam(P2f(px - tx, py - ty), vmax, angles[i]));
+                note_candidate(cand.back(), i, 0);
                 for (int j = 0; j < prm.max_pos + MATCH_CANDIDATE_NUM - 1; ++j) {
                     next_max_loc_block(res, px, py, tw, th, v, prm.max_overlap, bm);
                     if (v < layer_score[L]) break;
                     cand.push_back(MatchParam(P2f(px - tx, py - ty), v, angles[i]));
+                    note_candidate(cand.back(), i, j + 1);
                 }
             } else {
                 max_loc(res, 0, 0, res.w, res.h, &vmax, &px, &py);
                 if (vmax < layer_score[L]) continue;
                 cand.push_back(MatchParam(P2f(px - tx, py - ty), vmax, angles[i]));
+                note_candidate(cand.back(), i, 0);
                 for (int j = 0; j < prm.max_pos + MATCH_CANDIDATE_NUM - 1; ++j) {
                     next_max_loc(res, px, py, tw, th, v, prm.max_overlap);
                     if (v < layer_score[L]) break;
                     cand.push_back(MatchParam(P2f(px - tx, py - ty), v, angles[i]));
+                    note_candidate(cand.back(), i, j + 1);
                 }
             }
         }
@@ -876,6 +897,7 @@ public:
                 P2f p(lt.x * ((L == 0) ? 1 : 2), lt.y * ((L == 0) ? 1 : 2));
                 cand[i].pt = P2d(p.x, p.y);
                 all.push_back(cand[i]);
+                note_kept(cand[i].origin, all.back());
                 continue;
             }
             for (int l = L - 1; l >= stop; --l) {
@@ -928,6 +950,7 @@ public:
                     P2f pf(p.x * f, p.y * f);
                     nm[imax].pt = P2d(pf.x, pf.y);
                     all.push_back(nm[imax]);
+                    note_kept(cand[i].origin, all.back());
                 } else {
                     cand[i].angle = nang2;
                     lt = p;
@@ -1021,6 +1044,14 @@ int orc_search_stats(void* h, int64_t* s, int cap) {
     if (n < cap) s[n++] = m->stats.top_candidates;
     for (int v : m->stats.live_per_layer)
         if (n < cap) s[n++] = v;
+    return n;
+}
+
+// candidate records of the last match in push order (fpm_candidate, include/fpm.h); returns the count
+int orc_candidates(void* h, fpm_candidate* out, int cap) {
+    auto* m = (orc::Matcher*)h;
+    int n = (int)m->stats.cands.size();
+    for (int i = 0; i < n && i < cap; ++i) out[i] = m->stats.cands[i];
     return n;
 }
 

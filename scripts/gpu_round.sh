@@ -18,7 +18,7 @@ timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/s
 echo "smoke rc=$rc"; tail -2 $OUT/smoke_$TAG.log; stop_if_fault $rc smoke
 timeout -k 10 420 python -u bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.log; rc=$?
 echo "bench rc=$rc"; cat $OUT/bench_$TAG.json | head -c 3000; echo; stop_if_fault $rc bench
-cd /tmp && timeout -k 10 420 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o run --output-format csv -- python3 $ROOT/bench.py --steps 10 --warmup 2 --cpu-budget 0 --skip-latency > $OUT/prof_bench_$TAG.json 2> $OUT/prof_$TAG.log; rc=$?
+cd /tmp && timeout -k 10 420 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o run --output-format csv -- python3 $ROOT/bench.py --kernel-pass-only --steps 50 > $OUT/prof_bench_$TAG.json 2> $OUT/prof_$TAG.log; rc=$?
 echo "rocprof rc=$rc"; stop_if_fault $rc rocprof
 find $OUT/prof_$TAG -name '*stats*' | head
 exit 0

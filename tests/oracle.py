@@ -36,6 +36,7 @@ def load(path: str = ORACLE_LIB):
     lib.orc_match.argtypes = [C.c_void_p, _U8P, C.c_int, C.c_int, C.c_size_t, C.POINTER(Result), C.c_int,
                               C.POINTER(C.c_int), C.POINTER(C.c_double)]
     lib.orc_search_stats.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.c_int]
+    lib.orc_candidates.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
     lib.orc_top_candidates.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_int]
     lib.orc_template_info.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     lib.orc_template_level.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
@@ -139,6 +140,16 @@ class OracleMatcher:
         buf = (C.c_int64 * 64)()
         k = self._lib.orc_search_stats(self._h, buf, 64)
         return list(buf[:k])
+
+    def candidates(self) -> np.ndarray:
+        """Candidate records of the last match in push order (fpm_candidate / matcher.CANDIDATE_DTYPE)."""
+        from fastest_image_pattern_matching_amd.matcher import CANDIDATE_DTYPE
+
+        n = self._lib.orc_candidates(self._h, None, 0)
+        out = np.zeros(n, CANDIDATE_DTYPE)
+        if n:
+            self._lib.orc_candidates(self._h, out.ctypes.data_as(C.c_void_p), n)
+        return out
 
     def top_candidates(self):
         n = self._lib.orc_top_candidates(self._h, None, 0)

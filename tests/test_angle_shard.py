@@ -1,0 +1,139 @@
+"""Angle sharding of one search, host side: the coupled tail fpm_merge_candidates (libfpm_hip.so,
+host code, no device) over candidate records, and the gloo all_gather of records between ranks.
+
+The records come from the CPU oracle (tests/oracle.py: the restatement exports, for every top-layer candidate in
+the reference's push order, its top score, angle index, peak rank and refined pose).  fpm_merge_candidates over
+the full list must reproduce the oracle's own match() bit for bit, and so must the rank-order concatenation of
+per-rank angle blocks after an all_gather.  The GPU side (records produced by the HIP path per shard) is
+tests/test_gpu_angle_shard.py.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from fastest_image_pattern_matching_amd import sharding, synth
+from fastest_image_pattern_matching_amd.matcher import CANDIDATE_DTYPE, merge_candidates
+from tests import oracle
+from tests.cases import CASES
+
+FAST_CASES = ["plumbing_tol0", "dst10_multi", "dst10_nosimd", "dst5_subpixel", "dst4_overlap", "dst3_range",
+              "top_is_layer0", "score_low_many"]
+
+
+def _oracle_run(case, templates):
+    make, prm = CASES[case]
+    s, t = make(templates)
+    o = oracle.OracleMatcher().set(**prm)
+    assert o.learnPattern(t)
+    res = o.match(s)
+    return o, t, res, o.candidates()
+
+
+def _tuples(results):
+    return [r.as_tuple() for r in results]
+
+
+@pytest.mark.parametrize("case", FAST_CASES)
+def test_merge_reproduces_oracle(templates, case):
+    o, t, res, cands = _oracle_run(case, templates)
+    assert len(cands) == o.stats()[1]                 # one record per top-layer candidate
+    assert np.all(np.diff(cands["angle_index"]) >= 0)
+    merged = merge_candidates(o.params, t.shape[1], t.shape[0], cands)
+    assert _tuples(merged) == res, case
+
+
+@pytest.mark.parametrize("case", ["dst10_multi", "dst4_overlap", "score_low_many"])
+@pytest.mark.parametrize("shards", [2, 3, 8, 50])
+def test_block_concatenation_is_push_order(templates, case, shards):
+    """Per-shard angle blocks (sharding.angle_block) concatenated in shard order = the full list, and merge it."""
+    o, t, res, cands = _oracle_run(case, templates)
+    nang = o.stats()[0]
+    parts = []
+    for k in range(shards):
+        a0, a1 = sharding.angle_block(nang, k, shards)
+        parts.append(cands[(cands["angle_index"] >= a0) & (cands["angle_index"] < a1)])
+    cat = np.concatenate(parts)
+    assert cat.tobytes() == cands.tobytes()
+    assert _tuples(merge_candidates(o.params, t.shape[1], t.shape[0], cat)) == res
+
+
+def test_merge_rejects_out_of_order(templates):
+    o, t, res, cands = _oracle_run("dst10_multi", templates)
+    assert len(np.unique(cands["angle_index"])) >= 2
+    swapped = np.concatenate([cands[cands["angle_index"] > cands["angle_index"][0]],
+                              cands[cands["angle_index"] == cands["angle_index"][0]]])
+    with pytest.raises(ValueError):
+        merge_candidates(o.params, t.shape[1], t.shape[0], swapped)
+    bad = cands.copy()
+    bad["peak_rank"][0] = 1
+    with pytest.raises(ValueError):
+        merge_candidates(o.params, t.shape[1], t.shape[0], bad)
+    assert merge_candidates(o.params, t.shape[1], t.shape[0], cands[:0]) == []
+
+
+def test_merge_equal_scores_keep_reference_order():
+    """Equal top scores across angles: the tail's std::sort must see the push order (it is unstable), so the
+    first-pushed of two equal, overlapping candidates survives the rotated-rect filter."""
+    p = oracle.OracleMatcher().params
+    p.max_overlap = 0.0
+    rec = np.zeros(40, CANDIDATE_DTYPE)
+    rec["top_score"] = 0.9
+    rec["angle_index"] = np.arange(40)
+    rec["kept"] = 1
+    rec["x"], rec["y"] = 100.0, 100.0
+    rec["score"] = 0.95
+    rec["angle"] = np.arange(40) * 0.25
+    out = merge_candidates(p, 30, 20, rec)
+    assert len(out) == 1
+    # std::sort (introsort, > 16 elements) of 40 equal keys: the survivor is whatever libstdc++ puts first, the
+    # same element for any sharding of the same sequence
+    again = merge_candidates(p, 30, 20, np.concatenate([rec[:13], rec[13:]]))
+    assert _tuples(out) == _tuples(again)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, cases, q):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        templates = synth.load_templates()
+        for case in cases:
+            o, t, res, cands = _oracle_run(case, templates)
+            a0, a1 = sharding.angle_block(o.stats()[0], rank, world)
+            mine = cands[(cands["angle_index"] >= a0) & (cands["angle_index"] < a1)]
+            full = sharding.gather_candidates(mine)
+            merged = sharding.merge_gathered(o.params, t.shape[1], t.shape[0], full)
+            q.put((rank, case, full.tobytes() == cands.tobytes(), _tuples(merged) == res, len(res)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_angle_sharded_gloo(world):
+    cases = ["plumbing_tol0", "dst10_multi", "dst5_subpixel", "dst4_overlap"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=180) for _ in range(world * len(cases))]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len(got) == world * len(cases)
+    for rank, case, same_records, same_results, n in got:
+        assert same_records, (rank, case)
+        assert same_results, (rank, case)
+        assert n >= 1, (rank, case)

@@ -1,0 +1,128 @@
+"""Angle-sharded search on the HIP path, through the C ABI, against the oracle.
+
+Every shard's candidate records (fpm_last_candidates after a search restricted by fpm_set_angle_shard) must equal
+the oracle's records of that angle block byte for byte; their shard-order concatenation merged by
+fpm_merge_candidates must equal both the unsharded GPU search and the oracle's results bit for bit.  One GPU runs
+the shards one after another — the multi-rank exchange itself is tests/test_angle_shard.py (gloo).
+"""
+import numpy as np
+import pytest
+
+from fastest_image_pattern_matching_amd import sharding, synth
+from fastest_image_pattern_matching_amd.matcher import merge_candidates
+from tests import oracle
+from tests.cases import CASES
+from tests.test_gpu_parity import assert_same_results
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hip(gpu_matcher_factory):
+    return gpu_matcher_factory()
+
+
+def _setup(hip, t, prm):
+    hip.resetParams()
+    for k, v in prm.items():
+        setattr(hip._params, k, v)
+    assert hip.learnPattern(t)
+
+
+def _sharded(hip, s, t, shards):
+    parts = []
+    for k in range(shards):
+        hip.setAngleShard(k, shards)
+        hip.match(s)
+        parts.append(hip.last_candidates(0))
+    hip.setAngleShard(0, 1)
+    return parts
+
+
+def _check(hip, o, s, t, shards, label):
+    orc = o.match(s)
+    ocand = o.candidates()
+    nang = o.stats()[0]
+    full = hip.match(s)
+    assert hip.getAngleShard() == (0, 1)
+    assert hip.last_candidates(0).tobytes() == ocand.tobytes(), f"{label}: unsharded records differ"
+    assert_same_results(full, orc, label)
+    for w in shards:
+        parts = _sharded(hip, s, t, w)
+        for k, p in enumerate(parts):
+            a0, a1 = sharding.angle_block(nang, k, w)
+            exp = ocand[(ocand["angle_index"] >= a0) & (ocand["angle_index"] < a1)]
+            assert p.tobytes() == exp.tobytes(), f"{label}: shard {k}/{w} records differ"
+        merged = merge_candidates(hip._params, t.shape[1], t.shape[0], np.concatenate(parts))
+        assert_same_results(merged, orc, f"{label} merged over {w} shards")
+    return orc
+
+
+@pytest.mark.parametrize("case", ["plumbing_tol0", "dst10_multi", "dst10_nosimd", "dst5_subpixel", "dst4_block",
+                                  "dst4_overlap", "dst3_range", "top_is_layer0", "score_low_many"])
+def test_angle_shard_parity(hip, templates, case):
+    make, prm = CASES[case]
+    s, t = make(templates)
+    o = oracle.OracleMatcher().set(**prm)
+    assert o.learnPattern(t)
+    _setup(hip, t, prm)
+    orc = _check(hip, o, s, t, (2, 3, 8), case)
+    assert len(orc) >= 1
+
+
+def test_angle_shard_src7(hip, templates):
+    """configs[1] (Src7 4024x3036, +-180, TargetNum 3; 41 top angles) over 8 angle shards."""
+    s, t = synth.src7_scene(templates["Dst7"])
+    prm = dict(max_pos=3, tolerance_angle=180.0, score=0.7)
+    o = oracle.OracleMatcher().set(**prm)
+    o.learnPattern(t)
+    _setup(hip, t, prm)
+    assert len(_check(hip, o, s, t, (8,), "src7")) == 3
+
+
+def test_angle_shard_src10_sweep(hip, templates):
+    """configs[2] stress (+-180, TargetNum 100, s_BlockMax) on the 1824x1824 quarter: 47 angles over 8 shards."""
+    s, t = synth.src10_scene(templates["Dst10"])
+    crop = np.ascontiguousarray(s[:1824, :1824])
+    prm = dict(max_pos=100, score=0.7, tolerance_angle=180.0)
+    o = oracle.OracleMatcher().set(**prm)
+    o.learnPattern(t)
+    _setup(hip, t, prm)
+    assert len(_check(hip, o, crop, t, (8,), "src10_180")) >= 30
+
+
+def test_angle_shard_staged_batch(hip, templates):
+    """Sharded staged batch: per-source records of every shard, merged per source, equal the oracle per source."""
+    t = templates["Dst10"]
+    srcs = []
+    for k in range(4):
+        sc = synth.noise(360, 300, 128, 10, 80 + k)
+        synth.paste_rotated(sc, t, 110 + 30 * k, 130 + 10 * k, 40.0 * k - 70)
+        srcs.append(sc)
+    prm = dict(max_pos=2, tolerance_angle=180.0)
+    o = oracle.OracleMatcher().set(**prm)
+    o.learnPattern(t)
+    _setup(hip, t, prm)
+    W = 3
+    parts = [[] for _ in srcs]
+    for k in range(W):
+        hip.setAngleShard(k, W)
+        hip.match_batch(srcs)
+        for i in range(len(srcs)):
+            rec = hip.last_candidates(i)
+            assert np.all(rec["source"] == i)
+            parts[i].append(rec)
+    hip.setAngleShard(0, 1)
+    for i, sc in enumerate(srcs):
+        orc = o.match(sc)
+        merged = merge_candidates(hip._params, t.shape[1], t.shape[0], np.concatenate(parts[i]))
+        assert_same_results(merged, orc, f"staged{i}")
+        assert len(orc) >= 1
+
+
+def test_angle_shard_errors(hip):
+    with pytest.raises(ValueError):
+        hip.setAngleShard(2, 2)
+    with pytest.raises(ValueError):
+        hip.setAngleShard(0, 0)
+    hip.setAngleShard(0, 1)
