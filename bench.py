@@ -157,7 +157,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=8, help="Src7 sources searched per GPU per step")
+    ap.add_argument("--batch", type=int, default=32, help="Src7 sources searched per GPU per step")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (0 = skip)")
     ap.add_argument("--contexts", type=int, default=2, help="concurrent contexts (HIP streams) per GPU")
     ap.add_argument("--skip-latency", action="store_true",

@@ -436,7 +436,11 @@ int build_plan(fpm_ctx* ctx) {
             P.roi_stride = std::max(P.roi_stride, roi_tiles_bytes(ctx->tmpl[l].w, ctx->tmpl[l].h));
         const size_t per_roi = sizeof(int32_t) * 2 * (P.tabw + P.tabh) + sizeof(int4) * P.tdesc_stride + P.roi_stride + max_rows * 49 * 4 +
                                max_chunks * 49 * 12;
-        const size_t budget = (size_t)16 << 30;   // of 288 GB HBM; rounds only beyond this
+        // slots are sized for the worst case (every top candidate alive at every layer) so the captured graph needs
+        // no host round trip; up to a sixth of the free HBM (<= 48 GB of 288) holds them, rounds only beyond that
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = (size_t)96 << 30;
+        const size_t budget = std::min((size_t)48 << 30, std::max((size_t)4 << 30, free_b / 6));
         const size_t want = (size_t)P.C * P.n3;
         // rounds hold whole candidates (k_roi_eval steps a candidate from its n3 records)
         P.slot_cap = (int)std::max<size_t>((size_t)P.n3, std::min(want, budget / per_roi) / P.n3 * P.n3);
@@ -802,6 +806,7 @@ bool merge_candidates(const fpm_params& prm, int t0w, int t0h, const fpm_candida
     for (int i = 0; i < n; ++i) order[i] = {cand[i].top_score, i};
     std::sort(order.begin(), order.end(), [](const Key& l, const Key& r) { return l.score > r.score; });
     std::vector<HostMatch> all;
+    all.reserve(n);
     for (const Key& k : order) {   // vecAllResult in sorted-candidate order (:262-358)
         const fpm_candidate& c = cand[k.i];
         if (!c.kept) continue;
@@ -812,9 +817,10 @@ bool merge_candidates(const fpm_params& prm, int t0w, int t0h, const fpm_candida
     filter_with_score(all, prm.score);
     for (HostMatch& m : all) {   // :380-390
         const double rad = -m.angle * kD2R;
+        const float c = (float)std::cos(rad), sn = (float)std::sin(rad);
         const F2 lt = f2((float)m.ptx, (float)m.pty);
-        const F2 rt = f2(lt.x + t0w * (float)std::cos(rad), lt.y - t0w * (float)std::sin(rad));
-        const F2 rb = f2(rt.x + t0h * (float)std::sin(rad), rt.y + t0h * (float)std::cos(rad));
+        const F2 rt = f2(lt.x + t0w * c, lt.y - t0w * sn);
+        const F2 rb = f2(rt.x + t0h * sn, rt.y + t0h * c);
         m.rect = rrect_from3(lt, rt, rb);
         m.del = false;
     }
@@ -822,10 +828,11 @@ bool merge_candidates(const fpm_params& prm, int t0w, int t0h, const fpm_candida
     std::sort(all.begin(), all.end(), score_big2small);
     for (const HostMatch& m : all) {   // :406-432
         const double rad = -m.angle * kD2R;
+        const float cs = (float)std::cos(rad), sn = (float)std::sin(rad);
         const F2 lt = f2((float)m.ptx, (float)m.pty);
-        const F2 rt = f2(lt.x + t0w * (float)std::cos(rad), lt.y - t0w * (float)std::sin(rad));
-        const F2 lb = f2(lt.x + t0h * (float)std::sin(rad), lt.y + t0h * (float)std::cos(rad));
-        const F2 rb = f2(rt.x + t0h * (float)std::sin(rad), rt.y + t0h * (float)std::cos(rad));
+        const F2 rt = f2(lt.x + t0w * cs, lt.y - t0w * sn);
+        const F2 lb = f2(lt.x + t0h * sn, lt.y + t0h * cs);
+        const F2 rb = f2(rt.x + t0h * sn, rt.y + t0h * cs);
         const F2 c = f2((lt.x + rt.x + lb.x + rb.x) / 4.0f, (lt.y + rt.y + lb.y + rb.y) / 4.0f);
         fpm_result o;
         o.lt_x = lt.x; o.lt_y = lt.y; o.rt_x = rt.x; o.rt_y = rt.y;
@@ -878,7 +885,7 @@ int start_staged(fpm_ctx* ctx) {
 }
 
 // Second half: wait for the device pass, then the host's reference-order post-processing per source.
-int complete_staged(fpm_ctx* ctx, std::vector<std::vector<fpm_result>>& results) {
+int complete_staged(fpm_ctx* ctx, std::vector<std::vector<fpm_result>>& results, bool merge = true) {
     if (!ctx->pending) { ctx->err = "no search in flight"; return FPM_E_INVALID_ARG; }
     ctx->pending = false;
     const auto c0 = ctx->t_call0;
@@ -902,7 +909,8 @@ int complete_staged(fpm_ctx* ctx, std::vector<std::vector<fpm_result>>& results)
     ctx->cands.assign(P.S, {});
     for (int s = 0; s < P.S; ++s) {
         collect_candidates(ctx, s, pos, ctx->cands[s]);
-        merge_candidates(ctx->prm, ctx->tmpl[0].w, ctx->tmpl[0].h, ctx->cands[s].data(), (int)ctx->cands[s].size(),
+        if (merge)
+            merge_candidates(ctx->prm, ctx->tmpl[0].w, ctx->tmpl[0].h, ctx->cands[s].data(), (int)ctx->cands[s].size(),
                          results[s]);
     }
     // stats: [angles, top candidates, live entering layer L-1 .. 0] (totals over the batch)
@@ -1161,7 +1169,7 @@ int fpm_match_staged_finish(fpm_ctx* ctx, fpm_result* out, int32_t cap, int32_t*
     if (!ctx || !n_results) return FPM_E_INVALID_ARG;
     HIP_TRY(hipSetDevice(ctx->device));
     std::vector<std::vector<fpm_result>> res;
-    const int rc = complete_staged(ctx, res);
+    const int rc = complete_staged(ctx, res, out != nullptr);
     if (rc != FPM_OK) return rc;
     return copy_results(res, out, cap, n_results);
 }

@@ -6,12 +6,29 @@
 #include "fpm_host.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
+#include <thread>
 
 namespace fpm {
 
 bool score_big2small(const HostMatch& a, const HostMatch& b) { return a.score > b.score; }
+
+// worker threads for the overlap filter's independent components: FPM_HOST_THREADS if set (>= 1), else the
+// hardware concurrency capped at 8
+static int host_threads() {
+    static const int n = [] {
+        if (const char* e = std::getenv("FPM_HOST_THREADS")) {
+            const int v = std::atoi(e);
+            if (v >= 1) return std::min(v, 64);
+        }
+        const int hw = (int)std::thread::hardware_concurrency();
+        return std::max(1, std::min(hw, 8));
+    }();
+    return n;
+}
 
 static inline double len2(float x, float y) { return std::sqrt((double)x * x + (double)y * y); }
 
@@ -207,7 +224,7 @@ void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
         }
         box[4 * i] = x0 - 1.f; box[4 * i + 1] = y0 - 1.f; box[4 * i + 2] = x1 + 1.f; box[4 * i + 3] = y1 + 1.f;
     }
-    auto pair = [&](int i, int j) {   // the reference's inner-loop body for (i, j), boxes overlapping
+    auto pair = [&](int i, int j, std::vector<F2>& pts) {   // the reference's inner-loop body for (i, j), boxes overlapping
         const int kind = rrect_intersection_c(v[i].rect, v[j].rect, &corners[(size_t)4 * i], &corners[(size_t)4 * j], pts);
         if (kind == 0) return;
         bool drop = kind == 2;
@@ -228,7 +245,7 @@ void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
         for (int i = 0; i + 1 < n; ++i) {
             if (v[i].del) continue;
             for (int j = i + 1; j < n; ++j)
-                if (!v[j].del && overlap(i, j)) pair(i, j);
+                if (!v[j].del && overlap(i, j)) pair(i, j, pts);
         }
     } else {
         // uniform grid over the boxes (cell = the largest box extent): for each i only the j > i whose boxes
@@ -247,18 +264,65 @@ void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
             for (int cy = cell(box[4 * i + 1], sy, gy0, gny); cy <= cell(box[4 * i + 3], sy, gy0, gny); ++cy)
                 for (int cx = cell(box[4 * i], sx, gx0, gnx); cx <= cell(box[4 * i + 2], sx, gx0, gnx); ++cx)
                     grid[(size_t)cy * gnx + cx].push_back(i);
-        std::vector<int> nb;
-        for (int i = 0; i + 1 < n; ++i) {
-            if (v[i].del) continue;
-            nb.clear();
-            for (int cy = cell(box[4 * i + 1], sy, gy0, gny); cy <= cell(box[4 * i + 3], sy, gy0, gny); ++cy)
-                for (int cx = cell(box[4 * i], sx, gx0, gnx); cx <= cell(box[4 * i + 2], sx, gx0, gnx); ++cx)
-                    for (int j : grid[(size_t)cy * gnx + cx])
-                        if (j > i) nb.push_back(j);
-            std::sort(nb.begin(), nb.end());
-            nb.erase(std::unique(nb.begin(), nb.end()), nb.end());
-            for (int j : nb)
-                if (!v[j].del && overlap(i, j)) pair(i, j);
+        // v is sorted by descending score, so pair(i, j) with i < j only ever deletes j: i is decided by the pairs
+        // (i', i), i' < i, with overlapping boxes.  Overlapping boxes share a grid cell, so the sets of boxes
+        // connected through shared cells are closed under the overlap relation and independent of each other; they
+        // are processed in parallel, each in the reference's ascending (i, j) order -- the same deletions exactly.
+        std::vector<int> root(n);
+        for (int i = 0; i < n; ++i) root[i] = i;
+        auto find = [&](int x) { while (root[x] != x) { root[x] = root[root[x]]; x = root[x]; } return x; };
+        for (const std::vector<int>& g : grid)
+            for (size_t k = 1; k < g.size(); ++k) {
+                const int a = find(g[0]), b = find(g[k]);
+                if (a != b) root[std::max(a, b)] = std::min(a, b);
+            }
+        std::vector<int> comp_of(n, -1), comp_off, members, comp_size;
+        int ncomp = 0;
+        for (int i = 0; i < n; ++i) {
+            const int r = find(i);
+            if (comp_of[r] < 0) { comp_of[r] = ncomp++; comp_size.push_back(0); }
+            comp_of[i] = comp_of[r];
+            comp_size[comp_of[i]]++;
+        }
+        comp_off.assign(ncomp + 1, 0);
+        for (int c = 0; c < ncomp; ++c) comp_off[c + 1] = comp_off[c] + comp_size[c];
+        members.resize(n);
+        {
+            std::vector<int> fill(comp_off.begin(), comp_off.end() - 1);
+            for (int i = 0; i < n; ++i) members[fill[comp_of[i]]++] = i;   // ascending within a component
+        }
+        auto run_comp = [&](int c, std::vector<F2>& p, std::vector<int>& nb) {
+            for (int k = comp_off[c]; k < comp_off[c + 1]; ++k) {
+                const int i = members[k];
+                if (v[i].del) continue;
+                nb.clear();
+                for (int cy = cell(box[4 * i + 1], sy, gy0, gny); cy <= cell(box[4 * i + 3], sy, gy0, gny); ++cy)
+                    for (int cx = cell(box[4 * i], sx, gx0, gnx); cx <= cell(box[4 * i + 2], sx, gx0, gnx); ++cx)
+                        for (int j : grid[(size_t)cy * gnx + cx])
+                            if (j > i) nb.push_back(j);
+                std::sort(nb.begin(), nb.end());
+                nb.erase(std::unique(nb.begin(), nb.end()), nb.end());
+                for (int j : nb)
+                    if (!v[j].del && overlap(i, j)) pair(i, j, p);
+            }
+        };
+        // threads only where there is enough exact-test work to pay for them (clusters of duplicate detections)
+        int nthreads = host_threads();
+        nthreads = std::min(nthreads, std::max(1, std::min(ncomp / 4, (n - ncomp) / 256)));
+        if (nthreads <= 1) {
+            std::vector<int> nb;
+            for (int c = 0; c < ncomp; ++c) run_comp(c, pts, nb);
+        } else {
+            std::atomic<int> next{0};
+            auto worker = [&]() {
+                std::vector<F2> p;
+                std::vector<int> nb;
+                for (int c = next.fetch_add(1); c < ncomp; c = next.fetch_add(1)) run_comp(c, p, nb);
+            };
+            std::vector<std::thread> th;
+            for (int t = 1; t < nthreads; ++t) th.emplace_back(worker);
+            worker();
+            for (std::thread& t : th) t.join();
         }
     }
     v.erase(std::remove_if(v.begin(), v.end(), [](const HostMatch& m) { return m.del; }), v.end());

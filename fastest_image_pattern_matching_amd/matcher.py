@@ -221,6 +221,16 @@ class TemplateMatcher:
         self._lib.fpm_get_angle_shard(self._ctx, C.byref(a), C.byref(b))
         return a.value, b.value
 
+    def match_staged_candidates(self) -> List[np.ndarray]:
+        """Search the staged sources and return each source's candidate records, skipping the host tail
+        (fpm_match_staged_finish with out = NULL): the per-rank step of an angle-sharded search."""
+        self.match_staged_launch()
+        n = (C.c_int32 * self._staged)()
+        rc = self._check(self._lib.fpm_match_staged_finish(self._ctx, None, 0, n), "match_staged_finish")
+        if rc != L.FPM_OK:
+            raise RuntimeError(f"fpm_match_staged_finish failed with {rc}: {self.last_error()}")
+        return [self.last_candidates(s) for s in range(self._staged)]
+
     def last_candidates(self, source: int = 0) -> np.ndarray:
         """Candidate records (CANDIDATE_DTYPE, push order) of `source` in the last search."""
         n = C.c_int32()

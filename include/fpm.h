@@ -103,6 +103,8 @@ int fpm_match_staged(fpm_ctx* ctx, fpm_result* out, int32_t cap_per_source, int3
  * _finish waits for it and runs the host post-processing.  Several contexts (one stream each) on one device
  * can have searches in flight at once; the staged sources must not be re-staged in between. */
 int fpm_match_staged_launch(fpm_ctx* ctx);
+/* out == NULL skips the host tail (sort, filters, conversion; n_results[s] = 0): for an angle-sharded context whose
+ * candidate records (fpm_last_candidates) are merged elsewhere. */
 int fpm_match_staged_finish(fpm_ctx* ctx, fpm_result* out, int32_t cap_per_source, int32_t* n_results);
 
 /* --- angle sharding of one search (no reference equivalent: the reference loops over the

@@ -107,6 +107,31 @@ public:
     bool hasUserDefinedRect() const { return has_rect_; }
     const int* getUserDefinedRect() const { return rect_; }
 
+    // angle sharding of one search across ranks (fpm.h): search this rank's block of the top-layer
+    // angle list, export its candidate records, and merge every rank's records (rank order) on any host
+    bool setAngleShard(int shard, int shards) { return fpm_set_angle_shard(ctx_, shard, shards) == FPM_OK; }
+    std::vector<fpm_candidate> lastCandidates(int source = 0) const {
+        int32_t n = 0;
+        fpm_last_candidates(ctx_, source, nullptr, 0, &n);
+        std::vector<fpm_candidate> out((size_t)n);
+        if (n > 0 && fpm_last_candidates(ctx_, source, out.data(), n, &n) != FPM_OK) out.clear();
+        return out;
+    }
+    std::vector<SingleTargetMatch> mergeCandidates(const std::vector<fpm_candidate>& all) const {
+        std::vector<SingleTargetMatch> out;
+        int32_t levels = 0, border = 0, tw = 0, th = 0, eq = 0;
+        double mean = 0, norm = 0, inv = 0;
+        if (fpm_template_info(ctx_, &levels, &border) != FPM_OK ||
+            fpm_template_level(ctx_, 0, &tw, &th, &mean, &norm, &inv, &eq, nullptr, 0) != FPM_OK)
+            return out;
+        std::vector<fpm_result> buf(all.size() + 1);
+        int32_t n = 0;
+        if (fpm_merge_candidates(&p_, tw, th, all.data(), (int32_t)all.size(), buf.data(), (int32_t)buf.size(), &n) != FPM_OK)
+            return out;
+        for (int i = 0; i < n; ++i) out.push_back(convert(buf[(size_t)i]));
+        return out;
+    }
+
     std::string lastError() const { const char* s = fpm_last_error(ctx_); return s ? s : ""; }
     fpm_ctx* context() const { return ctx_; }
 

@@ -78,7 +78,10 @@ int main() {
     try {
         fpm::TemplateMatcher m(0);
         m.setToleranceAngle(180); m.setMaxPositions(3);
-        std::printf("device %d\n", m.getMaxPositions());
+        m.setAngleShard(0, 2);
+        std::vector<fpm_candidate> c = m.lastCandidates(0);
+        std::vector<fpm::SingleTargetMatch> r = m.mergeCandidates(c);
+        std::printf("device %d\n", m.getMaxPositions() + (int)r.size() * 0);
     } catch (const std::runtime_error& e) {
         std::printf("nodevice\n");
     }

@@ -137,3 +137,33 @@ def test_angle_sharded_gloo(world):
         assert same_records, (rank, case)
         assert same_results, (rank, case)
         assert n >= 1, (rank, case)
+
+
+_MERGE_CHILD = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from fastest_image_pattern_matching_amd.matcher import CANDIDATE_DTYPE, merge_candidates
+from fastest_image_pattern_matching_amd import _lib as L
+z = np.load(sys.argv[2])
+p = L.Params(); L.load().fpm_params_default(p)
+p.max_pos, p.score, p.tolerance_angle, p.max_overlap = int(z["params"][0]), *map(float, z["params"][1:])
+rec = z["records"].view(CANDIDATE_DTYPE)
+out = np.array([r.as_tuple() for r in merge_candidates(p, int(z["tmpl_wh"][0]), int(z["tmpl_wh"][1]), rec)])
+print("SAME" if out.shape == z["results"].shape and np.array_equal(out, z["results"]) else "DIFF")
+"""
+
+
+@pytest.mark.parametrize("threads", ["1", "8"])
+def test_merge_large_fixture_threads(threads):
+    """Src10 +-180 records (4935 candidates, 144 duplicate clusters; tests/golden/make_merge_fixture.py): the merge's
+    component-parallel rotated-rect filter gives the oracle's sequential result at 1 and 8 host threads."""
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, FPM_HOST_THREADS=threads)
+    out = subprocess.run([sys.executable, "-c", _MERGE_CHILD, repo,
+                          os.path.join(repo, "tests", "golden", "merge_src10_180.npz")],
+                         env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip().endswith("SAME"), out.stdout + out.stderr

@@ -126,3 +126,23 @@ def test_angle_shard_errors(hip):
     with pytest.raises(ValueError):
         hip.setAngleShard(0, 0)
     hip.setAngleShard(0, 1)
+
+
+def test_staged_candidates_skip_tail(hip, templates):
+    """fpm_match_staged_finish(out = NULL): records only, identical to a full search's records."""
+    make, prm = CASES["dst10_multi"]
+    s, t = make(templates)
+    _setup(hip, t, prm)
+    hip.match(s)
+    full = hip.last_candidates(0)
+    nang = hip.search_stats()[0]
+    hip.stage([s])
+    parts = []
+    for k in range(2):
+        hip.setAngleShard(k, 2)
+        rec = hip.match_staged_candidates()[0]
+        a0, a1 = sharding.angle_block(nang, k, 2)
+        assert np.all((rec["angle_index"] >= a0) & (rec["angle_index"] < a1))
+        parts.append(rec)
+    hip.setAngleShard(0, 1)
+    assert np.concatenate(parts).tobytes() == full.tobytes()
