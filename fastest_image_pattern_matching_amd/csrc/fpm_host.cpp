@@ -259,11 +259,24 @@ void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
         const int gnx = std::min(1024, (int)((gx1 - gx0) / cs) + 1), gny = std::min(1024, (int)((gy1 - gy0) / cs) + 1);
         const float sx = gnx / std::max(gx1 - gx0, 1e-3f), sy = gny / std::max(gy1 - gy0, 1e-3f);
         auto cell = [&](float x, float s_, float o, int nmax) { return std::min(nmax - 1, std::max(0, (int)((x - o) * s_))); };
-        std::vector<std::vector<int>> grid((size_t)gnx * gny);
-        for (int i = 0; i < n; ++i)
-            for (int cy = cell(box[4 * i + 1], sy, gy0, gny); cy <= cell(box[4 * i + 3], sy, gy0, gny); ++cy)
-                for (int cx = cell(box[4 * i], sx, gx0, gnx); cx <= cell(box[4 * i + 2], sx, gx0, gnx); ++cx)
-                    grid[(size_t)cy * gnx + cx].push_back(i);
+        // cell -> ascending box indices, as CSR (count, prefix sum, fill)
+        const size_t ncell = (size_t)gnx * gny;
+        std::vector<int> cell_off(ncell + 1, 0), cell_box;
+        std::vector<int4> span(n);   // cx0, cy0, cx1, cy1 per box
+        for (int i = 0; i < n; ++i) {
+            span[i] = make_int4(cell(box[4 * i], sx, gx0, gnx), cell(box[4 * i + 1], sy, gy0, gny),
+                                cell(box[4 * i + 2], sx, gx0, gnx), cell(box[4 * i + 3], sy, gy0, gny));
+            for (int cy = span[i].y; cy <= span[i].w; ++cy)
+                for (int cx = span[i].x; cx <= span[i].z; ++cx) cell_off[(size_t)cy * gnx + cx + 1]++;
+        }
+        for (size_t c = 0; c < ncell; ++c) cell_off[c + 1] += cell_off[c];
+        cell_box.resize(cell_off[ncell]);
+        {
+            std::vector<int> fill(cell_off.begin(), cell_off.end() - 1);
+            for (int i = 0; i < n; ++i)
+                for (int cy = span[i].y; cy <= span[i].w; ++cy)
+                    for (int cx = span[i].x; cx <= span[i].z; ++cx) cell_box[fill[(size_t)cy * gnx + cx]++] = i;
+        }
         // v is sorted by descending score, so pair(i, j) with i < j only ever deletes j: i is decided by the pairs
         // (i', i), i' < i, with overlapping boxes.  Overlapping boxes share a grid cell, so the sets of boxes
         // connected through shared cells are closed under the overlap relation and independent of each other; they
@@ -271,9 +284,9 @@ void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
         std::vector<int> root(n);
         for (int i = 0; i < n; ++i) root[i] = i;
         auto find = [&](int x) { while (root[x] != x) { root[x] = root[root[x]]; x = root[x]; } return x; };
-        for (const std::vector<int>& g : grid)
-            for (size_t k = 1; k < g.size(); ++k) {
-                const int a = find(g[0]), b = find(g[k]);
+        for (size_t c = 0; c < ncell; ++c)
+            for (int k = cell_off[c] + 1; k < cell_off[c + 1]; ++k) {
+                const int a = find(cell_box[cell_off[c]]), b = find(cell_box[k]);
                 if (a != b) root[std::max(a, b)] = std::min(a, b);
             }
         std::vector<int> comp_of(n, -1), comp_off, members, comp_size;
@@ -296,10 +309,12 @@ void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
                 const int i = members[k];
                 if (v[i].del) continue;
                 nb.clear();
-                for (int cy = cell(box[4 * i + 1], sy, gy0, gny); cy <= cell(box[4 * i + 3], sy, gy0, gny); ++cy)
-                    for (int cx = cell(box[4 * i], sx, gx0, gnx); cx <= cell(box[4 * i + 2], sx, gx0, gnx); ++cx)
-                        for (int j : grid[(size_t)cy * gnx + cx])
-                            if (j > i) nb.push_back(j);
+                for (int cy = span[i].y; cy <= span[i].w; ++cy)
+                    for (int cx = span[i].x; cx <= span[i].z; ++cx) {
+                        const size_t c = (size_t)cy * gnx + cx;
+                        for (int k = cell_off[c]; k < cell_off[c + 1]; ++k)
+                            if (cell_box[k] > i) nb.push_back(cell_box[k]);
+                    }
                 std::sort(nb.begin(), nb.end());
                 nb.erase(std::unique(nb.begin(), nb.end()), nb.end());
                 for (int j : nb)

@@ -86,6 +86,29 @@ __device__ __forceinline__ float ccoeff(double num, double wsum, double wsq, dou
 // are all issued before the first use; columns outside the image are then patched in LDS with reflect-101.
 // Horizontal [1 4 6 4 1]: h = dot4(0x04060401, 4 bytes) + 5th byte with v_dot4_u32_u8; vertical sum of 5 rows,
 // (v + 128) >> 8, four output bytes per dword store.  Exact integer arithmetic.
+// XCD-aware work placement (cdna_hip_programming.md T1; a speed choice only, never a correctness one): blocks that
+// share an XCD (the same blockIdx % 8 group) take neighbouring work units, so the source lines that neighbouring
+// units share are fetched into one L2 instead of up to eight.
+// xcd_remap: bijection of [0, n) placing each group's blocks on one contiguous range of virtual ids.
+__device__ __forceinline__ int xcd_remap(int b, int n) {
+    const int q = n >> 3, r = n & 7, x = b & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+// xcd_split: the n work units of a 1-D grid-stride loop cut into one contiguous range per group, in proportion to the
+// group's block count; this block is block k of nk in its group.
+struct XcdSplit { int lo, hi, k, nk; };
+__device__ __forceinline__ XcdSplit xcd_split(int n) {
+    const int G = gridDim.x, b = blockIdx.x, x = b & 7, q = G >> 3, r = G & 7;
+    const int nk = q + (x < r ? 1 : 0);
+    const int first = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;   // group's first virtual block
+    XcdSplit s;
+    s.lo = (int)((int64_t)n * first / G);
+    s.hi = (int)((int64_t)n * (first + nk) / G);
+    s.k = b >> 3;
+    s.nk = nk;
+    return s;
+}
+
 constexpr int PD_OW = 128, PD_OH = 32;
 constexpr int PD_IW = 2 * PD_OW + 32, PD_IH = 2 * PD_OH + 4;   // 288 x 68 bytes
 constexpr uint32_t PD_K = 0x04060401u;                         // bytes {1, 4, 6, 4}
@@ -97,10 +120,15 @@ __global__ __launch_bounds__(256) void k_pyr_down(const uint8_t* __restrict__ sr
                                                   int dp, size_t d_img) {
     __shared__ __attribute__((aligned(16))) uint8_t tin[PD_IH][PD_IW];
     __shared__ __attribute__((aligned(16))) uint16_t hs[PD_IH][PD_OW];
-    src += (size_t)blockIdx.z * s_img;
-    dst += (size_t)blockIdx.z * d_img;
+    // tiles in row-major order per image, XCD groups on contiguous tile ranges (horizontal neighbours share the
+    // 16-byte halo columns' cache lines)
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int t = xcd_remap(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
+    const int bx = t % gx, byz = t / gx, by = byz % gy, bz = byz / gy;
+    src += (size_t)bz * s_img;
+    dst += (size_t)bz * d_img;
     const int tid = threadIdx.x;
-    const int ox0 = blockIdx.x * PD_OW, oy0 = blockIdx.y * PD_OH;
+    const int ox0 = bx * PD_OW, oy0 = by * PD_OH;
     const int ix0 = 2 * ox0 - 16;   // tin column 0 <-> source column ix0 (16-byte aligned)
     const int iy0 = 2 * oy0 - 2;    // tin row 0    <-> source row iy0 (reflected)
     constexpr int Q = PD_IW / 16;   // 18 uint4 per row
@@ -1458,12 +1486,15 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
     const int per_roi = txn * tyn;
     const int tasks = roi_count(a) * per_roi;
     const int lr = lane >> 3, lg = lane & 7;   // lane -> rows lr + 8i, columns 4*lg .. 4*lg+3
-    const int tstride = gridDim.x * 4;
+    // XCD groups take contiguous task ranges: a tile's neighbours (overlapping footprints) and the candidate's other
+    // angle ROIs (nearly the same source region) are staged through one L2
+    const XcdSplit xs = xcd_split(tasks);
+    const int tstride = xs.nk * 4;
     WarpTask nxt;
     uint64_t st_acc[3] = {0, 0, 0}, st_t = 0;   // ABL 9: per-wave cycles in task loads / staging / gathers
     int st_n = 0;
-    if (PF) warp_task_load(a, blockIdx.x * 4 + wv, tasks, per_roi, txn, RW, RH, lr, lg, nxt);
-    for (int task = blockIdx.x * 4 + wv; task < tasks; task += tstride) {
+    if (PF) warp_task_load(a, xs.lo + xs.k * 4 + wv, xs.hi, per_roi, txn, RW, RH, lr, lg, nxt);
+    for (int task = xs.lo + xs.k * 4 + wv; task < xs.hi; task += tstride) {
         if (ABL == 9) {   // the previous task's gathers + stores end here
             const uint64_t t = __builtin_readcyclecounter();
             if (st_n > 0) st_acc[2] += t - st_t;
@@ -1479,10 +1510,10 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
         WarpTask cur;
         if (PF) {
             cur = nxt;
-            warp_task_load(a, task + tstride, tasks, per_roi, txn, RW, RH, lr, lg, nxt);
+            warp_task_load(a, task + tstride, xs.hi, per_roi, txn, RW, RH, lr, lg, nxt);
             asm volatile("" ::: "memory");   // keep the prefetch here, ahead of this task's work
         } else {
-            warp_task_load(a, task, tasks, per_roi, txn, RW, RH, lr, lg, cur);
+            warp_task_load(a, task, xs.hi, per_roi, txn, RW, RH, lr, lg, cur);
         }
         const int4 dsc = cur.dsc, A = cur.A, B = cur.B;
         const int* X0r = cur.X0r;
@@ -1700,7 +1731,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const int nwr = (RW + 3) >> 2;                             // words holding ROI pixels
     const int g = lane >> 4, n = lane & 15;
     const int mt = wv & 1, nt = mt + (wv >> 1);                // this wave's (M, N) tile pair
-    for (int item = blockIdx.x; item < items; item += gridDim.x) {
+    const XcdSplit xs = xcd_split(items);   // an ROI's bands (overlapping rows) on one XCD group
+    for (int item = xs.lo + xs.k; item < xs.hi; item += xs.nk) {
         const int slot = item / nband, band = item - slot * nband;
         const int T0 = band * kBandRows, rb = min(kBandRows, th - T0), nsrc = rb + 6;
         __syncthreads();   // previous item done with SB / wi
