@@ -17,5 +17,7 @@ for k, v in sorted(d["kernels"].items(), key=lambda x: -x[1]["ms_total"]):
     print(f"{k:12s} {v['ms_total'] / st * 1000:8.1f} us/step {v['launches'] // st} launches {v['bytes'] / v['ms_total'] / 1e6:8.1f} GB/s")
 print("total us/step", sum(v["ms_total"] for v in d["kernels"].values()) / st * 1000)
 PY
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d $OUT/trace_$TAG -o run --output-format csv -- python3 $ROOT/bench.py --kernel-pass-only --steps 5 > /dev/null 2> $OUT/trace_$TAG.log || exit $?
+cd $ROOT && python3 scripts/step_timeline.py $(find $OUT/trace_$TAG -name '*kernel_trace.csv' | head -1)
 if [ -x build/merge_stages ]; then FPM_HOST_THREADS=1 ./build/merge_stages build/merge_src10_180.bin | tail -1; FPM_HOST_THREADS=8 ./build/merge_stages build/merge_src10_180.bin | tail -1; fi
 exit 0

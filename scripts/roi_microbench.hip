@@ -27,8 +27,13 @@ __global__ __launch_bounds__(256) void k_stream_copy(const uint4* __restrict__ s
 }
 
 int main(int argc, char** argv) {
-    const int W = 4024, H = 3036, P = 4096, TW = 762, TH = 521, TP = 832;
-    const int nsrc = 8, ncand = 11, n3 = 3;
+    // problem shape (defaults: Src7 layer 0); MB_W / MB_H / MB_P / MB_TW / MB_TH / MB_NSRC override (layer-1 shape:
+    // MB_W=2012 MB_H=1518 MB_P=2048 MB_TW=381 MB_TH=261); MB_WARP_ONLY=1 stops after the warp section
+    auto envi = [](const char* k, int d) { const char* v = getenv(k); return v ? atoi(v) : d; };
+    const int W = envi("MB_W", 4024), H = envi("MB_H", 3036), P = envi("MB_P", 4096), TW = envi("MB_TW", 762),
+              TH = envi("MB_TH", 521), TP = (TW + 70) / 64 * 64 + 64;
+    const int nsrc = envi("MB_NSRC", 8), ncand = 11, n3 = 3;
+    const float sc = W / 4024.f;
     const int reps = argc > 1 ? atoi(argv[1]) : 20;
     std::vector<uint8_t> img((size_t)P * (H + 1) * nsrc), tm((size_t)TP * (TH + 1));
     srand(1);
@@ -43,7 +48,7 @@ int main(int argc, char** argv) {
     std::vector<int> live(C);
     std::vector<AngleNode> nodes(C * n3);
     for (int i = 0; i < C; ++i) {
-        st[i].lt = f2(300.f + 137.f * (i % 11), 200.f + 91.f * (i % 7));
+        st[i].lt = f2(sc * (300.f + 137.f * (i % 11)), sc * (200.f + 91.f * (i % 7)));
         st[i].lt.x /= 2; st[i].lt.y /= 2;
         st[i].node = i; st[i].alive = 1; st[i].reached0 = 1;
         live[i] = i;
@@ -131,7 +136,9 @@ int main(int argc, char** argv) {
             CK(hipFree(d_st));
         }
         timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 3>), dim3(grid), dim3(256), 0, 0, a); }, "warp tables only");
+        printf("tiles %ld\n", tiles);
     }
+    if (envi("MB_WARP_ONLY", 0)) return 0;
     timeit([&] { launch_roi_corr(a, 0); }, "prod corr");
     timeit([&] { launch_roi_eval(a, 0); }, "prod eval");
     {
