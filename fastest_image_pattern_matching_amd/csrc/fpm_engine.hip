@@ -1282,7 +1282,8 @@ int fpm_op_pyr_down(fpm_ctx* ctx, const uint8_t* src, int32_t w, int32_t h, size
     HIP_TRY(ctx->d_op_a.ensure((size_t)sp * (h + 1)));
     HIP_TRY(ctx->d_op_b.ensure((size_t)dp * (dh + 1)));
     HIP_TRY(hipMemcpy2DAsync(ctx->d_op_a.p, sp, src, ss, w, h, hipMemcpyHostToDevice, ctx->stream));
-    launch_pyr_down(ctx->d_op_a.as<uint8_t>(), w, h, sp, 0, ctx->d_op_b.as<uint8_t>(), dw, dh, dp, 0, 1, ctx->stream);
+    // 3-chunk segments: every image taller than 64 output rows goes through the carried-window path
+    launch_pyr_down(ctx->d_op_a.as<uint8_t>(), w, h, sp, 0, ctx->d_op_b.as<uint8_t>(), dw, dh, dp, 0, 1, ctx->stream, 3);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpy2DAsync(dst, ds, ctx->d_op_b.p, dp, dw, dh, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));

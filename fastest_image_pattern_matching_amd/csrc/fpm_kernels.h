@@ -150,8 +150,10 @@ struct PackArgs {
 };
 
 // launchers (stream-ordered, no synchronisation)
+// seg_chunks > 0 forces that many 32-row chunks per workgroup (the op entry point uses it so single images exercise
+// the carried-window path); 0 = sized for the grid
 void launch_pyr_down(const uint8_t* src, int sw, int sh, int sp, size_t s_img, uint8_t* dst, int dw, int dh,
-                     int dp, size_t d_img, int nimg, hipStream_t st);
+                     int dp, size_t d_img, int nimg, hipStream_t st, int seg_chunks = 0);
 void launch_warp(const WarpJob* jobs, int njobs, int max_pixels, hipStream_t st);
 void launch_ncc_map(const NccJob* jobs, int njobs, int max_out, int tmpl_bytes, hipStream_t st);
 bool ncc_tile_fits(int tw, int th);   // LDS-tiled variant applies (templates up to 128 x 64)

@@ -221,10 +221,132 @@ __global__ __launch_bounds__(256) void k_pyr_down(const uint8_t* __restrict__ sr
     }
 }
 
+// ---- K1, streaming form (the product's): one workgroup = a strip of PD_OW output columns x a segment of output
+// rows, walked down in chunks of PD_OH output rows.  The 4 input rows two chunks share are carried as horizontal
+// sums (no re-read), and the next chunk's 64 input rows are loaded into registers while the current chunk is
+// filtered and stored, so every workgroup keeps its loads in flight for its whole life instead of one burst per
+// tile (the one-tile form above reaches 3.2-4.2 TB/s: its workgroups wait for their single burst).  Same integer
+// arithmetic as k_pyr_down, exact.
+constexpr int PS_NL = (PD_IH * (PD_IW / 16) + 255) / 256;   // 16-byte loads per thread for a 68-row window: 5
+
+__global__ __launch_bounds__(256) void k_pyr_down_s(const uint8_t* __restrict__ src, int sw, int sh, int sp,
+                                                    size_t s_img, uint8_t* __restrict__ dst, int dw, int dh,
+                                                    int dp, size_t d_img, int seg_rows) {
+    __shared__ __attribute__((aligned(16))) uint8_t tin[PD_IH][PD_IW];
+    __shared__ __attribute__((aligned(16))) uint16_t hs[PD_IH][PD_OW];
+    // (strip, segment, image) in row-major order, XCD groups on contiguous ranges (neighbouring strips share the
+    // halo columns' lines)
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int t = xcd_remap(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
+    const int bx = t % gx, byz = t / gx, by = byz % gy, bz = byz / gy;
+    src += (size_t)bz * s_img;
+    dst += (size_t)bz * d_img;
+    const int tid = threadIdx.x;
+    const int ox0 = bx * PD_OW;
+    const int oy_begin = by * seg_rows, oy_end = min(dh, oy_begin + seg_rows);
+    if (oy_begin >= oy_end) return;   // uniform per workgroup
+    const int ix0 = 2 * ox0 - 16;     // tin column 0 <-> source column ix0 (16-byte aligned)
+    constexpr int Q = PD_IW / 16;     // 18 uint4 per row
+    auto srow = [&](int y) {          // one reflection covers every row an output needs (-2 .. sh+1)
+        y = y < 0 ? -y : y;
+        y = y >= sh ? 2 * sh - 2 - y : y;
+        return y < 0 ? 0 : (y >= sh ? sh - 1 : y);
+    };
+    uint4 v[PS_NL];
+    // window rows [roff, roff + nrows) <- input rows iy .. iy + nrows - 1, element i = tid + 256k -> (i / Q, i % Q)
+    auto issue = [&](int iy, int nrows) {
+#pragma unroll
+        for (int k = 0; k < PS_NL; ++k) {
+            const int i = tid + 256 * k;
+            const int r = i / Q, c = i - r * Q;
+            const int x = ix0 + 16 * c;
+            v[k] = make_uint4(0, 0, 0, 0);
+            if (r < nrows && x >= 0 && x + 16 <= sp) v[k] = *(const uint4*)(src + (size_t)srow(iy + r) * sp + x);
+        }
+    };
+    auto commit = [&](int roff, int nrows) {
+#pragma unroll
+        for (int k = 0; k < PS_NL; ++k) {
+            const int i = tid + 256 * k;
+            const int r = i / Q, c = i - r * Q;
+            if (r < nrows) *(uint4*)&tin[roff + r][16 * c] = v[k];
+        }
+    };
+    // columns outside [0, sw) that an output of this strip reads (at most 2 on each side): reflect-101
+    const int xlo = 2 * ox0 - 2, xhi = min(2 * (ox0 + PD_OW - 1) + 2, 2 * (dw - 1) + 2);
+    const bool edge = xlo < 0 || xhi >= sw;   // uniform per workgroup
+    issue(2 * oy_begin - 2, PD_IH);
+    for (int oyc = oy_begin; oyc < oy_end; oyc += PD_OH) {
+        const bool first = oyc == oy_begin;
+        const int roff = first ? 0 : 4, nrows = first ? PD_IH : 2 * PD_OH;
+        const int iy = 2 * oyc - 2 + roff;
+        commit(roff, nrows);
+        if (edge) {
+            __syncthreads();   // the 16-byte tile stores above cover the patched bytes
+            for (int i = tid; i < nrows * 4; i += 256) {
+                const int r = i >> 2, k = i & 3;
+                const int x = k < 2 ? xlo + k : xhi - (k - 2);   // xlo, xlo+1, xhi, xhi-1
+                if ((x < 0 && k < 2) || (x >= sw && k >= 2))
+                    tin[roff + r][x - ix0] = src[(size_t)srow(iy + r) * sp + reflect101(x, sw)];
+            }
+        }
+        __syncthreads();
+        // the next chunk's 64 new input rows (its window rows 4..67) are in flight while this chunk is filtered
+        if (oyc + PD_OH < oy_end) issue(2 * oyc + 2 * PD_OH + 2, 2 * PD_OH);
+        // horizontal [1 4 6 4 1] of the new window rows: 4 consecutive outputs per item (as k_pyr_down)
+        const int nh = nrows * (PD_OW / 4);
+        for (int i = tid; i < nh; i += 256) {
+            const int r = roff + i / (PD_OW / 4), g = i % (PD_OW / 4);
+            const uint32_t* w = (const uint32_t*)&tin[r][8 * g + 12];
+            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
+            const uint32_t h0 = __builtin_amdgcn_udot4(PD_K, __builtin_amdgcn_alignbyte(w1, w0, 2), 0, false) + ((w1 >> 16) & 0xff);
+            const uint32_t h1 = __builtin_amdgcn_udot4(PD_K, w1, 0, false) + (w2 & 0xff);
+            const uint32_t h2 = __builtin_amdgcn_udot4(PD_K, __builtin_amdgcn_alignbyte(w2, w1, 2), 0, false) + ((w2 >> 16) & 0xff);
+            const uint32_t h3 = __builtin_amdgcn_udot4(PD_K, w2, 0, false) + (w3 & 0xff);
+            uint2 o;
+            o.x = h0 | (h1 << 16);
+            o.y = h2 | (h3 << 16);
+            *(uint2*)&hs[r][4 * g] = o;
+        }
+        __syncthreads();
+        // vertical: 4 consecutive outputs of one row per item
+#pragma unroll
+        for (int k = 0; k < PD_OH * (PD_OW / 4) / 256; ++k) {
+            const int i = tid + 256 * k;
+            const int orow = i / (PD_OW / 4), g = i - orow * (PD_OW / 4);
+            const int oy = oyc + orow, ox = ox0 + 4 * g;
+            if (oy >= oy_end || ox >= dw) continue;
+            uint32_t acc[4] = {128, 128, 128, 128};
+            const int kw[5] = {1, 4, 6, 4, 1};
+#pragma unroll
+            for (int tt = 0; tt < 5; ++tt) {
+                const uint2 q = *(const uint2*)&hs[2 * orow + tt][4 * g];
+                acc[0] += kw[tt] * (q.x & 0xffff); acc[1] += kw[tt] * (q.x >> 16);
+                acc[2] += kw[tt] * (q.y & 0xffff); acc[3] += kw[tt] * (q.y >> 16);
+            }
+            uint8_t* d = dst + (size_t)oy * dp + ox;
+            if (ox + 4 <= dw) {
+                *(uint32_t*)d = (acc[0] >> 8) | ((acc[1] >> 8) << 8) | ((acc[2] >> 8) << 16) | ((acc[3] >> 8) << 24);
+            } else {
+                for (int j = 0; j < dw - ox; ++j) d[j] = (uint8_t)(acc[j] >> 8);
+            }
+        }
+        __syncthreads();
+        // carry: window rows 64..67 (input rows 2 * (oyc + PD_OH) - 2 .. + 1) are the next window's rows 0..3
+        ((uint32_t*)hs[tid >> 6])[tid & 63] = ((uint32_t*)hs[2 * PD_OH + (tid >> 6)])[tid & 63];
+        __syncthreads();
+    }
+}
+
 void launch_pyr_down(const uint8_t* src, int sw, int sh, int sp, size_t s_img, uint8_t* dst, int dw, int dh,
-                     int dp, size_t d_img, int nimg, hipStream_t st) {
-    dim3 grid((dw + PD_OW - 1) / PD_OW, (dh + PD_OH - 1) / PD_OH, nimg);
-    hipLaunchKernelGGL(k_pyr_down<0>, grid, dim3(256), 0, st, src, sw, sh, sp, s_img, dst, dw, dh, dp, d_img);
+                     int dp, size_t d_img, int nimg, hipStream_t st, int seg_chunks) {
+    // segments of whole chunks, as many chunks per workgroup as keeps ~2048 workgroups (2 rounds of 4 per CU)
+    const int gx = (dw + PD_OW - 1) / PD_OW, chunks = (dh + PD_OH - 1) / PD_OH;
+    const long units = (long)gx * chunks * nimg;
+    const int per = seg_chunks > 0 ? seg_chunks : (int)std::max(1L, std::min((long)chunks, units / 2048));
+    const int seg_rows = per * PD_OH;
+    dim3 grid(gx, (dh + seg_rows - 1) / seg_rows, nimg);
+    hipLaunchKernelGGL(k_pyr_down_s, grid, dim3(256), 0, st, src, sw, sh, sp, s_img, dst, dw, dh, dp, d_img, seg_rows);
 }
 
 // ============================================================================================== K2
@@ -1956,15 +2078,21 @@ __global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
             stage_block4(FT, gftw, lvl + (size_t)gby0 * a.P + gbxa, a.P, gfth, wpr, gbxa, a.P, tid, 256);
             __syncthreads();
             STAMP(8);
+            // thread -> one fixed group of 4 columns (its column table entries held in registers) and every
+            // nrl-th row: no per-item division, 2 table reads per 4 pixels instead of 10
             const int ngrp = (RW + 3) >> 2;
-            for (int i = tid; i < RH * ngrp; i += 256) {   // thread -> (row, 4 columns)
-                const int r = i / ngrp, c0 = 4 * (i - r * ngrp);
+            const int nrl = 256 / ngrp;                   // row lanes (>= 1: RW <= 1024 for this kernel)
+            const int rl = tid / ngrp, c0 = 4 * (tid - rl * ngrp);
+            int ad4[4], bd4[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) { ad4[u] = lad[c0 + u]; bd4[u] = lbd[c0 + u]; }
+            for (int r = rl < nrl ? rl : RH; r < RH; r += nrl) {
                 const int X0 = lx0[r], Y0 = ly0[r];
                 uint32_t pk = 0;
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    const int X = (X0 + lad[c0 + u]) >> (kAbBits - kInterBits);
-                    const int Y = (Y0 + lbd[c0 + u]) >> (kAbBits - kInterBits);
+                    const int X = (X0 + ad4[u]) >> (kAbBits - kInterBits);
+                    const int Y = (Y0 + bd4[u]) >> (kAbBits - kInterBits);
                     int v;
                     if (g_interior) {
                         const int off = mad24(Y >> kInterBits, gftw, (X >> kInterBits) - gobase);
