@@ -109,6 +109,10 @@ __device__ __forceinline__ XcdSplit xcd_split(int n) {
     return s;
 }
 
+#ifndef FPM_FT_PITCH_FORCE
+#define FPM_FT_PITCH_FORCE 0
+#endif
+
 constexpr int PD_OW = 128, PD_OH = 32;
 constexpr int PD_IW = 2 * PD_OW + 32, PD_IH = 2 * PD_OH + 4;   // 288 x 68 bytes
 constexpr uint32_t PD_K = 0x04060401u;                         // bytes {1, 4, 6, 4}
@@ -1550,6 +1554,9 @@ __global__ __launch_bounds__(256) void k_roi_tables(RoiArgs a) {
             const int bxa = bx0 & ~3;
             int ftw = any ? ((bx1 - bxa + 4) & ~3) : 0;
             if (((ftw >> 2) & 1) == 0) ftw += 4;    // odd dword pitch: spread gather banks
+#if FPM_FT_PITCH_FORCE > 0   // profiling builds only (scripts/roi_microbench.hip): a fixed pitch in dwords
+            if (any && ftw <= 4 * FPM_FT_PITCH_FORCE) ftw = 4 * FPM_FT_PITCH_FORCE;
+#endif
             const int fth = any ? by1 - by0 + 1 : 0;
             const bool in_lds = (ftw >> 2) <= 16 && ftw * fth <= ROI_FT;
             a.tdesc[(size_t)slot * a.tdesc_stride + i] =
