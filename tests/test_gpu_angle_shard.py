@@ -70,6 +70,19 @@ def test_angle_shard_parity(hip, templates, case):
     assert len(orc) >= 1
 
 
+@pytest.mark.parametrize("seed", range(0, 150, 6))
+def test_angle_shard_fuzz(hip, seed):
+    """Every sixth randomized case of tests/test_gpu_fuzz.py (template crops, border-straddling targets, every
+    parameter) split over 3 angle shards: shard records = the oracle's records of the block, merge = the search.
+    Tolerance 0 gives one angle, so two of the three shards are empty."""
+    from tests.test_gpu_fuzz import _case
+    s, t, prm = _case(seed)
+    o = oracle.OracleMatcher().set(**prm)
+    assert o.learnPattern(t)
+    _setup(hip, t, prm)
+    _check(hip, o, s, t, (3,), f"fuzz{seed}")
+
+
 def test_angle_shard_src7(hip, templates):
     """configs[1] (Src7 4024x3036, +-180, TargetNum 3; 41 top angles) over 8 angle shards."""
     s, t = synth.src7_scene(templates["Dst7"])

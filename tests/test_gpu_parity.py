@@ -248,6 +248,26 @@ def test_batch_equals_single(hip, templates):
         assert_same_results(batch[k], o.match(s), f"batch{k}")
 
 
+def test_src7_batch_multichunk_pyramid(hip, templates):
+    """configs[1] as a batch of 6 full-size sources: the batched pyrDown launch walks several 32-row chunks per
+    workgroup (k_pyr_down_s's carried window at the sizes the bench runs), and every source's search equals the
+    oracle's."""
+    t = templates["Dst7"]
+    srcs = [synth.src7_scene(t, seed=7 + 13 * k)[0] for k in range(6)]
+    o = oracle.OracleMatcher().set(max_pos=3, tolerance_angle=180.0, score=0.7)
+    o.learnPattern(t)
+    hip.resetParams()
+    hip.setMaxPositions(3)
+    hip.setToleranceAngle(180.0)
+    hip.setScore(0.7)
+    assert hip.learnPattern(t)
+    batch = hip.match_batch(srcs)
+    for k, s in enumerate(srcs):
+        orc = o.match(s)
+        assert_same_results(batch[k], orc, f"src7_batch{k}")
+        assert len(orc) == 3
+
+
 def test_concurrent_contexts(hip, templates, gpu_matcher_factory):
     """Two contexts (two HIP streams) with searches in flight at once (fpm_match_staged_launch / _finish) give
     the oracle's results; staging or a second launch while a search is in flight is refused."""
