@@ -1839,10 +1839,43 @@ __device__ __forceinline__ void band_mfma_ga(const int8_t* ap, const uint8_t* bp
     acc[0] = c0; acc[1] = c1; acc[2] = c2; acc[3] = c3; acc[4] = c4; acc[5] = c5; acc[6] = c6;
 }
 
+// The same with this wave's A fragments held in registers (k_roi_corr's register-A form): the loop reads only LDS.
+template <int NK>
+__device__ __forceinline__ void band_mfma_regs(const fpm_v4i* A, const uint8_t* bp, int nk, fpm_v4i acc[7]) {
+    fpm_v4i c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0, c4 = c0, c5 = c0, c6 = c0;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+        if (k >= nk) continue;
+        const fpm_v4i av = A[k];
+        const uint8_t* bk = (const uint8_t*)__builtin_assume_aligned(bp + 64 * k, 16);
+        const uint4 lo = *(const uint4*)bk;
+        const uint2 hi = *(const uint2*)(bk + 16);
+        const uint32_t w0 = lo.x, w1 = lo.y, w2 = lo.z, w3 = lo.w, w4 = hi.x, w5 = hi.y;
+        const uint32_t a10 = __builtin_amdgcn_alignbyte(w1, w0, 1), a21 = __builtin_amdgcn_alignbyte(w2, w1, 1),
+                       a32 = __builtin_amdgcn_alignbyte(w3, w2, 1), a43 = __builtin_amdgcn_alignbyte(w4, w3, 1),
+                       a54 = __builtin_amdgcn_alignbyte(w5, w4, 1);
+        const uint32_t b10 = __builtin_amdgcn_alignbyte(w1, w0, 2), b21 = __builtin_amdgcn_alignbyte(w2, w1, 2),
+                       b32 = __builtin_amdgcn_alignbyte(w3, w2, 2), b43 = __builtin_amdgcn_alignbyte(w4, w3, 2),
+                       b54 = __builtin_amdgcn_alignbyte(w5, w4, 2);
+        const uint32_t e10 = __builtin_amdgcn_alignbyte(w1, w0, 3), e21 = __builtin_amdgcn_alignbyte(w2, w1, 3),
+                       e32 = __builtin_amdgcn_alignbyte(w3, w2, 3), e43 = __builtin_amdgcn_alignbyte(w4, w3, 3);
+        c0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)w0, (int)w1, (int)w2, (int)w3}, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)a10, (int)a21, (int)a32, (int)a43}, c1, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)b10, (int)b21, (int)b32, (int)b43}, c2, 0, 0, 0);
+        c3 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)e10, (int)e21, (int)e32, (int)e43}, c3, 0, 0, 0);
+        c4 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)w1, (int)w2, (int)w3, (int)w4}, c4, 0, 0, 0);
+        c5 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)a21, (int)a32, (int)a43, (int)a54}, c5, 0, 0, 0);
+        c6 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, fpm_v4i{(int)b21, (int)b32, (int)b43, (int)b54}, c6, 0, 0, 0);
+    }
+    acc[0] = c0; acc[1] = c1; acc[2] = c2; acc[3] = c3; acc[4] = c4; acc[5] = c5; acc[6] = c6;
+}
+
 // MODE (profiling ablations in scripts/roi_microbench.hip; the product uses 0): 2 = no MFMA loop, 3 = no staging
-// GA: A operand read from the global i8 slab (no template rows in LDS); WPE: register cap (waves per SIMD)
-template <int MODE, bool GA, int WPE>
+// GA: A operand read from the global i8 slab (no template rows in LDS); WPE: register cap (waves per SIMD);
+// NK > 0: register-A form (A fragments of nk <= NK k-steps held per wave, band-major item runs; needs GA)
+template <int MODE, bool GA, int WPE, int NK = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_corr(RoiArgs a) {
+    static_assert(NK == 0 || (GA && MODE == 0), "the register-A form stages no template rows");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tw = a.tw, th = a.th, RW = tw + 6;
     const int SBp = a.roi_pitch;
@@ -1855,22 +1888,76 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     uint32_t* wq = wi + kBandSrc * 7;                          // [row][dx] window sums of I^2
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int nband = (th + kBandRows - 1) / kBandRows;
-    const int items = roi_count(a) * nband;
+    const int rois = roi_count(a), items = rois * nband;
     const int q4 = SBp >> 4;                                   // 16-byte columns per row
     const int nwr = (RW + 3) >> 2;                             // words holding ROI pixels
     const int g = lane >> 4, n = lane & 15;
     const int mt = wv & 1, nt = mt + (wv >> 1);                // this wave's (M, N) tile pair
-    const XcdSplit xs = xcd_split(items);   // an ROI's bands (overlapping rows) on one XCD group
-    for (int item = xs.lo + xs.k; item < xs.hi; item += xs.nk) {
-        const int slot = item / nband, band = item - slot * nband;
+    const int txn = (RW + ROI_T - 1) / ROI_T;
+    const XcdSplit xs = xcd_split(items);   // the XCD group's contiguous range of items
+    // NK = 0: items slot-major (an ROI's bands, which share rows, on one XCD group), grid-stride over the range.
+    // NK > 0 (register-A form): items band-major (item = band * rois + slot) and each workgroup takes one
+    // contiguous run of its group's range, so consecutive items share their template band: the wave loads its A
+    // fragments once per band and the MFMA loop reads only LDS; the next item's ROI rows are loaded into
+    // registers while the current item computes, so staging costs one LDS store per item.
+    int it_lo = xs.lo + xs.k, it_hi = xs.hi, it_step = xs.nk;
+    if (NK > 0) {
+        const int64_t span = xs.hi - xs.lo;
+        it_lo = xs.lo + (int)(span * xs.k / xs.nk);
+        it_hi = xs.lo + (int)(span * (xs.k + 1) / xs.nk);
+        it_step = 1;
+    }
+    constexpr int NA = NK > 0 ? NK : 1;
+    fpm_v4i Areg[NA];
+#pragma unroll
+    for (int k = 0; k < NA; ++k) Areg[k] = fpm_v4i{0, 0, 0, 0};
+    int a_band = -1;
+    uint4 pv[kStageRows];
+    const int lc = min(lane, 2 * txn - 1);   // an in-bounds chunk for lanes past the ROI width (zeroed when stored)
+    auto load_rows = [&](int it) {           // unconditional loads: rows past the band repeat its last row
+        const int bd = it / rois, sl = it - bd * rois;
+        const int T0n = bd * kBandRows, nsn = min(kBandRows, th - T0n) + 6;
+        const uint8_t* rsrc = a.roi + (size_t)sl * a.roi_stride;
+#pragma unroll
+        for (int i = 0; i < kStageRows; ++i) {
+            const int R = T0n + min(wv + 4 * i, nsn - 1);
+            pv[i] = *(const uint4*)(rsrc + ((size_t)((R >> 5) * txn + (lc >> 1)) << 10) + (R & 31) * ROI_T + 16 * (lc & 1));
+        }
+    };
+    if (NK > 0 && it_lo < it_hi) load_rows(it_lo);
+    for (int item = it_lo; item < it_hi; item += it_step) {
+        int slot, band;
+        if (NK > 0) { band = item / rois; slot = item - band * rois; }
+        else { slot = item / nband; band = item - slot * nband; }
         const int T0 = band * kBandRows, rb = min(kBandRows, th - T0), nsrc = rb + 6;
-        __syncthreads();   // previous item done with SB / wi
+        __syncthreads();   // previous item done with SB / rall / wi
         if (tid < kBandSrc) { rall[tid] = 0; rallq[tid] = 0; }
-        __syncthreads();
-        if (MODE != 3) {   // stage: wave wv stages rows wv + 4i (kStageBatch rows' loads in flight), bytes ^ 0x80
+        if (NK > 0) {
+            // this item's rows (loaded during the previous item) ^ 0x80 into LDS; this wave's A fragments when the
+            // band changes (workgroup-uniform); then the next item's row loads
+            const bool in_roi = lane < 2 * txn;
+#pragma unroll
+            for (int i = 0; i < kStageRows; ++i) {
+                const int r = wv + 4 * i;
+                if (r < nsrc && lane < q4) {
+                    uint4 x = in_roi ? pv[i] : make_uint4(0, 0, 0, 0);
+                    x.x ^= 0x80808080u; x.y ^= 0x80808080u; x.z ^= 0x80808080u; x.w ^= 0x80808080u;
+                    *(uint4*)(SB + (size_t)r * SBp + 16 * lane) = x;
+                }
+            }
+            if (band != a_band) {
+                a_band = band;
+                if (kMmaRows * mt < rb) {
+                    const int8_t* ap = a.tmpl8 + (size_t)(T0 + kMmaRows * mt + n) * a.tp8 + 16 * g;
+#pragma unroll
+                    for (int k = 0; k < NA; ++k)
+                        if (k < a.nk) Areg[k] = *(const fpm_v4i*)(ap + 64 * k);
+                }
+            }
+            if (item + 1 < it_hi) load_rows(item + 1);
+        } else if (MODE != 3) {   // stage: wave wv stages rows wv + 4i (kStageBatch rows' loads in flight), ^ 0x80
             // tile-major ROI scratch (k_roi_warp): row R, 16-byte chunk c lives in tile (R >> 5, c >> 1)
             const uint8_t* rsrc = a.roi + (size_t)slot * a.roi_stride;
-            const int txn = (RW + ROI_T - 1) / ROI_T;
             for (int c0 = 0; c0 < q4; c0 += 64) {
                 const int c = c0 + lane;
                 for (int i0 = 0; i0 < kStageRows; i0 += kStageBatch) {
@@ -1941,7 +2028,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             if (sr >= nsrc) sr = 0;   // column outside the band: computed, never stored
             const uint8_t* bp = SB + (size_t)sr * SBp + 16 * g;
             fpm_v4i acc[7];
-            if (GA)
+            if (NK > 0)
+                band_mfma_regs<NA>(Areg, bp, a.nk, acc);
+            else if (GA)
                 band_mfma_ga(a.tmpl8 + (size_t)(T0 + kMmaRows * mt + n) * a.tp8 + 16 * g, bp, a.nk, acc);
             else
                 band_mfma(TB + (size_t)(kMmaRows * mt + n) * TBp + 16 * g, bp, a.nk, acc);
@@ -2507,9 +2596,29 @@ void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
 
 constexpr bool kCorrGlobalA = true;   // measured in scripts/roi_microbench.hip
 constexpr int kCorrWaves = 3;
+// register-A form: 2 waves per SIMD (its A fragments + prefetched rows need > 168 VGPRs), one workgroup per resident
+// slot (MI355X: 256 CUs)
+constexpr int kCorrRunWaves = 2;
+constexpr int kCorrRunWGs = 256 * kCorrRunWaves;
+template <int NK>
+static void launch_corr_regs(const RoiArgs& a, long items, size_t lds, hipStream_t st) {
+    const int grid = (int)(items < kCorrRunWGs ? items : kCorrRunWGs);
+    hipLaunchKernelGGL((k_roi_corr<0, true, kCorrRunWaves, NK>), dim3(grid), dim3(256), lds, st, a);
+}
 void launch_roi_corr(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0 || a.equal1) return;
     const size_t lds = roi_corr_lds(a.roi_pitch, a.tw, a.rc, kCorrGlobalA);
+    // register-A form where its staged rows fit one 64-lane pass and A fits 16 k-steps (templates 257..1024 wide;
+    // at <= 4 k-steps it measured no faster than the slot-major form); FPM_CORR_SLOTMAJOR=1 forces the slot-major
+    // form (profiling comparisons)
+    static const bool slot_major = getenv("FPM_CORR_SLOTMAJOR") && atoi(getenv("FPM_CORR_SLOTMAJOR")) != 0;
+    if (!slot_major && (a.roi_pitch >> 4) <= 64 && a.nk > 4 && a.nk <= 16 && lds <= 65536) {
+        const long items = (long)a.slot_cap * ((a.th + kBandRows - 1) / kBandRows);
+        if (a.nk <= 8) launch_corr_regs<8>(a, items, lds, st);
+        else if (a.nk <= 12) launch_corr_regs<12>(a, items, lds, st);
+        else launch_corr_regs<16>(a, items, lds, st);
+        return;
+    }
     static size_t lds_attr = 0;
     if (lds > 65536 && lds > lds_attr) {
         (void)hipFuncSetAttribute((const void*)k_roi_corr<0, kCorrGlobalA, kCorrWaves>,
