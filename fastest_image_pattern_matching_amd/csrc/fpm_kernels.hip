@@ -1873,7 +1873,8 @@ __device__ __forceinline__ void band_mfma_regs(const fpm_v4i* A, const uint8_t* 
 // MODE (profiling ablations in scripts/roi_microbench.hip; the product uses 0): 2 = no MFMA loop, 3 = no staging
 // GA: A operand read from the global i8 slab (no template rows in LDS); WPE: register cap (waves per SIMD);
 // NK > 0: register-A form (A fragments of nk <= NK k-steps held per wave, band-major item runs; needs GA)
-template <int MODE, bool GA, int WPE, int NK = 0>
+// PFR (register-A form): prefetch the next item's rows (false: load this item's rows at its start, fewer VGPRs)
+template <int MODE, bool GA, int WPE, int NK = 0, bool PFR = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_corr(RoiArgs a) {
     static_assert(NK == 0 || (GA && MODE == 0), "the register-A form stages no template rows");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1924,7 +1925,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             pv[i] = *(const uint4*)(rsrc + ((size_t)((R >> 5) * txn + (lc >> 1)) << 10) + (R & 31) * ROI_T + 16 * (lc & 1));
         }
     };
-    if (NK > 0 && it_lo < it_hi) load_rows(it_lo);
+    if (NK > 0 && PFR && it_lo < it_hi) load_rows(it_lo);
     for (int item = it_lo; item < it_hi; item += it_step) {
         int slot, band;
         if (NK > 0) { band = item / rois; slot = item - band * rois; }
@@ -1936,6 +1937,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             // this item's rows (loaded during the previous item) ^ 0x80 into LDS; this wave's A fragments when the
             // band changes (workgroup-uniform); then the next item's row loads
             const bool in_roi = lane < 2 * txn;
+            if (!PFR) load_rows(item);
 #pragma unroll
             for (int i = 0; i < kStageRows; ++i) {
                 const int r = wv + 4 * i;
@@ -1954,7 +1956,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                         if (k < a.nk) Areg[k] = *(const fpm_v4i*)(ap + 64 * k);
                 }
             }
-            if (item + 1 < it_hi) load_rows(item + 1);
+            if (PFR && item + 1 < it_hi) load_rows(item + 1);
         } else if (MODE != 3) {   // stage: wave wv stages rows wv + 4i (kStageBatch rows' loads in flight), ^ 0x80
             // tile-major ROI scratch (k_roi_warp): row R, 16-byte chunk c lives in tile (R >> 5, c >> 1)
             const uint8_t* rsrc = a.roi + (size_t)slot * a.roi_stride;
@@ -2596,25 +2598,32 @@ void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
 
 constexpr bool kCorrGlobalA = true;   // measured in scripts/roi_microbench.hip
 constexpr int kCorrWaves = 3;
-// register-A form: 2 waves per SIMD (its A fragments + prefetched rows need > 168 VGPRs), one workgroup per resident
-// slot (MI355X: 256 CUs)
+// register-A form at 13-16 k-steps: 2 waves per SIMD (A fragments + prefetched rows: 221 VGPRs), one workgroup per
+// resident slot (MI355X: 256 CUs)
 constexpr int kCorrRunWaves = 2;
 constexpr int kCorrRunWGs = 256 * kCorrRunWaves;
 template <int NK>
 static void launch_corr_regs(const RoiArgs& a, long items, size_t lds, hipStream_t st) {
-    const int grid = (int)(items < kCorrRunWGs ? items : kCorrRunWGs);
-    hipLaunchKernelGGL((k_roi_corr<0, true, kCorrRunWaves, NK>), dim3(grid), dim3(256), lds, st, a);
+    if constexpr (NK <= 12) {
+        // up to 12 k-steps the A fragments fit 3 waves per SIMD (166 VGPRs) without the row prefetch; measured
+        // faster than the prefetching 2-wave form (occupancy hides the staging latency better)
+        const int grid = (int)(items < 256 * kCorrWaves ? items : 256 * kCorrWaves);
+        hipLaunchKernelGGL((k_roi_corr<0, true, kCorrWaves, NK, false>), dim3(grid), dim3(256), lds, st, a);
+    } else {
+        const int grid = (int)(items < kCorrRunWGs ? items : kCorrRunWGs);
+        hipLaunchKernelGGL((k_roi_corr<0, true, kCorrRunWaves, NK>), dim3(grid), dim3(256), lds, st, a);
+    }
 }
 void launch_roi_corr(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0 || a.equal1) return;
     const size_t lds = roi_corr_lds(a.roi_pitch, a.tw, a.rc, kCorrGlobalA);
-    // register-A form where its staged rows fit one 64-lane pass and A fits 16 k-steps (templates 257..1024 wide;
-    // at <= 4 k-steps it measured no faster than the slot-major form); FPM_CORR_SLOTMAJOR=1 forces the slot-major
-    // form (profiling comparisons)
+    // register-A form where its staged rows fit one 64-lane pass and A fits 16 k-steps (templates <= 1024 wide);
+    // FPM_CORR_SLOTMAJOR=1 forces the slot-major form (profiling comparisons)
     static const bool slot_major = getenv("FPM_CORR_SLOTMAJOR") && atoi(getenv("FPM_CORR_SLOTMAJOR")) != 0;
-    if (!slot_major && (a.roi_pitch >> 4) <= 64 && a.nk > 4 && a.nk <= 16 && lds <= 65536) {
+    if (!slot_major && (a.roi_pitch >> 4) <= 64 && a.nk <= 16 && lds <= 65536) {
         const long items = (long)a.slot_cap * ((a.th + kBandRows - 1) / kBandRows);
-        if (a.nk <= 8) launch_corr_regs<8>(a, items, lds, st);
+        if (a.nk <= 4) launch_corr_regs<4>(a, items, lds, st);
+        else if (a.nk <= 8) launch_corr_regs<8>(a, items, lds, st);
         else if (a.nk <= 12) launch_corr_regs<12>(a, items, lds, st);
         else launch_corr_regs<16>(a, items, lds, st);
         return;
