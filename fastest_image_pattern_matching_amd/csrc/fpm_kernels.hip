@@ -5,9 +5,10 @@
 //   K3+K4 k_ncc_map   matchTemplate(TM_CCORR) + CCOEFF_Denominator   (:177 -> :514, :523, :527-598)
 //   K5  k_nms         minMaxLoc + getNextMaxLoc / s_BlockMax (:179-210, :1196-1221, DataStructures.h:118-246)
 //       k_cand_init   top candidate -> ptLT                (:262-266)
-//   K6+K7+K8 k_roi_corr  getRotatedROI + IM_Conv_SIMD fold + CCOEFF_Denominator + minMaxLoc + 3x3
-//                     (:309-328, :461-512, :527-598) fused: the ROI is sampled into LDS, never stored
-//       k_cand_step   best-of-3 / early break / back-mapping (:331-366) for layers > 0
+//   K6-K8 refinement  getRotatedROI + IM_Conv_SIMD fold + CCOEFF_Denominator + minMaxLoc + 3x3
+//                     (:309-328, :461-512, :527-598): k_roi_tables / k_roi_warp / k_roi_corr (i8 MFMA) / k_roi_eval
+//                     for large templates, k_roi_small (the ROI sampled into LDS, never stored) for small ones
+//       k_cand_step   best-of-3 / early break / back-mapping (:331-366) after k_roi_small
 //
 // Numerics contract: built with -ffp-contract=off, no fast-math; integer sums are exact; the per-row
 // int32 -> f32 fold is sequential in template-row order; the normalisation is IEEE f64 in the reference's
