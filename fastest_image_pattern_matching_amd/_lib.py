@@ -45,8 +45,9 @@ class Params(C.Structure):
         ("use_simd", C.c_int32),
         ("subpixel", C.c_int32),
         ("tolerance_range", C.c_int32),
-        ("reserved0", C.c_int32),
+        ("semantics", C.c_int32),
         ("tolerance", C.c_double * 4),
+        ("top_angle_step", C.c_double),
     ]
 
 

@@ -98,7 +98,7 @@ struct Plan {
     std::vector<size_t> canvas_off, map_off, blk_off;
     std::vector<int> canvas_pitch, map_w, map_h, nblk;
     size_t canvas_bytes = 0, map_floats = 0, blk_count = 0;
-    int max_canvas = 0, max_map = 0, max_nblk = 0;
+    int max_canvas = 0, max_map = 0, max_nblk = 0, max_cells = 0;
     // device buffers owned by the plan
     DevBuf d_ncand, d_ncnt;                    // s_BlockMax candidate lists (k_nms_blocks -> k_nms_fast)
     DevBuf d_canvas, d_map, d_bmax, d_bloc, d_jobs, d_nodes, d_top, d_topn, d_peaks, d_counts, d_state,
@@ -165,6 +165,8 @@ struct fpm_ctx {
     double last_device_ms = 0, last_host_ms = 0, last_call_ms = 0;
     std::chrono::steady_clock::time_point t_call0;
     bool pending = false;    // a staged search is in flight (fpm_match_staged_launch)
+    bool staged = false;     // the source slab holds an fpm_stage_sources batch (fpm_match re-lays it out for one source)
+    fpm_params run_prm{};    // parameters of the search in flight (snapshot at launch; the host tail reads these)
     // per-source candidate records of the last search (collect_candidates; fpm_match_*candidates)
     std::vector<std::vector<fpm_candidate>> cands;
 };
@@ -289,7 +291,8 @@ AngleNode make_node(double angle) {
 bool same_search_params(const fpm_params& a, const fpm_params& b) {
     return a.max_pos == b.max_pos && a.min_reduce_area == b.min_reduce_area && a.max_overlap == b.max_overlap &&
            a.score == b.score && a.tolerance_angle == b.tolerance_angle && a.use_simd == b.use_simd &&
-           a.tolerance_range == b.tolerance_range;
+           a.tolerance_range == b.tolerance_range && a.semantics == b.semantics &&
+           a.top_angle_step == b.top_angle_step && std::equal(a.tolerance, a.tolerance + 4, b.tolerance);
 }
 
 int build_plan(fpm_ctx* ctx) {
@@ -303,10 +306,16 @@ int build_plan(fpm_ctx* ctx) {
     P.shard = ctx->shard; P.shards = ctx->shards;
     const fpm_params& prm = ctx->prm;
     const TmplLevel& tt = ctx->tmpl[L];
-    // angle list (TemplateMatcher.cpp:130-144)
-    const double step = std::atan(2.0 / std::max(tt.w, tt.h)) * kR2D;
+    // angle list (TemplateMatcher.cpp:130-144); the step override is an extension (fpm_params.top_angle_step)
+    const double step = prm.top_angle_step > 0 ? prm.top_angle_step : std::atan(2.0 / std::max(tt.w, tt.h)) * kR2D;
+    const bool mfc = prm.semantics == FPM_SEMANTICS_MFC;
     P.angles.clear();
-    if (prm.tolerance_angle < kVisionTol) {
+    if (mfc && prm.tolerance_range) {   // MFC angle ranges (MatchToolDlg.cpp:805-815)
+        const double* t = prm.tolerance;
+        if (t[0] >= t[1] || t[2] >= t[3]) { ctx->err = "angle ranges need tolerance[0] < [1] and [2] < [3]"; return FPM_E_INVALID_ARG; }
+        for (double a = t[0]; a < t[1] + step; a += step) P.angles.push_back(a);
+        for (double a = t[2]; a < t[3] + step; a += step) P.angles.push_back(a);
+    } else if (prm.tolerance_angle < kVisionTol) {
         P.angles.push_back(0.0);
     } else {
         for (double a = 0; a < prm.tolerance_angle + step; a += step) P.angles.push_back(a);
@@ -334,7 +343,7 @@ int build_plan(fpm_ctx* ctx) {
     P.canvas_pitch.resize(P.nang); P.map_w.resize(P.nang); P.map_h.resize(P.nang); P.nblk.resize(P.nang);
     std::vector<std::array<double, 6>> mats(P.nang);
     size_t co = 0, mo = 0, bo = 0;
-    P.max_canvas = 0; P.max_map = 0; P.max_nblk = 0;
+    P.max_canvas = 0; P.max_map = 0; P.max_nblk = 0; P.max_cells = 0;
     for (int a = 0; a < P.nang; ++a) {
         int bw, bh;
         best_rotation_size(top.w, top.h, tt.w, tt.h, P.angles[a], &bw, &bh);
@@ -359,10 +368,13 @@ int build_plan(fpm_ctx* ctx) {
         P.map_off[a] = mo;
         mo += round_up((size_t)P.map_w[a] * P.map_h[a], (size_t)64);
         int nb = 0;
-        if (P.by_block && ok) {
-            const int ncol = P.map_w[a] / tt.w, nrow = P.map_h[a] / tt.h;
-            const int rw = P.map_w[a] - ncol * tt.w, rh = P.map_h[a] - nrow * tt.h;
-            nb = ncol * nrow + (rw > 0) + (rh > 0) + (rw > 0 && rh > 0);
+        if (P.by_block && ok) {   // s_BlockMax blocks (BlockGeom in fpm_kernels.hip: Qt or MFC layout)
+            const int bw = mfc ? 2 * tt.w : tt.w, bh = mfc ? 2 * tt.h : tt.h;
+            const int ncol = P.map_w[a] / bw, nrow = P.map_h[a] / bh;
+            const int rw = P.map_w[a] - ncol * bw, rh = P.map_h[a] - nrow * bh;
+            if (!mfc) nb = ncol * nrow + (rw > 0) + (rh > 0) + (rw > 0 && rh > 0);
+            else nb = (ncol == 0 || nrow == 0) ? 0 : ncol * nrow + ((rw > 0 && rh > 0) ? 2 : 1);
+            P.max_cells = std::max(P.max_cells, ((P.map_w[a] + tt.w - 1) / tt.w) * ((P.map_h[a] + tt.h - 1) / tt.h));
         }
         P.nblk[a] = nb;
         P.max_nblk = std::max(P.max_nblk, nb);
@@ -590,6 +602,7 @@ int enqueue_search(fpm_ctx* ctx) {
         na.peaks = P.d_peaks.as<Peak>();
         na.counts = P.d_counts.as<int32_t>();
         na.tw = tt.w; na.th = tt.h; na.cap = P.cap; na.by_block = P.by_block ? 1 : 0;
+        na.mfc = ctx->prm.semantics == FPM_SEMANTICS_MFC ? 1 : 0;
         na.thr = P.layer_score[L]; na.overlap = ctx->prm.max_overlap;
         na.lds_blocks = 0;
         na.cand = nullptr; na.cand_cnt = nullptr; na.cand_cap = 0; na.cand_lds = 0; na.stamps = nullptr;
@@ -599,7 +612,7 @@ int enqueue_search(fpm_ctx* ctx) {
         }
         int mdim = 0;
         for (int a = 0; a < P.nang; ++a) mdim = std::max(mdim, std::max(P.map_w[a], P.map_h[a]));
-        launch_nms(na, J, P.max_nblk, mdim, st);
+        launch_nms(na, J, P.max_nblk, mdim, P.max_cells, st);
     }
     HIP_TRY(hipMemsetAsync(P.d_livecnt.p, 0, sizeof(int32_t) * (L + 2), st));
     int32_t* live[2] = {P.d_live.as<int32_t>(), P.d_live.as<int32_t>() + P.C};
@@ -769,7 +782,7 @@ void collect_candidates(fpm_ctx* ctx, int s, const std::vector<int>& pos, std::v
                 if (nm[j].score > big) { imax = j; big = nm[j].score; }
             }
             if (nm[imax].score < P.layer_score[0]) { out.push_back(c); continue; }
-            if (ctx->prm.subpixel && !nm[imax].on_border && imax != 0 && imax != 2) {
+            if (ctx->run_prm.subpixel && !nm[imax].on_border && imax != 0 && imax != 2) {
                 double nx = 0, ny = 0, na = 0;
                 subpix_estimation(nm, &nx, &ny, &na, astep, imax);
                 nm[imax].ptx = nx; nm[imax].pty = ny;
@@ -826,6 +839,25 @@ bool merge_candidates(const fpm_params& prm, int t0w, int t0h, const fpm_candida
     }
     filter_with_rotated_rect(all, prm.max_overlap);
     std::sort(all.begin(), all.end(), score_big2small);
+    if (prm.semantics == FPM_SEMANTICS_MFC) {   // MatchToolDlg.cpp:1080-1116
+        for (const HostMatch& m : all) {
+            const double rad = -m.angle * kD2R;
+            fpm_result o;
+            o.lt_x = m.ptx; o.lt_y = m.pty;   // f64 corners from the f64 point (the Qt class rounds to Point2f)
+            o.rt_x = o.lt_x + t0w * std::cos(rad); o.rt_y = o.lt_y - t0w * std::sin(rad);
+            o.lb_x = o.lt_x + t0h * std::sin(rad); o.lb_y = o.lt_y + t0h * std::cos(rad);
+            o.rb_x = o.rt_x + t0h * std::sin(rad); o.rb_y = o.rt_y + t0h * std::cos(rad);
+            o.cx = (o.lt_x + o.rt_x + o.rb_x + o.lb_x) / 4;
+            o.cy = (o.lt_y + o.rt_y + o.rb_y + o.lb_y) / 4;
+            o.angle = -m.angle;   // negated, wrapped to [-180, 180]
+            if (o.angle < -180) o.angle += 360;
+            if (o.angle > 180) o.angle -= 360;
+            o.score = m.score;
+            out.push_back(o);
+            if ((int)out.size() == prm.max_pos) break;   // at most MaxPos rows (:1115-1116)
+        }
+        return true;
+    }
     for (const HostMatch& m : all) {   // :406-432
         const double rad = -m.angle * kD2R;
         const float cs = (float)std::cos(rad), sn = (float)std::sin(rad);
@@ -868,6 +900,8 @@ int launch_search(fpm_ctx* ctx) {
 // First half of a staged search: plan, then the whole device pass enqueued on the context's stream (no wait).
 int start_staged(fpm_ctx* ctx) {
     ctx->t_call0 = std::chrono::steady_clock::now();
+    ctx->cands.clear();
+    ctx->stats.clear();
     int rc = build_plan(ctx);
     if (rc != FPM_OK) return rc;
     if (!ctx->t_ev[0]) {
@@ -880,6 +914,7 @@ int start_staged(fpm_ctx* ctx) {
         if (rc != FPM_OK) return rc;
     }
     HIP_TRY(hipEventRecord(ctx->t_ev[1], ctx->stream));
+    ctx->run_prm = ctx->prm;
     ctx->pending = true;
     return FPM_OK;
 }
@@ -910,7 +945,7 @@ int complete_staged(fpm_ctx* ctx, std::vector<std::vector<fpm_result>>& results,
     for (int s = 0; s < P.S; ++s) {
         collect_candidates(ctx, s, pos, ctx->cands[s]);
         if (merge)
-            merge_candidates(ctx->prm, ctx->tmpl[0].w, ctx->tmpl[0].h, ctx->cands[s].data(), (int)ctx->cands[s].size(),
+            merge_candidates(ctx->run_prm, ctx->tmpl[0].w, ctx->tmpl[0].h, ctx->cands[s].data(), (int)ctx->cands[s].size(),
                          results[s]);
     }
     // stats: [angles, top candidates, live entering layer L-1 .. 0] (totals over the batch)
@@ -984,6 +1019,8 @@ void fpm_params_default(fpm_params* p) {
     p->use_simd = 1;            // :34
     p->subpixel = 0;            // :35
     p->tolerance_range = 0;     // :38
+    p->semantics = FPM_SEMANTICS_QT;
+    p->top_angle_step = 0.0;    // extension: the reference's derived step
 }
 
 int fpm_abi_version(void) { return FPM_ABI_VERSION; }
@@ -1029,6 +1066,7 @@ const char* fpm_last_error(const fpm_ctx* ctx) { return ctx ? ctx->err.c_str() :
 
 int fpm_set_params(fpm_ctx* ctx, const fpm_params* p) {
     if (!ctx || !p) return FPM_E_INVALID_ARG;
+    if (ctx->pending) { ctx->err = "a search is in flight (fpm_match_staged_finish first)"; return FPM_E_INVALID_ARG; }
     ctx->prm = *p;
     return FPM_OK;
 }
@@ -1043,8 +1081,10 @@ int fpm_get_params(const fpm_ctx* ctx, fpm_params* p) {
 int fpm_learn(fpm_ctx* ctx, const uint8_t* gray, int32_t w, int32_t h, size_t stride) {
     if (!ctx) return FPM_E_INVALID_ARG;
     if (!gray || w <= 0 || h <= 0 || stride < (size_t)w) { ctx->err = "empty template"; return FPM_E_INVALID_ARG; }
+    if (ctx->pending) { ctx->err = "a search is in flight (fpm_match_staged_finish first)"; return FPM_E_INVALID_ARG; }
     HIP_TRY(hipSetDevice(ctx->device));
     ctx->learned = false;
+    ctx->staged = false;
     ctx->tmpl.clear();
     const int L = top_layer(w, h, (int)std::sqrt((double)ctx->prm.min_reduce_area));
     std::vector<TmplLevel> lv(L + 1);
@@ -1120,7 +1160,9 @@ int fpm_learn(fpm_ctx* ctx, const uint8_t* gray, int32_t w, int32_t h, size_t st
 
 int fpm_clear_pattern(fpm_ctx* ctx) {
     if (!ctx) return FPM_E_INVALID_ARG;
+    if (ctx->pending) { ctx->err = "a search is in flight (fpm_match_staged_finish first)"; return FPM_E_INVALID_ARG; }
     ctx->learned = false;
+    ctx->staged = false;
     ctx->tmpl.clear();
     ctx->tmpl_gen++;
     return FPM_OK;
@@ -1137,9 +1179,11 @@ int fpm_stage_sources(fpm_ctx* ctx, const uint8_t* const* grays, int32_t count, 
     int rc = check_sizes(ctx, w, h);
     if (rc != FPM_OK) return rc;
     HIP_TRY(hipSetDevice(ctx->device));
+    ctx->staged = false;
     rc = upload_sources(ctx, grays, count, w, h, stride);
     if (rc != FPM_OK) return rc;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    ctx->staged = true;
     return FPM_OK;
 }
 
@@ -1159,7 +1203,7 @@ static int copy_results(const std::vector<std::vector<fpm_result>>& res, fpm_res
 int fpm_match_staged_launch(fpm_ctx* ctx) {
     if (!ctx) return FPM_E_INVALID_ARG;
     if (!ctx->learned) { ctx->err = "template not learned"; return FPM_E_NOT_LEARNED; }
-    if (ctx->S <= 0) { ctx->err = "no staged sources"; return FPM_E_INVALID_ARG; }
+    if (ctx->S <= 0 || !ctx->staged) { ctx->err = "no staged sources (fpm_match replaces a staged batch)"; return FPM_E_INVALID_ARG; }
     if (ctx->pending) { ctx->err = "a search is already in flight"; return FPM_E_INVALID_ARG; }
     HIP_TRY(hipSetDevice(ctx->device));
     return start_staged(ctx);
@@ -1186,14 +1230,21 @@ int fpm_match(fpm_ctx* ctx, const uint8_t* gray, int32_t w, int32_t h, size_t st
               int32_t* n_results, double* seconds) {
     if (!ctx || !n_results) return FPM_E_INVALID_ARG;
     *n_results = 0;
-    if (!gray || w <= 0 || h <= 0 || stride < (size_t)w) { ctx->err = "empty source"; return FPM_E_INVALID_ARG; }
     if (ctx->pending) { ctx->err = "a search is in flight (fpm_match_staged_finish first)"; return FPM_E_INVALID_ARG; }
+    // a failed call leaves no stale candidate records behind (fpm_last_candidates of a sharded search)
+    ctx->cands.clear();
+    ctx->stats.clear();
+    if (!gray || w <= 0 || h <= 0 || stride < (size_t)w) { ctx->err = "empty source"; return FPM_E_INVALID_ARG; }
     int rc = check_sizes(ctx, w, h);
     if (rc != FPM_OK) return rc;
     HIP_TRY(hipSetDevice(ctx->device));
-    const auto t0 = std::chrono::high_resolution_clock::now();
+    ctx->staged = false;   // the slab is re-laid out for this one source
+    // the reference deep-copies the source before its clock starts (TemplateMatcher.cpp:104 then :117): the upload
+    // is that copy, so getLastExecutionTime() starts once it has landed
     rc = upload_sources(ctx, &gray, 1, w, h, stride);
     if (rc != FPM_OK) return rc;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    const auto t0 = std::chrono::high_resolution_clock::now();
     std::vector<std::vector<fpm_result>> res;
     rc = run_staged(ctx, res);
     if (rc != FPM_OK) return rc;

@@ -52,6 +52,7 @@ struct NmsArgs {
     int32_t tw, th;          // top template size
     int32_t cap;             // max_pos + MATCH_CANDIDATE_NUM
     int32_t by_block;
+    int32_t mfc;             // MFC s_BlockMax semantics (fpm_params.semantics, MatchToolDlg.h:93-210)
     int32_t lds_blocks;      // block-maxima capacity in LDS (set by launch_nms; 0 = global scratch)
     int32_t* cand;           // s_BlockMax mode: indices of the map pixels >= thr, [job][cand_cap] (k_nms_blocks)
     int32_t* cand_cnt;       // [job], zeroed before the launch
@@ -160,7 +161,8 @@ bool ncc_tile_fits(int tw, int th);   // LDS-tiled variant applies (templates up
 void launch_ncc_tile(const NccJob* jobs, int njobs, int max_ow, int max_oh, int tw, int th, hipStream_t st);
 constexpr int kNmsCandCap = 8192;   // s_BlockMax candidates (pixels >= the top-layer score) kept per map
 // max_blocks: s_BlockMax blocks of the largest map (block mode); max_map_dim: largest map width or height
-void launch_nms(const NmsArgs& a, int njobs, int max_blocks, int max_map_dim, hipStream_t st);
+// max_cells: the largest ceil(mw / tw) * ceil(mh / th) over the maps (k_nms_greedy's coverage cells)
+void launch_nms(const NmsArgs& a, int njobs, int max_blocks, int max_map_dim, int max_cells, hipStream_t st);
 void launch_cand_init(const CandInitArgs& a, hipStream_t st);
 void launch_roi_tables(const RoiArgs& a, hipStream_t st);
 void launch_roi_warp(const RoiArgs& a, hipStream_t st);

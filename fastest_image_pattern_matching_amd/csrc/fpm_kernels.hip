@@ -16,7 +16,26 @@
 #include <float.h>
 #include <limits.h>
 
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "fpm_kernels.h"
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) is per device: remember, per (device, kernel), the largest dynamic
+// LDS already allowed, under a mutex (contexts on several devices / host threads launch concurrently)
+static void ensure_lds_attr(const void* fn, size_t bytes) {
+    if (bytes <= 65536) return;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    static std::mutex mu;
+    static std::map<std::pair<int, const void*>, size_t> done;
+    std::lock_guard<std::mutex> lock(mu);
+    size_t& cur = done[std::make_pair(dev, fn)];
+    if (bytes <= cur) return;
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    cur = bytes;
+}
 
 namespace fpm {
 
@@ -543,12 +562,7 @@ void launch_ncc_tile(const NccJob* jobs, int njobs, int max_ow, int max_oh, int 
     if (njobs <= 0 || max_ow <= 0 || max_oh <= 0) return;
     const int tiles_x = (max_ow + NT_W - 1) / NT_W, tiles_y = (max_oh + NT_H - 1) / NT_H;
     const size_t lds = ncc_tile_lds(tw, th);
-    static bool attr = false;
-    if (lds > 65536 && !attr) {
-        (void)hipFuncSetAttribute((const void*)k_ncc_tile, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)ncc_tile_lds(4 * NT_MAXW, NT_MAXH));
-        attr = true;
-    }
+    if (lds > 65536) ensure_lds_attr((const void*)k_ncc_tile, ncc_tile_lds(4 * NT_MAXW, NT_MAXH));
     hipLaunchKernelGGL(k_ncc_tile, dim3(tiles_x * tiles_y, njobs), dim3(256), lds, st, jobs, tiles_x);
 }
 
@@ -588,20 +602,32 @@ __device__ __forceinline__ void rect_max(const float* m, int mw, int x0, int y0,
     *bi = (y0 + by) * mw + x0 + bx;
 }
 
+// s_BlockMax block layout of one map.  Qt (DataStructures.h:150-213): blocks of the template size, grid row-major, right
+// strip, bottom strip, corner.  MFC (MatchTool/MatchToolDlg.h:108-175, fpm_params.semantics): blocks of twice the
+// template size, no blocks at all when the map holds no whole block (the peaks then come from full-map scans), then
+// right + bottom strips, the right strip alone, or else the full-width bottom strip (empty without any residue).
 struct BlockGeom {
-    int ncol, nrow, rw, rh, nb;
-    __device__ void init(int mw, int mh, int tw, int th) {
-        ncol = mw / tw; nrow = mh / th;
-        rw = mw - ncol * tw; rh = mh - nrow * th;
-        nb = ncol * nrow + (rw > 0) + (rh > 0) + (rw > 0 && rh > 0);
+    int bw, bh, ncol, nrow, rw, rh, nb, mfc;
+    __device__ void init(int mw, int mh, int tw, int th, int mfc_ = 0) {
+        mfc = mfc_;
+        bw = mfc ? 2 * tw : tw; bh = mfc ? 2 * th : th;
+        ncol = mw / bw; nrow = mh / bh;
+        rw = mw - ncol * bw; rh = mh - nrow * bh;
+        if (!mfc) nb = ncol * nrow + (rw > 0) + (rh > 0) + (rw > 0 && rh > 0);
+        else nb = (ncol == 0 || nrow == 0) ? 0 : ncol * nrow + ((rw > 0 && rh > 0) ? 2 : 1);
     }
-    // s_BlockMax block order (DataStructures.h:150-213): grid row-major, right strip, bottom strip, corner
-    __device__ void rect(int b, int mw, int mh, int tw, int th, int& x, int& y, int& w, int& h) const {
-        if (b < ncol * nrow) { x = (b % ncol) * tw; y = (b / ncol) * th; w = tw; h = th; return; }
+    __device__ void rect(int b, int mw, int mh, int& x, int& y, int& w, int& h) const {
+        if (b < ncol * nrow) { x = (b % ncol) * bw; y = (b / ncol) * bh; w = bw; h = bh; return; }
         b -= ncol * nrow;
-        if (rw > 0) { if (b == 0) { x = ncol * tw; y = 0; w = rw; h = mh; return; } --b; }
-        if (rh > 0) { if (b == 0) { x = 0; y = nrow * th; w = ncol * tw; h = rh; return; } --b; }
-        x = ncol * tw; y = nrow * th; w = rw; h = rh;
+        if (mfc) {
+            if (rw > 0 && b == 0) { x = ncol * bw; y = 0; w = rw; h = mh; return; }
+            if (rw > 0 && rh > 0) { x = 0; y = nrow * bh; w = ncol * bw; h = rh; return; }
+            x = 0; y = nrow * bh; w = mw; h = rh;   // the full-width bottom strip (h = 0 without any residue)
+            return;
+        }
+        if (rw > 0) { if (b == 0) { x = ncol * bw; y = 0; w = rw; h = mh; return; } --b; }
+        if (rh > 0) { if (b == 0) { x = 0; y = nrow * bh; w = ncol * bw; h = rh; return; } --b; }
+        x = ncol * bw; y = nrow * bh; w = rw; h = rh;
     }
 };
 
@@ -625,13 +651,17 @@ __device__ __forceinline__ void wave_better_reduce(float& v, int& b) {
     b = __builtin_amdgcn_readlane(b, 63);
 }
 
-// minMaxLoc over a sub-rectangle by one wave: first max in row-major order (rect_max), result in every lane
+__device__ __forceinline__ int empty_loc(int b) { return -1 - b; }
+
+// minMaxLoc over a sub-rectangle by one wave: first max in row-major order (rect_max), result in every lane.  An empty
+// rectangle (a zero-width or zero-height s_BlockMax strip) gives cv::minMaxLoc's answer for an empty array, 0 at
+// (-1, -1) relative to the strip: bi = -1 here, which callers store as the block's empty marker (empty_loc)
 __device__ __forceinline__ void wave_rect_max(const float* m, int mw, int x0, int y0, int w, int h, int lane,
                                               float& bv, int& bi) {
     const int n = w * h;
-    if (n <= 0) {   // empty rectangle (a zero-width strip): its origin pixel, as rect_max / the oracle's max_loc
-        bi = y0 * mw + x0;
-        bv = m[bi];
+    if (n <= 0) {
+        bv = 0.f;
+        bi = -1;
         return;
     }
     float v = -INFINITY;
@@ -659,17 +689,17 @@ __global__ __launch_bounds__(256) void k_nms_blocks(NmsArgs a) {
     const NmsJob& j = a.jobs[blockIdx.y];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     BlockGeom g;
-    g.init(j.mw, j.mh, a.tw, a.th);
+    g.init(j.mw, j.mh, a.tw, a.th, a.mfc);
     if (j.mw <= 0 || j.mh <= 0) return;
-    const int corner = (g.rw > 0 && g.rh > 0) ? g.nb - 1 : -1;
+    const int corner = (!g.mfc && g.rw > 0 && g.rh > 0) ? g.nb - 1 : -1;   // (MFC has no corner block)
     int32_t* cand = a.cand ? a.cand + (size_t)blockIdx.y * a.cand_cap : nullptr;
     for (int b = blockIdx.x * 4 + wv; b < g.nb; b += gridDim.x * 4) {
         int x, y, w, h;
-        g.rect(b, j.mw, j.mh, a.tw, a.th, x, y, w, h);
+        g.rect(b, j.mw, j.mh, x, y, w, h);
         float v;
         int i;
         wave_rect_max(j.map, j.mw, x, y, w, h, lane, v, i);
-        if (lane == 0) { j.bmax[b] = v; j.bloc[b] = i; }
+        if (lane == 0) { j.bmax[b] = v; j.bloc[b] = i >= 0 ? i : empty_loc(b); }
         if (cand && b != corner && w * h > 0) {
             const int n = w * h;
             int r = lane / w, c = lane - (lane / w) * w;
@@ -693,14 +723,24 @@ __global__ __launch_bounds__(256) void k_nms_blocks(NmsArgs a) {
     }
 }
 
-// argmax over the block maxima (GetMaxValueLoc: max_element, first block on ties), broadcast to every thread
-__device__ __forceinline__ void block_argmax(const float* bm, const int* bl, int nb, float* sv, int* si, float& v,
-                                             int& i) {
+// argmax over the block maxima, broadcast to every thread: GetMaxValueLoc, Qt max_element (first block on ties,
+// DataStructures.h:232-245) or MFC's '>=' scan (the last block on ties, MatchToolDlg.h:194-210)
+__device__ __forceinline__ void block_argmax(const float* bm, const int* bl, int nb, bool last, float* sv, int* si,
+                                             float& v, int& i) {
     v = -INFINITY;
     i = INT_MAX;
-    for (int b = threadIdx.x; b < nb; b += 256) better(v, i, bm[b], b);
+    for (int b = threadIdx.x; b < nb; b += 256) better(v, i, bm[b], last ? nb - 1 - b : b);
     wg_argmax(v, i, sv, si);
-    i = bl[i];
+    i = bl[last ? nb - 1 - i : i];
+}
+
+// a block location: a map index, or empty_loc(b) for the empty strip b, whose minMaxLoc answer is (x0 - 1, y0 - 1)
+__device__ __forceinline__ void block_loc_xy(const BlockGeom& g, int loc, int mw, int mh, int& px, int& py) {
+    if (loc >= 0) { px = loc % mw; py = loc / mw; return; }
+    int x, y, w, h;
+    g.rect(-1 - loc, mw, mh, x, y, w, h);
+    px = x - 1;
+    py = y - 1;
 }
 
 // K5: peak extraction of one map per workgroup: getNextMaxLoc (plain: painted rectangle + full-map argmax) or its
@@ -713,29 +753,33 @@ __global__ __launch_bounds__(256) void k_nms(NmsArgs a) {
     __shared__ int naff;
     __shared__ int aff[256];
     const NmsJob& j = a.jobs[blockIdx.x];
+    if (a.cand && a.cand_cnt[blockIdx.x] < 0) return;   // taken by k_nms_greedy
     float* m = j.map;
     const int mw = j.mw, mh = j.mh, n = mw * mh, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     Peak* out = a.peaks + (size_t)blockIdx.x * a.cap;
     const double ov = a.overlap;
     BlockGeom g;
-    g.init(mw, mh, a.tw, a.th);
+    g.init(mw, mh, a.tw, a.th, a.mfc);
+    const bool blocks = a.by_block && g.nb > 0;   // (an MFC map without a whole block: full-map scans)
+    const bool last = g.mfc != 0;
     float v = -INFINITY;
     int i = INT_MAX;
     if (n <= 0) { if (tid == 0) a.counts[blockIdx.x] = 0; return; }
     float* bm = j.bmax;
     int* bl = j.bloc;
-    if (a.by_block) {
-        block_argmax(bm, bl, g.nb, sv, si, v, i);
+    if (blocks) {
+        block_argmax(bm, bl, g.nb, last, sv, si, v, i);
     } else {
         for (int k = tid; k < n; k += 256) { const float x = m[k]; if (x > v) { v = x; i = k; } }
         wg_argmax(v, i, sv, si);
     }
     if ((double)v < a.thr) { if (tid == 0) a.counts[blockIdx.x] = 0; return; }
     int cnt = 0;
-    if (tid == 0) { out[0].x = i % mw; out[0].y = i / mw; out[0].score = v; }
+    int px, py;
+    block_loc_xy(g, i, mw, mh, px, py);
+    if (tid == 0) { out[0].x = px; out[0].y = py; out[0].score = v; }
     ++cnt;
     for (int it = 0; it < a.cap - 1; ++it) {
-        const int px = i % mw, py = i / mw;
         // rect of getNextMaxLoc (TemplateMatcher.cpp:1198-1201 / :1211-1214): int truncation of f64
         const int sx = (int)(px - a.tw * (1 - ov)), sy = (int)(py - a.th * (1 - ov));
         const int rw = (int)(2 * a.tw * (1 - ov)), rh = (int)(2 * a.th * (1 - ov));
@@ -748,11 +792,11 @@ __global__ __launch_bounds__(256) void k_nms(NmsArgs a) {
         }
         if (tid == 0) naff = 0;
         __syncthreads();
-        if (a.by_block) {
+        if (blocks) {
             // blocks whose rectangle intersects the painted one (UpdateMax), listed, then re-scanned per wave
             for (int b = tid; b < g.nb; b += 256) {
                 int x, y, w, h;
-                g.rect(b, mw, mh, a.tw, a.th, x, y, w, h);
+                g.rect(b, mw, mh, x, y, w, h);
                 const int ix1 = max(x, sx), iy1 = max(y, sy);
                 const int iw = min(x + w, sx + rw) - ix1, ih = min(y + h, sy + rh) - iy1;
                 if (iw > 0 && ih > 0) {
@@ -766,7 +810,7 @@ __global__ __launch_bounds__(256) void k_nms(NmsArgs a) {
                 for (int k = wv; k < na; k += 4) {
                     const int b = aff[k];
                     int x, y, w, h;
-                    g.rect(b, mw, mh, a.tw, a.th, x, y, w, h);
+                    g.rect(b, mw, mh, x, y, w, h);
                     float bv;
                     int bi;
                     wave_rect_max(m, mw, x, y, w, h, lane, bv, bi);
@@ -775,14 +819,14 @@ __global__ __launch_bounds__(256) void k_nms(NmsArgs a) {
             } else {   // (a painted rectangle spanning > 256 blocks: overlap < 0 with tiny blocks) one per thread
                 for (int b = tid; b < g.nb; b += 256) {
                     int x, y, w, h;
-                    g.rect(b, mw, mh, a.tw, a.th, x, y, w, h);
+                    g.rect(b, mw, mh, x, y, w, h);
                     const int ix1 = max(x, sx), iy1 = max(y, sy);
                     const int iw = min(x + w, sx + rw) - ix1, ih = min(y + h, sy + rh) - iy1;
                     if (iw > 0 && ih > 0) rect_max(m, mw, x, y, w, h, &bm[b], &bl[b]);
                 }
             }
             __syncthreads();
-            block_argmax(bm, bl, g.nb, sv, si, v, i);
+            block_argmax(bm, bl, g.nb, last, sv, si, v, i);
         } else {
             v = -INFINITY;
             i = INT_MAX;
@@ -790,7 +834,8 @@ __global__ __launch_bounds__(256) void k_nms(NmsArgs a) {
             wg_argmax(v, i, sv, si);
         }
         if ((double)v < a.thr) break;
-        if (tid == 0) { out[cnt].x = i % mw; out[cnt].y = i / mw; out[cnt].score = v; }
+        block_loc_xy(g, i, mw, mh, px, py);
+        if (tid == 0) { out[cnt].x = px; out[cnt].y = py; out[cnt].score = v; }
         ++cnt;
     }
     if (tid == 0) a.counts[blockIdx.x] = cnt;
@@ -814,6 +859,14 @@ __device__ __forceinline__ int nms_block_of(const BlockGeom& g, int x, int y, in
         if (y >= gh) b2 = base + 2;   // rw > 0 and rh > 0: right strip, bottom strip, corner
         return base;
     }
+    return base + (g.rw > 0 ? 1 : 0);
+}
+
+// the MFC block holding map pixel (x, y) (MatchToolDlg.h:108-175: grid, then right strip, then bottom strip)
+__device__ __forceinline__ int nms_block_of_mfc(const BlockGeom& g, int x, int y) {
+    const int gw = g.ncol * g.bw, gh = g.nrow * g.bh, base = g.ncol * g.nrow;
+    if (x < gw && y < gh) return (y / g.bh) * g.ncol + x / g.bw;
+    if (x >= gw) return base;
     return base + (g.rw > 0 ? 1 : 0);
 }
 
@@ -1074,7 +1127,7 @@ __global__ __launch_bounds__(256) void k_nms_greedy(NmsArgs a) {
     const int tw = a.tw, th = a.th;
     const int rw = (int)(2 * tw * (1 - ov)), rh = (int)(2 * th * (1 - ov));
     BlockGeom g;
-    g.init(mw, mh, tw, th);
+    g.init(mw, mh, tw, th, a.mfc);
     const int K = a.cand_cnt[blockIdx.x];
     const int cxn = (mw + tw - 1) / tw, cyn = (mh + th - 1) / th, ncell = cxn * cyn;
     if (!(mw > 0 && mh > 0 && g.ncol > 0 && g.nrow > 0 && rw > 0 && rh > 0 && a.thr > -1.0 && K >= 0 &&
@@ -1093,7 +1146,8 @@ __global__ __launch_bounds__(256) void k_nms_greedy(NmsArgs a) {
         if (i < K) {
             const int idx = cand[i], x = idx % mw, y = idx / mw;
             int b2;
-            const int b = nms_block_of(g, x, y, tw, th, b2);
+            // MFC: the last block wins equal maxima, so the block part of the key counts down
+            const int b = g.mfc ? g.nb - 1 - nms_block_of_mfc(g, x, y) : nms_block_of(g, x, y, tw, th, b2);
             sv[i] = m[idx];
             sk[i] = ((uint64_t)b << 32) | (uint32_t)((y << 16) | x);
         } else {
@@ -1191,33 +1245,38 @@ static size_t nms_fast_lds(int blocks, int /*cap*/, int cands) {
 constexpr int kNmsLdsBlocksMax = 12 * 1024;   // block maxima kept in LDS up to this many blocks
 constexpr int kNmsLdsBytes = 160 * 1024 - 4096;   // k_nms_fast dynamic LDS budget (statics take the rest)
 
-void launch_nms(const NmsArgs& a0, int njobs, int max_blocks, int max_map_dim, hipStream_t st) {
+void launch_nms(const NmsArgs& a0, int njobs, int max_blocks, int max_map_dim, int max_cells, hipStream_t st) {
     if (njobs <= 0) return;
     NmsArgs a = a0;
     if (a.by_block && max_blocks > 0) {
         hipLaunchKernelGGL(k_nms_blocks, dim3((max_blocks + 3) / 4 < 16384 ? (max_blocks + 3) / 4 : 16384, njobs),
                            dim3(256), 0, st, a);
+        // the greedy form takes what it can (thr > 0: an empty strip's stale 0 is never a peak); k_nms the rest
+        const bool greedy = a.cand && !a.stamps && a.thr > 0.0 && max_map_dim < 65536 && a.cap <= 256 &&
+                            nms_greedy_lds(max_cells) <= (size_t)kNmsLdsBytes;
+        if (greedy) ensure_lds_attr((const void*)k_nms_greedy, kNmsLdsBytes);
+        if (a.mfc) {   // MFC block semantics: greedy form + k_nms (k_nms_fast is Qt-only)
+            if (greedy) {
+                NmsArgs gA = a;
+                gA.lds_blocks = max_cells;
+                hipLaunchKernelGGL(k_nms_greedy, dim3(njobs), dim3(256), nms_greedy_lds(max_cells), st, gA);
+            }
+            a.lds_blocks = 0;
+            hipLaunchKernelGGL(k_nms, dim3(njobs), dim3(256), 0, st, a);
+            return;
+        }
         const size_t fixed = nms_fast_lds(max_blocks, a.cap, 0);
         if (max_blocks <= kNmsLdsBlocksMax && a.cap <= 256 && a.overlap >= 0.0 && max_map_dim < 65536 &&
-            fixed <= (size_t)kNmsLdsBytes) {
+            a.thr > 0.0 && fixed <= (size_t)kNmsLdsBytes) {
             a.lds_blocks = max_blocks;
             const long room = ((long)kNmsLdsBytes - (long)fixed) / 8;
             a.cand_lds = a.cand ? (int)(room < kNmsCandCap ? room : kNmsCandCap) : 0;
             const size_t lds = nms_fast_lds(max_blocks, a.cap, a.cand_lds);
-            static bool attr = false;
-            if (!attr) {
-                (void)hipFuncSetAttribute((const void*)k_nms_fast, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          kNmsLdsBytes);
-                (void)hipFuncSetAttribute((const void*)k_nms_greedy, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          kNmsLdsBytes);
-                attr = true;
-            }
-            // cells of template size cover the map: (ceil(mw / tw) * ceil(mh / th)) <= max_blocks + ncol + nrow + 1
-            const int cells = max_blocks + max_map_dim / (a.tw > 0 ? a.tw : 1) + max_map_dim / (a.th > 0 ? a.th : 1) + 2;
-            if (a.cand && !a.stamps && nms_greedy_lds(cells) <= (size_t)kNmsLdsBytes) {
+            ensure_lds_attr((const void*)k_nms_fast, kNmsLdsBytes);
+            if (greedy) {
                 NmsArgs gA = a;
-                gA.lds_blocks = cells;
-                hipLaunchKernelGGL(k_nms_greedy, dim3(njobs), dim3(256), nms_greedy_lds(cells), st, gA);
+                gA.lds_blocks = max_cells;
+                hipLaunchKernelGGL(k_nms_greedy, dim3(njobs), dim3(256), nms_greedy_lds(max_cells), st, gA);
             }
             hipLaunchKernelGGL(k_nms_fast, dim3(njobs), dim3(256), lds, st, a);
             return;
@@ -2579,11 +2638,7 @@ void launch_roi_tables(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0 || a.equal1) return;
     const int grid = a.slot_cap < 4096 ? a.slot_cap : 4096;
     const size_t lds = sizeof(int32_t) * 2 * (a.tabw + a.tabh);
-    static size_t lds_attr = 0;
-    if (lds > 65536 && lds > lds_attr) {
-        (void)hipFuncSetAttribute((const void*)k_roi_tables, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        lds_attr = lds;
-    }
+    ensure_lds_attr((const void*)k_roi_tables, lds);
     hipLaunchKernelGGL(k_roi_tables, dim3(grid), dim3(256), lds, st, a);
 }
 
@@ -2629,12 +2684,7 @@ void launch_roi_corr(const RoiArgs& a, hipStream_t st) {
         else launch_corr_regs<16>(a, items, lds, st);
         return;
     }
-    static size_t lds_attr = 0;
-    if (lds > 65536 && lds > lds_attr) {
-        (void)hipFuncSetAttribute((const void*)k_roi_corr<0, kCorrGlobalA, kCorrWaves>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        lds_attr = lds;
-    }
+    ensure_lds_attr((const void*)k_roi_corr<0, kCorrGlobalA, kCorrWaves>, lds);
     const long items = (long)a.slot_cap * ((a.th + kBandRows - 1) / kBandRows);
     const int grid = (int)(items < 16384 ? items : 16384);
     hipLaunchKernelGGL((k_roi_corr<0, kCorrGlobalA, kCorrWaves>), dim3(grid), dim3(256), lds, st, a);
@@ -2656,11 +2706,7 @@ void launch_roi_small(const RoiArgs& a, hipStream_t st) {
         return;
     }
     const size_t lds = (size_t)small_layout(a.tw, a.th).total;
-    static size_t lds_attr = 0;
-    if (lds > 65536 && lds > lds_attr) {
-        (void)hipFuncSetAttribute((const void*)k_roi_small<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        lds_attr = lds;
-    }
+    ensure_lds_attr((const void*)k_roi_small<0>, lds);
     const int grid = a.slot_cap < 8192 ? a.slot_cap : 8192;
     hipLaunchKernelGGL(k_roi_small<0>, dim3(grid), dim3(256), lds, st, a);
 }

@@ -93,6 +93,7 @@ class TemplateMatcher:
         self._last_time = 0.0
         self._user_rect = None
         self._cap = 64                 # results per source; grown on FPM_E_CAPACITY
+        self._staged = 0               # sources of the last stage() (0 after a plain match())
         self._bufs = None              # reusable ctypes result buffers for match_staged
 
     def __del__(self):
@@ -134,7 +135,10 @@ class TemplateMatcher:
     # -- search ---------------------------------------------------------------------------------------------
     def match(self, sourceImage) -> List[SingleTargetMatch]:
         a = np.asarray(sourceImage)
+        self._staged = 0   # fpm_match replaces a staged batch (fpm_match_staged_launch then fails loudly)
         if a.size == 0 or not self.isPatternLearned():
+            # an argument-less fpm_match fails its checks and drops the previous search's candidate records
+            self._lib.fpm_match(self._ctx, None, 0, 0, 0, None, 0, C.byref(C.c_int32()), None)
             return []
         g = _gray(a)
         self._push()
@@ -230,6 +234,15 @@ class TemplateMatcher:
         if rc != L.FPM_OK:
             raise RuntimeError(f"fpm_match_staged_finish failed with {rc}: {self.last_error()}")
         return [self.last_candidates(s) for s in range(self._staged)]
+
+    def last_candidates_if_searched(self, source: int = 0):
+        """last_candidates(source), or None when the last call ran no search for it (fpm_match returned before the
+        device pass: empty source, unlearned template, size mismatch)."""
+        n = C.c_int32()
+        rc = self._lib.fpm_last_candidates(self._ctx, int(source), None, 0, C.byref(n))
+        if rc not in (L.FPM_OK, L.FPM_E_CAPACITY):
+            return None
+        return self.last_candidates(source)
 
     def last_candidates(self, source: int = 0) -> np.ndarray:
         """Candidate records (CANDIDATE_DTYPE, push order) of `source` in the last search."""

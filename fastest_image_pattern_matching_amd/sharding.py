@@ -158,9 +158,17 @@ def match_angle_sharded(matcher, source: np.ndarray, group=None, device=None):
 
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    prev = matcher.getAngleShard()
     matcher.setAngleShard(rank, world)
-    matcher.match(source)
-    local = matcher.last_candidates(0)
+    try:
+        matcher.match(source)
+        # None when the search did not run (empty source, unlearned template, size mismatch: TemplateMatcher.cpp:99-114);
+        # those checks depend only on the source and the template, so every rank takes the same branch
+        local = matcher.last_candidates_if_searched(0)
+    finally:
+        matcher.setAngleShard(*prev)   # later plain match() calls search the whole angle list again
+    if local is None:
+        return []
     full = gather_candidates(local, group=group, device=device)
     tw, th = matcher.template_level(0)[0].shape[::-1]
     return merge_gathered(matcher._params, tw, th, full)

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define FPM_ABI_VERSION 6
+#define FPM_ABI_VERSION 7
 
 /* status codes */
 #define FPM_OK 0
@@ -34,6 +34,17 @@ extern "C" {
 #define FPM_E_DEVICE (-4)        /* HIP runtime error / no gfx950 device                     */
 #define FPM_E_CAPACITY (-5)      /* caller-provided result buffer too small                 */
 #define FPM_E_INTERNAL (-6)
+
+/* Result semantics (fpm_params.semantics).  The drop-in target is the Qt TemplateMatcher (src/TemplateMatcher.cpp);
+ * the README's published numbers come from the MFC tool (MatchTool/MatchToolDlg.cpp), whose search differs in
+ * a few places.  FPM_SEMANTICS_MFC reproduces those:
+ *   - s_BlockMax blocks of 2x the template, right + bottom strips without a corner block, the last block on
+ *     equal maxima, and a full-map minMaxLoc when the map holds no whole block (MatchToolDlg.h:108-210);
+ *   - the angle list from the tolerance ranges when tolerance_range is set (MatchToolDlg.cpp:805-815);
+ *   - corners and centre in f64, the reported angle negated and wrapped to [-180, 180], at most max_pos
+ *     results (MatchToolDlg.cpp:1080-1116). */
+#define FPM_SEMANTICS_QT 0
+#define FPM_SEMANTICS_MFC 1
 
 /* Search parameters: the 7 public setters of TemplateMatcher (TemplateMatcher.h:22-28) plus the hidden
  * fixed members m_bToleranceRange / m_dTolerance1..4 (TemplateMatcher.h:88-89, TemplateMatcher.cpp:38).
@@ -47,9 +58,14 @@ typedef struct fpm_params {
     int32_t use_simd;         /* setUseSIMD           (default 1): lower layers use the per-row int32 ->
                                  float fold of IM_Conv_SIMD (TemplateMatcher.cpp:487-512); 0 = TM_CCORR */
     int32_t subpixel;         /* setSubPixelEstimation(default 0)    */
-    int32_t tolerance_range;  /* m_bToleranceRange    (fixed false in the reference)          */
-    int32_t reserved0;
-    double tolerance[4];      /* m_dTolerance1..4     (unused by the reference search)         */
+    int32_t tolerance_range;  /* m_bToleranceRange    (fixed false in the Qt class; MFC toggles it,
+                                 MatchToolDlg.cpp:2137): 3 refinement angles always; with FPM_SEMANTICS_MFC
+                                 also the top-layer angle list from tolerance[0..3]                   */
+    int32_t semantics;        /* FPM_SEMANTICS_QT (default) or FPM_SEMANTICS_MFC                       */
+    double tolerance[4];      /* m_dTolerance1..4: the MFC ranges [t1, t2] and [t3, t4] (MatchToolDlg.cpp:812-815) */
+    double top_angle_step;    /* extension, no reference knob: the top-layer angle step in degrees replacing the
+                                 derived atan(2 / max(w, h)) of TemplateMatcher.cpp:130 when > 0 (BASELINE
+                                 configs[3] "1 degree step"); 0 = the reference's step (default)     */
 } fpm_params;
 
 /* One result; POD-identical to s_SingleTargetMatch (DataStructures.h:97-115): five cv::Point2d then two
@@ -60,7 +76,8 @@ typedef struct fpm_result {
     double rb_x, rb_y;        /* ptRB     */
     double lb_x, lb_y;        /* ptLB     */
     double cx, cy;            /* ptCenter */
-    double angle;             /* dMatchedAngle (Qt sign convention, TemplateMatcher.cpp:428) */
+    double angle;             /* dMatchedAngle (Qt: +dMatchAngle, TemplateMatcher.cpp:428; MFC: negated and
+                                 wrapped, MatchToolDlg.cpp:1093-1099) */
     double score;             /* dMatchScore */
 } fpm_result;
 

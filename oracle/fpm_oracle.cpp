@@ -198,8 +198,11 @@ static void mean_stddev(const Mat8& m, double* mean, double* sdv) {
     *sdv = std::sqrt(std::max((double)sq * scale - ds * ds, 0.));
 }
 
-// cv::minMaxLoc maximum: first occurrence, row-major, strict '>'  (A.7)
+// cv::minMaxLoc maximum: first occurrence, row-major, strict '>'  (A.7).  An empty ROI (a zero-width s_BlockMax strip)
+// gives 0 at (-1, -1): cv::minMaxIdx leaves its index at 0 for an empty array, which reads as value 0 and a location
+// of -1 in every dimension
 static void max_loc(const MatF& m, int x0, int y0, int w, int h, double* vmax, int* lx, int* ly) {
+    if (w <= 0 || h <= 0) { *vmax = 0; *lx = -1; *ly = -1; return; }
     float best = m.at(y0, x0);
     int bx = 0, by = 0;
     for (int y = 0; y < h; ++y)
@@ -388,11 +391,12 @@ struct MatchParam {
 
 static bool score_big2small(const MatchParam& l, const MatchParam& r) { return l.score > r.score; }
 
-// s_BlockMax, Qt semantics (DataStructures.h:118-246)
+// s_BlockMax: Qt semantics (DataStructures.h:118-246) or, with mfc, the MFC tool's (MatchTool/MatchToolDlg.h:93-210)
 struct BlockMax {
     struct Block { RectI r; double vmax; int mx, my; };
     std::vector<Block> blocks;
     MatF* m = nullptr;
+    bool mfc = false;
     void add(RectI r) {
         Block b; b.r = r;
         int lx, ly;
@@ -400,14 +404,35 @@ struct BlockMax {
         b.mx = r.x + lx; b.my = r.y + ly;
         blocks.push_back(b);
     }
-    BlockMax(MatF& mat, int bw, int bh) : m(&mat) {
-        int ncol = mat.w / bw, nrow = mat.h / bh;
+    BlockMax(MatF& mat, int tw, int th, bool mfc_ = false) : m(&mat), mfc(mfc_) {
+        if (!mfc) {   // blocks of the template size: grid, right strip, bottom strip, corner (DataStructures.h:150-213)
+            const int bw = tw, bh = th;
+            int ncol = mat.w / bw, nrow = mat.h / bh;
+            for (int y = 0; y < nrow; ++y)
+                for (int x = 0; x < ncol; ++x) add(RectI(x * bw, y * bh, bw, bh));
+            if (ncol * bw < mat.w) add(RectI(ncol * bw, 0, mat.w - ncol * bw, mat.h));
+            if (nrow * bh < mat.h) add(RectI(0, nrow * bh, ncol * bw, mat.h - nrow * bh));
+            if (ncol * bw < mat.w && nrow * bh < mat.h)
+                add(RectI(ncol * bw, nrow * bh, mat.w - ncol * bw, mat.h - nrow * bh));
+            return;
+        }
+        // MFC (MatchToolDlg.h:108-175): blocks of twice the template size, none at all when the map holds no whole
+        // block; then right + bottom strips, the right strip alone, or else the full-width bottom strip (empty when
+        // there is no residue at all)
+        const int bw = tw * 2, bh = th * 2;
+        const int ncol = mat.w / bw, nrow = mat.h / bh;
+        const bool hres = mat.w % bw != 0, vres = mat.h % bh != 0;
+        if (ncol == 0 || nrow == 0) return;
         for (int y = 0; y < nrow; ++y)
             for (int x = 0; x < ncol; ++x) add(RectI(x * bw, y * bh, bw, bh));
-        if (ncol * bw < mat.w) add(RectI(ncol * bw, 0, mat.w - ncol * bw, mat.h));
-        if (nrow * bh < mat.h) add(RectI(0, nrow * bh, ncol * bw, mat.h - nrow * bh));
-        if (ncol * bw < mat.w && nrow * bh < mat.h)
-            add(RectI(ncol * bw, nrow * bh, mat.w - ncol * bw, mat.h - nrow * bh));
+        if (hres && vres) {
+            add(RectI(ncol * bw, 0, mat.w - ncol * bw, mat.h));
+            add(RectI(0, nrow * bh, ncol * bw, mat.h - nrow * bh));
+        } else if (hres) {
+            add(RectI(ncol * bw, 0, mat.w - ncol * bw, mat.h));
+        } else {
+            add(RectI(0, nrow * bh, mat.w, mat.h - nrow * bh));
+        }
     }
     void update(RectI ignore) {
         for (auto& b : blocks) {
@@ -420,6 +445,14 @@ struct BlockMax {
         }
     }
     void get_max(double* v, int* x, int* y) const {
+        if (mfc) {   // GetMaxValueLoc (MatchToolDlg.h:194-210): the whole map without blocks, else the LAST maximum
+            if (blocks.empty()) { max_loc(*m, 0, 0, m->w, m->h, v, x, y); return; }
+            size_t k = 0;
+            for (size_t i = 1; i < blocks.size(); ++i)
+                if (blocks[i].vmax >= blocks[k].vmax) k = i;
+            *v = blocks[k].vmax; *x = blocks[k].mx; *y = blocks[k].my;
+            return;
+        }
         if (blocks.empty()) { *v = -1; *x = -1; *y = -1; return; }
         auto it = std::max_element(blocks.begin(), blocks.end(),
                                    [](const Block& a, const Block& b) { return a.vmax < b.vmax; });
@@ -823,8 +856,15 @@ public:
         std::vector<Mat8> spyr = build_pyramid(src, L);
 
         double step = std::atan(2.0 / std::max(T.pyr[L].w, T.pyr[L].h)) * R2D;
+        if (prm.top_angle_step > 0) step = prm.top_angle_step;   // extension (fpm.h): the top-layer step override
+        const bool mfc = prm.semantics == FPM_SEMANTICS_MFC;
         std::vector<double> angles;
-        if (prm.tolerance_angle < VISION_TOLERANCE) {
+        if (mfc && prm.tolerance_range) {   // MatchToolDlg.cpp:805-815
+            const double* t = prm.tolerance;
+            if (t[0] >= t[1] || t[2] >= t[3]) return FPM_E_INVALID_ARG;   // the tool refuses the ranges (:807-811)
+            for (double a = t[0]; a < t[1] + step; a += step) angles.push_back(a);
+            for (double a = t[2]; a < t[3] + step; a += step) angles.push_back(a);
+        } else if (prm.tolerance_angle < VISION_TOLERANCE) {
             angles.push_back(0.0);
         } else {
             for (double a = 0; a < prm.tolerance_angle + step; a += step) angles.push_back(a);
@@ -855,7 +895,7 @@ public:
             int px, py;
             double v, vmax;
             if (by_block) {
-                BlockMax bm(res, tw, th);
+                BlockMax bm(res, tw, th, mfc);
                 bm.get_max(&vmax, &px, &py);
                 if (vmax < layer_score[L]) continue;
                 cand.push_back(MatchParam(P2f(px - tx, py - ty), vmax, angles[i]));
@@ -977,6 +1017,21 @@ public:
         last_seconds = std::chrono::duration<double>(t_end - t_start).count();
         for (const auto& r : all) {
             double rad = -r.angle * D2R;
+            if (mfc) {   // MatchToolDlg.cpp:1080-1116: f64 corners, negated + wrapped angle, at most MaxPos results
+                fpm_result o;
+                o.lt_x = r.pt.x; o.lt_y = r.pt.y;
+                o.rt_x = o.lt_x + iW * std::cos(rad); o.rt_y = o.lt_y - iW * std::sin(rad);
+                o.lb_x = o.lt_x + iH * std::sin(rad); o.lb_y = o.lt_y + iH * std::cos(rad);
+                o.rb_x = o.rt_x + iH * std::sin(rad); o.rb_y = o.rt_y + iH * std::cos(rad);
+                o.cx = (o.lt_x + o.rt_x + o.rb_x + o.lb_x) / 4; o.cy = (o.lt_y + o.rt_y + o.rb_y + o.lb_y) / 4;
+                o.angle = -r.angle;
+                o.score = r.score;
+                if (o.angle < -180) o.angle += 360;
+                if (o.angle > 180) o.angle -= 360;
+                out.push_back(o);
+                if ((int)out.size() == prm.max_pos) break;
+                continue;
+            }
             P2f lt((float)r.pt.x, (float)r.pt.y);
             P2f rt(lt.x + iW * (float)std::cos(rad), lt.y - iW * (float)std::sin(rad));
             P2f lb(lt.x + iH * (float)std::sin(rad), lt.y + iH * (float)std::cos(rad));
@@ -1010,6 +1065,7 @@ void fpm_params_default(fpm_params* p) {
     std::memset(p, 0, sizeof(*p));
     p->max_pos = 70; p->min_reduce_area = 256; p->max_overlap = 0.0; p->score = 0.7;
     p->tolerance_angle = 0.0; p->use_simd = 1; p->subpixel = 0; p->tolerance_range = 0;
+    p->semantics = FPM_SEMANTICS_QT; p->top_angle_step = 0.0;
 }
 
 void* orc_create(void) { return new orc::Matcher(); }

@@ -57,7 +57,7 @@ int main() {
         hipEventCreate(&e0); hipEventCreate(&e1);
         hipEventRecord(e0);
         if (fast) {
-            launch_nms(b, 1, g.nb, 899, 0);
+            launch_nms(b, 1, g.nb, 899, ((mw + tw - 1) / tw) * ((mh + th - 1) / th), 0);
         } else {
             hipLaunchKernelGGL(k_nms_blocks, dim3((g.nb + 3) / 4), dim3(256), 0, 0, b);
             b.lds_blocks = 0;
