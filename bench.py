@@ -12,6 +12,16 @@ data-path collective); barrier + synchronize bracket the K timed steps and the m
 Also reported: the dominant kernel's roofline (HIP events around every launch on the library's stream, in a
 second pass of K steps so the timed pass carries no event overhead) and the CPU baseline (the oracle
 restatement, single thread, on a bounded sample of the same workload, rank 0 at N=1 only).
+
+Roofline bytes are SURVEY.md §8(d)'s algorithmic bytes, reported by the library per search (fpm_search_bytes) and per
+kernel (fpm_profile_get): B_pyr + B_top + B_ref, where a refinement ROI costs its source footprint, the template
+level and the 7x7 f32 scores; scratch this design writes between its kernels (sampled ROIs, row sums) is not
+algorithmic and shows up only in `traffic` (PMC HBM bytes), so traffic / algorithmic bytes measures that overhead.
+``roofline`` is the dominant kernel's (its §8(d) share per launch / its average launch time); ``roofline_search``
+is the whole search's (bytes of all searches of the timed region / its wall time).
+
+``python bench.py --gpus N`` with no torchrun environment starts N ranks itself (torch.distributed.run, one process
+per GPU) before anything touches a GPU; under torchrun, --gpus must equal WORLD_SIZE.
 """
 import argparse
 import json
@@ -35,11 +45,14 @@ def log(*a):
 
 
 TRAFFIC_CSV = os.path.join(REPO, "profiles", "latest", "pmc_traffic.csv")
+TRAFFIC_SOURCE = ("committed rocprofv3 --pmc snapshot profiles/latest/pmc_traffic.csv (scripts/pmc_bench.sh: separate "
+                  "FETCH_SIZE / WRITE_SIZE passes of bench.py --kernel-pass-only, FETCH_SIZE doubled for gfx950, mean per "
+                  "dispatch); not measured in this run")
 
 
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` (a profiling index name, _lib.KERNEL_NAMES) from the committed PMC summary
-    (scripts/pmc_bench.sh: separate FETCH_SIZE / WRITE_SIZE passes over `bench.py --skip-latency`, FETCH_SIZE
+    (scripts/pmc_bench.sh: separate FETCH_SIZE / WRITE_SIZE passes over `bench.py --kernel-pass-only`, FETCH_SIZE
     doubled for gfx950, per-dispatch means); None if not collected for this kernel."""
     import csv
 
@@ -146,10 +159,42 @@ def kernel_pass(m, sources, steps, L):
     avg_s = d["ms_total"] / d["launches"] * 1e-3
     bytes_per_launch = d["bytes"] / d["launches"]
     achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
+    traffic = pmc_traffic(dom)
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic(dom), "kernel": dom,
-                "avg_launch_us": round(avg_s * 1e6, 3), "algorithmic_bytes_per_launch": int(bytes_per_launch)}
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": dom,
+                "avg_launch_us": round(avg_s * 1e6, 3), "algorithmic_bytes_per_launch": int(bytes_per_launch),
+                "bytes_definition": "SURVEY.md §8(d) share of this kernel per launch (fpm_profile_get)",
+                "traffic_source": TRAFFIC_SOURCE if traffic is not None else None}
     return kern, roofline
+
+
+def cpu_identity():
+    """CPU model (/proc/cpuinfo, as lscpu reports it) and the host's online CPU count."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count()}
+
+
+def spawn_ranks(args):
+    """`--gpus N` outside torchrun: run this script under torch.distributed.run with N processes (one per GPU) and
+    return its exit status.  Nothing here touches a GPU; the ranks start fresh."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"[bench] starting {args.gpus} ranks: {' '.join(cmd)}")
+    return subprocess.call(cmd)
 
 
 def main():
@@ -162,15 +207,25 @@ def main():
     ap.add_argument("--contexts", type=int, default=2, help="concurrent contexts (HIP streams) per GPU")
     ap.add_argument("--skip-latency", action="store_true",
                     help="skip the single-search latency probe (PMC runs: only batch dispatches)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print each rank's (rank, world) and exit before any GPU work (launcher test)")
     ap.add_argument("--kernel-pass-only", action="store_true",
                     help="run only the per-kernel pass (one context, the whole batch, K eager steps) and print its "
                          "kernel table + roofline: the command whose rocprofv3 --kernel-trace --stats averages are "
                          "directly comparable to roofline.avg_launch_us")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a wrong n_gpus")
+        sys.exit(2)
+    if args.dry_run:
+        print(json.dumps({"rank": rank, "world": world, "local_rank": local}), flush=True)
+        return
     import torch
 
     dist = None
@@ -262,6 +317,24 @@ def main():
     else:
         n_matches = [len(r) for r in res]
 
+    # §8(d) algorithmic bytes of one step on this rank (each context's last pass covers its share of the batch)
+    b_pyr = b_top = b_ref = 0
+    for c in ctxs:
+        bp, bt, br = c.search_bytes()
+        b_pyr, b_top, b_ref = b_pyr + bp, b_top + bt, b_ref + br
+    step_bytes = b_pyr + b_top + b_ref
+    if dist is not None:
+        t = torch.tensor([step_bytes], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t)
+        step_bytes = float(t.item())
+    search_gbs = step_bytes * args.steps / elapsed / 1e9
+    roofline_search = {"bound": "hbm", "achieved": round(search_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": round(search_gbs / HBM_PEAK_GBS, 5),
+                       "bytes_per_search": {"B_pyr": b_pyr // args.batch, "B_top": b_top // args.batch,
+                                            "B_ref": b_ref // args.batch},
+                       "definition": "SURVEY.md §8(d) B_pyr + B_top + B_ref of every search in the timed region "
+                                     "(fpm_search_bytes, live counts of this workload) / the timed wall time"}
+
     kern, roofline = kernel_pass(m, sources, args.steps, L)
 
     searches = world * args.batch * args.steps
@@ -297,10 +370,12 @@ def main():
         "matches_per_search": n_matches,
         "kernels": kern,
         "roofline": roofline,
+        "roofline_search": roofline_search,
     }
     if world == 1 and rank == 0 and args.cpu_budget > 0:
         log("[rank 0] CPU baseline (oracle restatement: 1 thread, fast-math 1 thread, all cores)")
         out["cpu_baseline"], out["cpu_baseline_variants"] = cpu_baseline(templ, sources[0], args.cpu_budget)
+        out["cpu_baseline"].update(cpu_identity())
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:

@@ -101,6 +101,7 @@ SIGNATURES = {
     "fpm_merge_candidates": (C.c_int, [C.POINTER(Params), C.c_int32, C.c_int32, C.POINTER(Candidate), C.c_int32,
                                        C.POINTER(Result), C.c_int32, C.POINTER(C.c_int32)]),
     "fpm_search_stats": (C.c_int, [_P, C.POINTER(C.c_int64), C.c_int32]),
+    "fpm_search_bytes": (C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "fpm_profile_enable": (C.c_int, [_P, C.c_int32]),
     "fpm_profile_reset": (C.c_int, [_P]),
     "fpm_profile_get": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_int64),

@@ -152,6 +152,7 @@ struct fpm_ctx {
     DevBuf d_op_a, d_op_b, d_op_job;
     // last search stats
     std::vector<int64_t> stats;
+    int64_t alg_bytes[3] = {0, 0, 0};   // SURVEY.md §8(d) algorithmic bytes of the last search: B_pyr, B_top, B_ref
     // profiling
     bool prof = false;
     KProf kp[FPM_K_COUNT];
@@ -574,16 +575,16 @@ int enqueue_search(fpm_ctx* ctx) {
     }
     const SrcLevel& top = ctx->src[L];
     const TmplLevel& tt = ctx->tmpl[L];
+    // profiling bytes: each kernel's share of §8(d)'s B_top = sum_angles (W_L H_L + 4 |R_a|): the rotation reads the
+    // top level, the correlation writes the map (the rotated canvases are this design's scratch)
     {
-        int64_t bytes = 0;
-        for (int a = 0; a < P.nang; ++a) bytes += (int64_t)top.w * top.h + (int64_t)P.top[a].bw * P.top[a].bh;
+        const int64_t bytes = (int64_t)P.nang * top.w * top.h;
         ProfScope ps(ctx, FPM_K_TOP_WARP, bytes * S);
         launch_warp(P.d_jobs.as<WarpJob>(P.off_warp), J, P.max_canvas, st);
     }
     {
         int64_t bytes = 0;
-        for (int a = 0; a < P.nang; ++a)
-            bytes += (int64_t)P.top[a].bw * P.top[a].bh + (int64_t)tt.w * tt.h + 4LL * P.map_w[a] * P.map_h[a];
+        for (int a = 0; a < P.nang; ++a) bytes += 4LL * P.map_w[a] * P.map_h[a];
         ProfScope ps(ctx, FPM_K_TOP_NCC, bytes * S);
         if (ncc_tile_fits(tt.w, tt.h)) {
             int mw = 0, mh = 0;
@@ -594,9 +595,7 @@ int enqueue_search(fpm_ctx* ctx) {
         }
     }
     {
-        int64_t bytes = 0;
-        for (int a = 0; a < P.nang; ++a) bytes += 4LL * P.map_w[a] * P.map_h[a];
-        ProfScope ps(ctx, FPM_K_TOP_NMS, bytes * S);
+        ProfScope ps(ctx, FPM_K_TOP_NMS, 0);   // (reads the maps counted once in B_top)
         NmsArgs na;
         na.jobs = P.d_jobs.as<NmsJob>(P.off_nms);
         na.peaks = P.d_peaks.as<Peak>();
@@ -957,26 +956,39 @@ int complete_staged(fpm_ctx* ctx, std::vector<std::vector<fpm_result>>& results,
     static const int32_t zeros[64] = {};
     const int32_t* lc = P.nang > 0 ? (const int32_t*)(h + P.h_live) : zeros;
     for (int d = 0; d < P.L; ++d) ctx->stats.push_back(lc[d]);
-    if (ctx->prof && P.nang > 0) {   // refinement bytes need the live counts
+    // SURVEY.md §8(d) algorithmic bytes (compulsory input + output of each stage, u8 = 1 B, f32 = 4 B; scratch
+    // between the stages of this design is not counted), summed over the batch:
+    //   B_pyr = sum_{l<L} (W_l H_l + W_{l+1} H_{l+1});  B_top = sum_angles (W_L H_L + 4 |R_a|);
+    //   B_ref = sum_{l<L} sum_{live ROIs at l} ((w_l + 6)(h_l + 6) + w_l h_l + 49 * 4)
+    {
+        int64_t bp = 0, bt = 0, br = 0;
+        for (int l = 0; l < P.L; ++l)
+            bp += (int64_t)ctx->src[l].w * ctx->src[l].h + (int64_t)ctx->src[l + 1].w * ctx->src[l + 1].h;
+        for (int a = 0; a < P.nang; ++a)
+            bt += (int64_t)ctx->src[P.L].w * ctx->src[P.L].h + 4LL * P.map_w[a] * P.map_h[a];
+        for (int d = 0; d < P.L && P.nang > 0; ++d) {
+            const TmplLevel& t = ctx->tmpl[P.L - 1 - d];
+            br += (int64_t)lc[d] * P.n3 * ((int64_t)(t.w + 6) * (t.h + 6) + (int64_t)t.w * t.h + 49 * 4);
+        }
+        ctx->alg_bytes[0] = bp * P.S;
+        ctx->alg_bytes[1] = bt * P.S;
+        ctx->alg_bytes[2] = br;
+    }
+    if (ctx->prof && P.nang > 0) {   // per-kernel share of B_ref (the live counts are known only now)
         for (int d = 0; d < P.L; ++d) {
             const int l = P.L - 1 - d;
             const TmplLevel& t = ctx->tmpl[l];
             const int64_t rois = (int64_t)lc[d] * P.n3;
-            const int rc = roi_pick_rc(t.w, t.h);
-            const int64_t nch = (t.h + rc - 1) / rc;
-            if (roi_small_fits(t.w, t.h)) {   // one kernel: source samples + template in, one record out
-                ctx->kp[FPM_K_ROI_SMALL].bytes +=
-                    rois * ((int64_t)(t.w + 6) * (t.h + 6) + (int64_t)t.w * t.h + (int64_t)sizeof(RoiRecord));
+            const int64_t foot = (int64_t)(t.w + 6) * (t.h + 6), tmpl = (int64_t)t.w * t.h;
+            if (roi_small_fits(t.w, t.h)) {   // one kernel: footprint + template in, the 7x7 scores out
+                ctx->kp[FPM_K_ROI_SMALL].bytes += rois * (foot + tmpl + 49 * 4);
                 continue;
             }
-            // tables: written tables + descriptors; warp: one source sample per ROI pixel read + the ROI written;
-            // corr: ROI + template read, row sums + window partials written; eval: those read, one record written
-            ctx->kp[FPM_K_ROI_TABLES].bytes +=
-                rois * (int64_t)(8 * (t.w + 6) + 8 * (t.h + 6) + 16 * (((t.w + 37) / 32) * ((t.h + 37) / 32)));
-            ctx->kp[FPM_K_ROI_WARP].bytes += rois * 2 * (int64_t)(t.w + 6) * (t.h + 6);
-            ctx->kp[FPM_K_ROI_CORR].bytes +=
-                rois * ((int64_t)(t.w + 6) * (t.h + 6) + (int64_t)t.w * t.h + (int64_t)t.h * 49 * 4 + nch * 49 * 12);
-            ctx->kp[FPM_K_ROI_EVAL].bytes += rois * ((int64_t)t.h * 49 * 4 + nch * 49 * 12 + (int64_t)sizeof(RoiRecord));
+            // the sampled ROI, row sums and window partials are this design's scratch, not §8(d) traffic: the
+            // sampling kernel is charged the footprint read, the correlation the template, the evaluation the scores
+            ctx->kp[FPM_K_ROI_WARP].bytes += rois * foot;
+            ctx->kp[FPM_K_ROI_CORR].bytes += rois * tmpl;
+            ctx->kp[FPM_K_ROI_EVAL].bytes += rois * 49 * 4;
         }
     }
     const auto c2 = std::chrono::steady_clock::now();
@@ -1292,6 +1304,14 @@ int fpm_merge_candidates(const fpm_params* p, int32_t tmpl_w, int32_t tmpl_h, co
     *n_results = (int32_t)res.size();
     for (int i = 0; i < (int)res.size() && i < cap && out; ++i) out[i] = res[i];
     return (int)res.size() > cap ? FPM_E_CAPACITY : FPM_OK;
+}
+
+int fpm_search_bytes(const fpm_ctx* ctx, int64_t* b_pyr, int64_t* b_top, int64_t* b_ref) {
+    if (!ctx || !b_pyr || !b_top || !b_ref) return FPM_E_INVALID_ARG;
+    *b_pyr = ctx->alg_bytes[0];
+    *b_top = ctx->alg_bytes[1];
+    *b_ref = ctx->alg_bytes[2];
+    return FPM_OK;
 }
 
 int fpm_search_stats(const fpm_ctx* ctx, int64_t* stats, int32_t cap) {

@@ -256,6 +256,12 @@ class TemplateMatcher:
                                           n.value, C.byref(n))
         return out
 
+    def search_bytes(self) -> Tuple[int, int, int]:
+        """(B_pyr, B_top, B_ref): SURVEY.md §8(d) algorithmic bytes of the last search (fpm_search_bytes)."""
+        a, b, c = C.c_int64(), C.c_int64(), C.c_int64()
+        self._lib.fpm_search_bytes(self._ctx, C.byref(a), C.byref(b), C.byref(c))
+        return a.value, b.value, c.value
+
     def search_stats(self) -> List[int]:
         buf = (C.c_int64 * 64)()
         k = self._lib.fpm_search_stats(self._ctx, buf, 64)

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define FPM_ABI_VERSION 7
+#define FPM_ABI_VERSION 8
 
 /* status codes */
 #define FPM_OK 0
@@ -186,11 +186,16 @@ int fpm_template_level(const fpm_ctx* ctx, int32_t level, int32_t* w, int32_t* h
  *   [0] top-layer angles  [1] top-layer candidates  [2..2+L) live candidates entering layer L-1..0
  * Returns the number of entries written. */
 int fpm_search_stats(const fpm_ctx* ctx, int64_t* stats, int32_t cap);
+/* SURVEY.md §8(d) algorithmic bytes of the last search, summed over its sources: B_pyr (pyramid in + out), B_top
+ * (top-layer level read per angle + the f32 maps), B_ref (per live refinement ROI: the source footprint, the template
+ * level and the 7x7 f32 scores).  The roofline's achieved bandwidth is these bytes over the measured time. */
+int fpm_search_bytes(const fpm_ctx* ctx, int64_t* b_pyr, int64_t* b_top, int64_t* b_ref);
 
 /* Kernel timing: when enabled, HIP events bracket every launch of each kernel on the context's stream (the
  * search then runs eagerly instead of as a replayed graph); fpm_profile_get returns total milliseconds, launch
  * count and algorithmic bytes (compulsory inputs + outputs, u8 = 1 B, f32 = 4 B) accumulated since the last
- * reset.  One index per kernel. */
+ * reset (bytes: each kernel's share of SURVEY.md §8(d)'s per-stage figures, as fpm_search_bytes; intermediate
+ * scratch of this design is not counted).  One index per kernel. */
 #define FPM_K_PYR 0         /* k_pyr_down     K1 pyrDown                                          */
 #define FPM_K_TOP_WARP 1    /* k_warp         K2 top-layer rotation                               */
 #define FPM_K_TOP_NCC 2     /* k_ncc_tile / k_ncc_map  K3+K4 top-layer CCORR + normalisation      */
