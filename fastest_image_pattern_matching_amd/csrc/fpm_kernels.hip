@@ -1429,6 +1429,24 @@ __device__ __forceinline__ int ft_tap_bytes(const uint8_t* FT, int off, int ftw,
     return (32 * h0 + __mul24(fy, h1 - h0) + 512) >> 10;
 }
 
+// Interior taps addressed directly in the LDS address space: the caller offsets the fixed-point row coordinates by
+// whole multiples of 2^10 per tile so that (X0 + ad) >> 10 is the tap's column inside the wave's footprint plus the
+// footprint's LDS byte offset and (Y0 + bd) >> 10 its footprint row; the byte address is then one 24-bit
+// multiply-add and every ds_read carries its own offset (no base adds), fractions untouched.
+typedef __attribute__((address_space(3))) const uint8_t fpm_lds_u8;
+__device__ __forceinline__ uint32_t lds_offset_of(const uint8_t* p) { return (uint32_t)(size_t)(fpm_lds_u8*)p; }
+// the four taps of one pixel: (p, p + 1) and (p + ftw, p + ftw + 1)
+__device__ __forceinline__ void lds_taps(uint32_t off, int ftw, int v[4]) {
+    fpm_lds_u8* p = (fpm_lds_u8*)(size_t)off;
+    fpm_lds_u8* q = (fpm_lds_u8*)(size_t)(off + ftw);
+    v[0] = p[0]; v[1] = p[1]; v[2] = q[0]; v[3] = q[1];
+}
+// (32*h0 + fy*(h1 - h0) + 512) >> 10 with h = 32*va + fx*(vb - va), on the 24-bit multiplier only
+__device__ __forceinline__ int bilerp24(const int v[4], int fx, int fy) {
+    const int h0 = mad24(fx, v[1] - v[0], v[0] << 5), h1 = mad24(fx, v[3] - v[2], v[2] << 5);
+    return mad24(fy, h1 - h0, (h0 << 5) + 512) >> 10;
+}
+
 // One bilinear ROI pixel from a staged footprint, BORDER_CONSTANT(0) rules of remapBilinear (general path).
 __device__ __forceinline__ int ft_tap_general(const uint8_t* FT, int ftw, int bxa, int by0, int W, int H, int X, int Y) {
     const int sx = sat_s16(X >> kInterBits), sy = sat_s16(Y >> kInterBits);
@@ -1741,9 +1759,8 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
             continue;
         }
         const int adv[4] = {A.x, A.y, A.z, A.w}, bdv[4] = {B.x, B.y, B.z, B.w};
-        if ((flags & kTileInterior) && in_lds) {
+        if ((flags & kTileInterior) && in_lds && ABL == 4) {
             const int obase = by0 * ftw + bxa;
-            // columns past the ROI's right edge are zero: one byte mask per lane instead of a select per pixel
             const int nvalid = RW - c0;
             const uint32_t colmask = nvalid >= 4 ? 0xffffffffu : (1u << (8 * nvalid)) - 1u;
 #pragma unroll
@@ -1756,10 +1773,39 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
                     const int X = (X0r[i] + adv[u]) >> (kAbBits - kInterBits);
                     const int Y = (Y0r[i] + bdv[u]) >> (kAbBits - kInterBits);
                     const int off = mad24(Y >> kInterBits, ftw, (X >> kInterBits) - obase);
-                    const int v = ABL == 4 ? ft_tap_interior(FT, off, ftw, X, Y) : ft_tap_bytes(FT, off, ftw, X, Y);
-                    pk |= (uint32_t)v << (8 * u);
+                    pk |= (uint32_t)ft_tap_interior(FT, off, ftw, X, Y) << (8 * u);
                 }
                 *(uint32_t*)(dst + (size_t)r * ROI_T) = pk & colmask;
+            }
+            continue;
+        }
+        if ((flags & kTileInterior) && in_lds) {
+            // columns past the ROI's right edge are zero: one byte mask per lane instead of a select per pixel
+            const int nvalid = RW - c0;
+            const uint32_t colmask = nvalid >= 4 ? 0xffffffffu : (1u << (8 * nvalid)) - 1u;
+            const int xo = ((int)lds_offset_of(FT) - bxa) << kAbBits, yo = -(by0 << kAbBits);
+            // one output row (4 pixels) at a time: all 16 tap reads issued before any arithmetic (measured: 126.8 ->
+            // 113.1 us per Src7 layer-0 launch at 8 sources with the folded addressing, scripts/warp_exp.hip; rows
+            // past the tile repeat its last row's coordinates and are not stored)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = ry0 + lr + 8 * i;
+                const int x0r = X0r[i] + xo, y0r = Y0r[i] + yo;
+                uint32_t off[4];
+                int fxv[4], fyv[4], v[4][4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int sxv = x0r + adv[u], syv = y0r + bdv[u];
+                    fxv[u] = __builtin_amdgcn_ubfe(sxv, kAbBits - kInterBits, kInterBits);
+                    fyv[u] = __builtin_amdgcn_ubfe(syv, kAbBits - kInterBits, kInterBits);
+                    off[u] = (uint32_t)mad24(syv >> kAbBits, ftw, sxv >> kAbBits);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) lds_taps(off[u], ftw, v[u]);
+                uint32_t pk = 0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) pk |= (uint32_t)bilerp24(v[u], fxv[u], fyv[u]) << (8 * u);
+                if (r <= ry1) *(uint32_t*)(dst + (size_t)r * ROI_T) = pk & colmask;
             }
             continue;
         }
@@ -2244,24 +2290,48 @@ __global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
             int ad4[4], bd4[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) { ad4[u] = lad[c0 + u]; bd4[u] = lbd[c0 + u]; }
-            for (int r = rl < nrl ? rl : RH; r < RH; r += nrl) {
-                const int X0 = lx0[r], Y0 = ly0[r];
-                uint32_t pk = 0;
+            if (g_interior && MODE != 5) {   // folded LDS addressing, a row's 16 tap reads before its arithmetic
+                const int xo = ((int)lds_offset_of(FT) - gbxa) << kAbBits, yo = -(gby0 << kAbBits);
+                const int nvalid = RW - c0;
+                const uint32_t colmask = nvalid >= 4 ? 0xffffffffu : (nvalid <= 0 ? 0u : (1u << (8 * nvalid)) - 1u);
+                for (int r = rl < nrl ? rl : RH; r < RH; r += nrl) {
+                    const int x0r = lx0[r] + xo, y0r = ly0[r] + yo;
+                    uint32_t off[4];
+                    int fxv[4], fyv[4], v[4][4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int X = (X0 + ad4[u]) >> (kAbBits - kInterBits);
-                    const int Y = (Y0 + bd4[u]) >> (kAbBits - kInterBits);
-                    int v;
-                    if (g_interior) {
-                        const int off = mad24(Y >> kInterBits, gftw, (X >> kInterBits) - gobase);
-                        v = MODE == 5 ? ft_tap_bytes(FT, off, gftw, X, Y) : ft_tap_interior(FT, off, gftw, X, Y);
-                    } else {
-                        v = ft_tap_general(FT, gftw, gbxa, gby0, W, H, X, Y);
+                    for (int u = 0; u < 4; ++u) {
+                        const int sxv = x0r + ad4[u], syv = y0r + bd4[u];
+                        fxv[u] = __builtin_amdgcn_ubfe(sxv, kAbBits - kInterBits, kInterBits);
+                        fyv[u] = __builtin_amdgcn_ubfe(syv, kAbBits - kInterBits, kInterBits);
+                        off[u] = (uint32_t)mad24(syv >> kAbBits, gftw, sxv >> kAbBits);
                     }
-                    if (c0 + u >= RW) v = 0;
-                    pk |= (uint32_t)v << (8 * u);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) lds_taps(off[u], gftw, v[u]);
+                    uint32_t pk = 0;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) pk |= (uint32_t)bilerp24(v[u], fxv[u], fyv[u]) << (8 * u);
+                    *(uint32_t*)(SB + r * SBp + c0) = pk & colmask;
                 }
-                *(uint32_t*)(SB + r * SBp + c0) = pk;
+            } else {
+                for (int r = rl < nrl ? rl : RH; r < RH; r += nrl) {
+                    const int X0 = lx0[r], Y0 = ly0[r];
+                    uint32_t pk = 0;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int X = (X0 + ad4[u]) >> (kAbBits - kInterBits);
+                        const int Y = (Y0 + bd4[u]) >> (kAbBits - kInterBits);
+                        int v;
+                        if (g_interior) {
+                            const int off = mad24(Y >> kInterBits, gftw, (X >> kInterBits) - gobase);
+                            v = ft_tap_bytes(FT, off, gftw, X, Y);
+                        } else {
+                            v = ft_tap_general(FT, gftw, gbxa, gby0, W, H, X, Y);
+                        }
+                        if (c0 + u >= RW) v = 0;
+                        pk |= (uint32_t)v << (8 * u);
+                    }
+                    *(uint32_t*)(SB + r * SBp + c0) = pk;
+                }
             }
             STAMP(9);
         } else if (!g_any) {   // the ROI lies entirely outside the image: all zero (BORDER_CONSTANT 0)
