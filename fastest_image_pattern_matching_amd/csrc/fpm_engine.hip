@@ -100,7 +100,7 @@ struct Plan {
     size_t canvas_bytes = 0, map_floats = 0, blk_count = 0;
     int max_canvas = 0, max_map = 0, max_nblk = 0, max_cells = 0;
     // device buffers owned by the plan
-    DevBuf d_ncand, d_ncnt;                    // s_BlockMax candidate lists (k_nms_blocks -> k_nms_fast)
+    DevBuf d_ncand;                            // s_BlockMax candidate lists (k_nms_blocks -> k_nms_fast)
     DevBuf d_canvas, d_map, d_bmax, d_bloc, d_jobs, d_nodes, d_top, d_topn, d_peaks, d_counts, d_state,
         d_live, d_livecnt, d_rec, d_rowsum, d_wsum, d_wsq, d_tab, d_roi, d_tdesc;
     int tabw = 0, tabh = 0, roi_pitch = 0, tdesc_stride = 1;
@@ -111,7 +111,7 @@ struct Plan {
     size_t h_counts = 0, h_peaks = 0, h_live = 0, h_live0 = 0, h_state = 0, h_rec = 0, h_total = 0;
     char* h_dev = nullptr;   // device-side address of h_out (k_pack writes it over PCIe)
     void release() {
-        for (DevBuf* b : {&d_ncand, &d_ncnt, &d_canvas, &d_map, &d_bmax, &d_bloc, &d_jobs, &d_nodes, &d_top, &d_topn, &d_peaks,
+        for (DevBuf* b : {&d_ncand, &d_canvas, &d_map, &d_bmax, &d_bloc, &d_jobs, &d_nodes, &d_top, &d_topn, &d_peaks,
                           &d_counts, &d_state, &d_live, &d_livecnt, &d_rec, &d_rowsum, &d_wsum, &d_wsq, &d_tab, &d_roi, &d_tdesc})
             b->release();
         h_out.release();
@@ -422,13 +422,11 @@ int build_plan(fpm_ctx* ctx) {
     HIP_TRY(P.d_topn.ensure(sizeof(AngleNode) * P.nang));
     HIP_TRY(P.d_peaks.ensure(sizeof(Peak) * (size_t)P.C));
     HIP_TRY(P.d_counts.ensure(sizeof(int32_t) * J));
-    if (P.by_block) {
-        HIP_TRY(P.d_ncand.ensure(sizeof(int32_t) * (size_t)kNmsCandCap * J));
-        HIP_TRY(P.d_ncnt.ensure(sizeof(int32_t) * J));
-    }
+    if (P.by_block) HIP_TRY(P.d_ncand.ensure(sizeof(int32_t) * (size_t)kNmsCandCap * J));
     HIP_TRY(P.d_state.ensure(sizeof(CandState) * (size_t)P.C));
     HIP_TRY(P.d_live.ensure(sizeof(int32_t) * (size_t)P.C * 2));
-    HIP_TRY(P.d_livecnt.ensure(sizeof(int32_t) * (L + 2)));
+    // live counts [L + 2], then (s_BlockMax) the per-map candidate counts [J]: zeroed together by k_warp
+    HIP_TRY(P.d_livecnt.ensure(sizeof(int32_t) * ((size_t)L + 2 + (P.by_block ? J : 0))));
     HIP_TRY(P.d_rec.ensure(sizeof(RoiRecord) * (size_t)P.C * P.n3));
     {   // refinement scratch per ROI (tables, sampled ROI, row sums, window partials); bounded, rounds cover the rest
         size_t max_rows = 1, max_chunks = 1;
@@ -580,7 +578,8 @@ int enqueue_search(fpm_ctx* ctx) {
     {
         const int64_t bytes = (int64_t)P.nang * top.w * top.h;
         ProfScope ps(ctx, FPM_K_TOP_WARP, bytes * S);
-        launch_warp(P.d_jobs.as<WarpJob>(P.off_warp), J, P.max_canvas, st);
+        launch_warp(P.d_jobs.as<WarpJob>(P.off_warp), J, P.max_canvas, st, P.d_livecnt.as<int32_t>(),
+                    L + 2 + (P.by_block ? J : 0));
     }
     {
         int64_t bytes = 0;
@@ -605,15 +604,13 @@ int enqueue_search(fpm_ctx* ctx) {
         na.thr = P.layer_score[L]; na.overlap = ctx->prm.max_overlap;
         na.lds_blocks = 0;
         na.cand = nullptr; na.cand_cnt = nullptr; na.cand_cap = 0; na.cand_lds = 0; na.stamps = nullptr;
-        if (P.by_block) {
-            HIP_TRY(hipMemsetAsync(P.d_ncnt.p, 0, sizeof(int32_t) * J, st));
-            na.cand = P.d_ncand.as<int32_t>(); na.cand_cnt = P.d_ncnt.as<int32_t>(); na.cand_cap = kNmsCandCap;
+        if (P.by_block) {   // (the counts were zeroed by k_warp)
+            na.cand = P.d_ncand.as<int32_t>(); na.cand_cnt = P.d_livecnt.as<int32_t>() + L + 2; na.cand_cap = kNmsCandCap;
         }
         int mdim = 0;
         for (int a = 0; a < P.nang; ++a) mdim = std::max(mdim, std::max(P.map_w[a], P.map_h[a]));
         launch_nms(na, J, P.max_nblk, mdim, P.max_cells, st);
     }
-    HIP_TRY(hipMemsetAsync(P.d_livecnt.p, 0, sizeof(int32_t) * (L + 2), st));
     int32_t* live[2] = {P.d_live.as<int32_t>(), P.d_live.as<int32_t>() + P.C};
     int32_t* livecnt = P.d_livecnt.as<int32_t>();
     {
@@ -800,6 +797,50 @@ void collect_candidates(fpm_ctx* ctx, int s, const std::vector<int>& pos, std::v
     }
 }
 
+// vecAllResult after filterWithScore (:214, :262-358, :373-378) when that needs no sort emulation: if the kept
+// candidates scoring at least the threshold have pairwise distinct scores (and none is NaN), the sorted order after
+// filterWithScore is the unique descending order, whatever the push order and the first std::sort did with equal
+// top scores.  LSD radix sort on order-preserving 64-bit keys; false (nothing decided) on a tie or a NaN, and the
+// caller replays both std::sorts.
+static bool select_distinct_scores(const fpm_params& prm, const fpm_candidate* cand, int n, std::vector<HostMatch>& all) {
+    struct SK { uint64_t k; int32_t i; };
+    std::vector<SK> a, b;
+    a.reserve(n);
+    for (int i = 0; i < n; ++i) {
+        const fpm_candidate& c = cand[i];
+        if (!c.kept) continue;
+        if (std::isnan(c.score)) return false;
+        if (c.score < prm.score) continue;
+        uint64_t u;
+        std::memcpy(&u, &c.score, 8);
+        u = (u >> 63) ? ~u : (u | (1ULL << 63));   // ascending key = ascending score
+        a.push_back({~u, i});                        // ascending ~key = descending score
+    }
+    const size_t m = a.size();
+    b.resize(m);
+    uint64_t diff = 0;
+    for (size_t t = 1; t < m; ++t) diff |= a[t].k ^ a[0].k;
+    for (int sh = 0; sh < 64; sh += 8) {
+        if (!((diff >> sh) & 0xFF)) continue;   // every key shares this byte
+        size_t cnt[257] = {};
+        for (const SK& e : a) cnt[((e.k >> sh) & 0xFF) + 1]++;
+        for (int d = 0; d < 256; ++d) cnt[d + 1] += cnt[d];
+        for (const SK& e : a) b[cnt[(e.k >> sh) & 0xFF]++] = e;
+        a.swap(b);
+    }
+    for (size_t t = 1; t < m; ++t)
+        if (cand[a[t].i].score == cand[a[t - 1].i].score) return false;   // equal scores (+0 == -0 included)
+    all.clear();
+    all.reserve(m);
+    for (const SK& e : a) {
+        const fpm_candidate& c = cand[e.i];
+        HostMatch h{};
+        h.ptx = c.x; h.pty = c.y; h.score = c.score; h.angle = c.angle;
+        all.push_back(h);
+    }
+    return true;
+}
+
 // Returns false when `cand` is not in push order (angle_index ascending, peak_rank 0, 1, ... within an angle).
 bool merge_candidates(const fpm_params& prm, int t0w, int t0h, const fpm_candidate* cand, int n,
                       std::vector<fpm_result>& out) {
@@ -810,32 +851,42 @@ bool merge_candidates(const fpm_params& prm, int t0w, int t0h, const fpm_candida
                   : cand[i].peak_rank != cand[i - 1].peak_rank + 1)
             return false;
     }
-    // std::sort(vecMatchParameter, compareScoreBig2Small) (:214) over the push-order sequence.  The permutation
-    // std::sort produces depends only on the sequence of comparison results, so sorting light (score, index) keys
-    // with the same comparator reproduces the reference's order of equal scores exactly.
-    struct Key { double score; int i; };
-    std::vector<Key> order(n);
-    for (int i = 0; i < n; ++i) order[i] = {cand[i].top_score, i};
-    std::sort(order.begin(), order.end(), [](const Key& l, const Key& r) { return l.score > r.score; });
     std::vector<HostMatch> all;
-    all.reserve(n);
-    for (const Key& k : order) {   // vecAllResult in sorted-candidate order (:262-358)
-        const fpm_candidate& c = cand[k.i];
-        if (!c.kept) continue;
-        HostMatch m{};
-        m.ptx = c.x; m.pty = c.y; m.score = c.score; m.angle = c.angle;
-        all.push_back(m);
+    if (!select_distinct_scores(prm, cand, n, all)) {
+        // std::sort(vecMatchParameter, compareScoreBig2Small) (:214) over the push-order sequence.  The permutation
+        // std::sort produces depends only on the sequence of comparison results, so sorting light (score, index)
+        // keys with the same comparator reproduces the reference's order of equal scores exactly.
+        struct Key { double score; int i; };
+        std::vector<Key> order(n);
+        for (int i = 0; i < n; ++i) order[i] = {cand[i].top_score, i};
+        std::sort(order.begin(), order.end(), [](const Key& l, const Key& r) { return l.score > r.score; });
+        all.clear();
+        all.reserve(n);
+        for (const Key& k : order) {   // vecAllResult in sorted-candidate order (:262-358)
+            const fpm_candidate& c = cand[k.i];
+            if (!c.kept) continue;
+            HostMatch m{};
+            m.ptx = c.x; m.pty = c.y; m.score = c.score; m.angle = c.angle;
+            all.push_back(m);
+        }
+        filter_with_score(all, prm.score);
     }
-    filter_with_score(all, prm.score);
-    for (HostMatch& m : all) {   // :380-390
-        const double rad = -m.angle * kD2R;
-        const float c = (float)std::cos(rad), sn = (float)std::sin(rad);
-        const F2 lt = f2((float)m.ptx, (float)m.pty);
-        const F2 rt = f2(lt.x + t0w * c, lt.y - t0w * sn);
-        const F2 rb = f2(rt.x + t0h * sn, rt.y + t0h * c);
-        m.rect = rrect_from3(lt, rt, rb);
-        m.del = false;
-    }
+    // rotated rectangles (:380-390), per candidate
+    auto rects = [&](int i0, int i1) {
+        for (int i = i0; i < i1; ++i) {
+            HostMatch& m = all[i];
+            const double rad = -m.angle * kD2R;
+            const float c = (float)std::cos(rad), sn = (float)std::sin(rad);
+            const F2 lt = f2((float)m.ptx, (float)m.pty);
+            const F2 rt = f2(lt.x + t0w * c, lt.y - t0w * sn);
+            const F2 rb = f2(rt.x + t0h * sn, rt.y + t0h * c);
+            m.rect = rrect_from3(lt, rt, rb);
+            m.del = false;
+        }
+    };
+    const int na = (int)all.size();
+    if (na <= 512) rects(0, na);
+    else host_parallel((na + 511) / 512, [&](int t) { rects(t * 512, std::min(na, t * 512 + 512)); });
     filter_with_rotated_rect(all, prm.max_overlap);
     std::sort(all.begin(), all.end(), score_big2small);
     if (prm.semantics == FPM_SEMANTICS_MFC) {   // MatchToolDlg.cpp:1080-1116

@@ -9,10 +9,18 @@
 #include <atomic>
 #include <cfloat>
 #include <cmath>
+#include <chrono>
+#include <condition_variable>
 #include <cstdlib>
+#include <functional>
+#include <mutex>
 #include <thread>
+#include <immintrin.h>
 
 namespace fpm {
+#ifdef FPM_HOST_STATS
+long g_stats[40];
+#endif
 
 bool score_big2small(const HostMatch& a, const HostMatch& b) { return a.score > b.score; }
 
@@ -28,6 +36,94 @@ static int host_threads() {
         return std::max(1, std::min(hw, 8));
     }();
     return n;
+}
+
+// Persistent worker pool for the host tail's independent pieces (per-candidate geometry, per-cluster overlap
+// tests).  Thread creation per search cost more than the work it spread; the workers spin for a short while after
+// a region (the tail runs a few regions back to back) and then sleep on a condition variable.  One region at a time:
+// a caller that finds the pool busy (another context finishing on another host thread) runs its tasks inline.
+// Results never depend on which thread runs a task.
+namespace {
+struct Pool {
+    std::mutex m, region;
+    std::condition_variable cv;
+    std::atomic<uint64_t> gen{0};
+    const std::function<void(int)>* fn = nullptr;   // guarded by m; null between regions
+    int ntasks = 0;
+    std::atomic<int> next{0}, done{0}, active{0};
+
+    void worker() {
+        uint64_t seen = 0;
+        for (;;) {
+            const auto t0 = std::chrono::steady_clock::now();
+            while (gen.load(std::memory_order_acquire) == seen) {
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(300)) {
+                    std::unique_lock<std::mutex> lk(m);
+                    cv.wait(lk, [&] { return gen.load(std::memory_order_acquire) != seen; });
+                } else {
+                    _mm_pause();
+                }
+            }
+            const std::function<void(int)>* f;
+            int nt;
+            {
+                std::lock_guard<std::mutex> lk(m);
+                seen = gen.load(std::memory_order_acquire);
+                f = fn;
+                nt = ntasks;
+                if (f) active.fetch_add(1, std::memory_order_acq_rel);
+            }
+            if (!f) continue;
+            for (int t = next.fetch_add(1); t < nt; t = next.fetch_add(1)) {
+                (*f)(t);
+                done.fetch_add(1, std::memory_order_acq_rel);
+            }
+            active.fetch_sub(1, std::memory_order_acq_rel);
+        }
+    }
+};
+
+Pool* pool_instance(int workers) {   // leaked on purpose: workers block forever, nothing to tear down at exit
+    static Pool* p = [&] {
+        Pool* q = new Pool;
+        for (int i = 0; i < workers; ++i) std::thread([q] { q->worker(); }).detach();
+        return q;
+    }();
+    return p;
+}
+}  // namespace
+
+void host_parallel(int ntasks, const std::function<void(int)>& fn) {
+    const int nthreads = host_threads();
+    if (ntasks <= 1 || nthreads <= 1) {
+        for (int t = 0; t < ntasks; ++t) fn(t);
+        return;
+    }
+    Pool* p = pool_instance(nthreads - 1);
+    std::unique_lock<std::mutex> reg(p->region, std::try_to_lock);
+    if (!reg.owns_lock()) {
+        for (int t = 0; t < ntasks; ++t) fn(t);
+        return;
+    }
+    {
+        std::lock_guard<std::mutex> lk(p->m);
+        p->fn = &fn;
+        p->ntasks = ntasks;
+        p->next.store(0);
+        p->done.store(0);
+        p->gen.fetch_add(1, std::memory_order_acq_rel);
+    }
+    p->cv.notify_all();
+    for (int t = p->next.fetch_add(1); t < ntasks; t = p->next.fetch_add(1)) {
+        fn(t);
+        p->done.fetch_add(1, std::memory_order_acq_rel);
+    }
+    while (p->done.load(std::memory_order_acquire) < ntasks) _mm_pause();
+    {
+        std::lock_guard<std::mutex> lk(p->m);
+        p->fn = nullptr;   // workers that wake from here on skip this region
+    }
+    while (p->active.load(std::memory_order_acquire) > 0) _mm_pause();
 }
 
 static inline double len2(float x, float y) { return std::sqrt((double)x * x + (double)y * y); }
@@ -57,31 +153,24 @@ static void rrect_corners(const RRect& r, F2 pt[4]) {
 }
 
 // returns 0 = INTERSECT_NONE, 1 = INTERSECT_PARTIAL, 2 = INTERSECT_FULL
-// the same on precomputed corners (rrect_corners of ra / rb)
-static int rrect_intersection_c(const RRect& ra, const RRect& rb, const F2* A, const F2* B, std::vector<F2>& pts);
-
-int rrect_intersection(const RRect& ra, const RRect& rb, std::vector<F2>& pts) {
-    F2 A[4], B[4];
-    rrect_corners(ra, A);
-    rrect_corners(rb, B);
-    return rrect_intersection_c(ra, rb, A, B, pts);
-}
-
-static int rrect_intersection_c(const RRect& ra, const RRect& rb, const F2* A, const F2* B, std::vector<F2>& pts) {
-    pts.clear();
+// on precomputed corners (rrect_corners of ra / rb), into a fixed array: at most 16 edge crossings + 8 corners
+// before the near-duplicate pass, at most 8 after it (cv::rotatedRectangleIntersection, OpenCV 4.5.x)
+static int rrect_isect(const RRect& ra, const RRect& rb, const F2* A, const F2* B, F2* pts, int* np) {
+    int n = 0;
     F2 eA[4], eB[4];
     float eps = 1e-6f * std::max(ra.w * ra.h, rb.w * rb.h);
     bool coincident = true;
     for (int i = 0; i < 4 && coincident; ++i)
         coincident = !(std::fabs(A[i].x - B[i].x) > eps || std::fabs(A[i].y - B[i].y) > eps);
     if (coincident) {
-        pts.assign(A, A + 4);
+        for (int i = 0; i < 4; ++i) pts[i] = A[i];
+        *np = 4;
         return 2;
     }
     for (int i = 0; i < 4; ++i) {
-        const int n = (i + 1) & 3;
-        eA[i] = f2(A[n].x - A[i].x, A[n].y - A[i].y);
-        eB[i] = f2(B[n].x - B[i].x, B[n].y - B[i].y);
+        const int k = (i + 1) & 3;
+        eA[i] = f2(A[k].x - A[i].x, A[k].y - A[i].y);
+        eB[i] = f2(B[k].x - B[i].x, B[k].y - B[i].y);
     }
     for (int i = 0; i < 4; ++i) {
         eps = std::min(eps, std::sqrt(eA[i].x * eA[i].x + eA[i].y * eA[i].y));
@@ -99,10 +188,10 @@ static int rrect_intersection_c(const RRect& ra, const RRect& rb, const F2* A, c
             const float tb = (eA[i].x * dy - eA[i].y * dx) / det;
             if (!std::isfinite(ta) || !std::isfinite(tb)) continue;
             if (ta >= 0.0f && ta <= 1.0f && tb >= 0.0f && tb <= 1.0f)
-                pts.push_back(f2(A[i].x + eA[i].x * ta, A[i].y + eA[i].y * ta));
+                pts[n++] = f2(A[i].x + eA[i].x * ta, A[i].y + eA[i].y * ta);
         }
     }
-    if (!pts.empty()) kind = 1;
+    if (n > 0) kind = 1;
     // corners of one rectangle inside the other (sign test against the 4 edge lines)
     auto inside = [](const F2& p, const F2* Q, const F2* eQ) {
         int pos = 0, neg = 0;
@@ -115,13 +204,11 @@ static int rrect_intersection_c(const RRect& ra, const RRect& rb, const F2* A, c
         return pos == 4 || neg == 4;
     };
     for (int i = 0; i < 4; ++i)
-        if (inside(A[i], B, eB)) pts.push_back(A[i]);
+        if (inside(A[i], B, eB)) pts[n++] = A[i];
     for (int i = 0; i < 4; ++i)
-        if (inside(B[i], A, eA)) pts.push_back(B[i]);
-    int n = (int)pts.size();
-    if (n == 0) return 0;
+        if (inside(B[i], A, eA)) pts[n++] = B[i];
+    if (n == 0) { *np = 0; return 0; }
     // drop near-duplicates (swap-with-last), remembering pairwise distances for the > 8 pass
-    // (n <= 16 edge crossings + 8 corners)
     const int stride = n;
     float dist[24 * 24];
     int slot[24];
@@ -153,20 +240,31 @@ static int rrect_intersection_c(const RRect& ra, const RRect& rb, const F2* A, c
         if (bj < n - 1) { pts[bj] = pts[n - 1]; slot[bj] = slot[n - 1]; }
         --n;
     }
-    pts.resize(n);
+    *np = n;
     return kind;
 }
 
-void sort_pt_with_center(std::vector<F2>& pts) {
-    const int n = (int)pts.size();
+int rrect_intersection(const RRect& ra, const RRect& rb, std::vector<F2>& pts) {
+    F2 A[4], B[4], p[24];
+    rrect_corners(ra, A);
+    rrect_corners(rb, B);
+    int n = 0;
+    const int kind = rrect_isect(ra, rb, A, B, p, &n);
+    pts.assign(p, p + n);
+    return kind;
+}
+
+// sortPtWithCenter (TemplateMatcher.cpp:1093-1131) with its own keys: acos(x) * R2D above the centre, 360 - that
+// below, x = dot / |v|^2 (the squared norm is the reference's), 0 / 180 on the centre's row; std::sort by key.
+static void sort_pts_keyed(F2* pts, int n) {
     F2 ctr = f2(0.f, 0.f);
-    for (const F2& p : pts) { ctr.x += p.x; ctr.y += p.y; }
+    for (int i = 0; i < n; ++i) { ctr.x += pts[i].x; ctr.y += pts[i].y; }
     ctr.x = ctr.x / n;
     ctr.y = ctr.y / n;
-    std::pair<F2, double> keyed[24];   // n <= 24 (rrect_intersection)
+    std::pair<F2, double> keyed[24];   // n <= 24 (rrect_isect)
     for (int i = 0; i < n; ++i) {
         const F2 d = f2(pts[i].x - ctr.x, pts[i].y - ctr.y);
-        const float nn = d.x * d.x + d.y * d.y;   // (squared norm: reference behaviour)
+        const float nn = d.x * d.x + d.y * d.y;
         double key;
         if (d.y < 0) key = std::acos(d.x / nn) * kR2D;
         else if (d.y > 0) key = 360 - std::acos(d.x / nn) * kR2D;
@@ -178,17 +276,71 @@ void sort_pt_with_center(std::vector<F2>& pts) {
     for (int i = 0; i < n; ++i) pts[i] = keyed[i].first;
 }
 
-double contour_area(const std::vector<F2>& pts) {
-    const int n = (int)pts.size();
+// The same permutation without a transcendental per point.  For n <= 16 libstdc++'s std::sort is one insertion
+// sort (introsort stops at 16 elements), so the result depends only on the outcomes of `key_a < key_b`.  With every
+// off-row |x| <= 1/2 the keys fall in disjoint bands -- row-left 0 < above (60..120) < row-right 180 < below
+// (240..300) -- and within a band acos is strictly monotone with slope >= 1 in magnitude, so two x at least 2^-16
+// apart have keys ordered as their x (acosf's error is a few ulp of at most 2^-22); only closer pairs, which may
+// round to equal keys, compare acosf results exactly as the key does (both keys are monotone in the float acosf).
+// Anything outside that envelope takes the keyed path.
+static void sort_pts_center(F2* pts, int n) {
+    if (n > 16) { sort_pts_keyed(pts, n); return; }
+    F2 ctr = f2(0.f, 0.f);
+    for (int i = 0; i < n; ++i) { ctr.x += pts[i].x; ctr.y += pts[i].y; }
+    ctr.x = ctr.x / n;
+    ctr.y = ctr.y / n;
+    struct E { F2 p; float x; int band; };
+    E e[16];
+    for (int i = 0; i < n; ++i) {
+        const F2 d = f2(pts[i].x - ctr.x, pts[i].y - ctr.y);
+        e[i].p = pts[i];
+        e[i].x = 0.f;
+        if (d.y < 0 || d.y > 0) {
+            const float nn = d.x * d.x + d.y * d.y;
+            const float x = d.x / nn;
+            if (!(std::fabs(x) <= 0.5f)) { sort_pts_keyed(pts, n); return; }
+            e[i].x = x;
+            e[i].band = d.y < 0 ? 1 : 3;
+        } else {
+            e[i].band = (d.x - ctr.x > 0) ? 0 : 2;
+        }
+    }
+    auto less = [](const E& a, const E& b) {
+        if (a.band != b.band) return a.band < b.band;
+        if (a.band == 0 || a.band == 2) return false;
+        if (std::fabs(a.x - b.x) >= 0x1p-16f) return a.band == 1 ? a.x > b.x : a.x < b.x;
+        const float fa = std::acos(a.x), fb = std::acos(b.x);
+        return a.band == 1 ? fa < fb : fa > fb;
+    };
+    for (int i = 1; i < n; ++i) {   // libstdc++ __insertion_sort
+        const E v = e[i];
+        int j = i;
+        while (j > 0 && less(v, e[j - 1])) { e[j] = e[j - 1]; --j; }
+        e[j] = v;
+    }
+    for (int i = 0; i < n; ++i) pts[i] = e[i].p;
+}
+
+void sort_pt_with_center(std::vector<F2>& pts) {
+    if (!pts.empty()) sort_pts_center(pts.data(), (int)pts.size());
+}
+
+void sort_pt_with_center_keyed(std::vector<F2>& pts) {
+    if (!pts.empty()) sort_pts_keyed(pts.data(), (int)pts.size());
+}
+
+static double contour_area_a(const F2* pts, int n) {
     if (n == 0) return 0.;
     double acc = 0;
     F2 prev = pts[n - 1];
-    for (const F2& p : pts) {
-        acc += (double)prev.x * p.y - (double)prev.y * p.x;
-        prev = p;
+    for (int i = 0; i < n; ++i) {
+        acc += (double)prev.x * pts[i].y - (double)prev.y * pts[i].x;
+        prev = pts[i];
     }
     return std::fabs(acc * 0.5);
 }
+
+double contour_area(const std::vector<F2>& pts) { return contour_area_a(pts.data(), (int)pts.size()); }
 
 void filter_with_score(std::vector<HostMatch>& v, double score) {
     // std::sort's permutation depends only on the comparison results, so sorting light (score, index) keys with
@@ -208,30 +360,38 @@ void filter_with_score(std::vector<HostMatch>& v, double score) {
 void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
     if (v.empty()) return;
     const int n = (int)v.size();
-    std::vector<F2> pts;
     // corner bounding boxes: pairs whose boxes are > 1 px apart cannot have an edge crossing or a contained corner,
     // so rrect_intersection would return INTERSECT_NONE; skipping them keeps the reference's O(n^2) loop order
     // and deletions exactly while avoiding the exact test for far-apart detections
     std::vector<float> box((size_t)4 * n);
     std::vector<F2> corners((size_t)4 * n);
-    for (int i = 0; i < n; ++i) {
-        F2* c = &corners[(size_t)4 * i];
-        rrect_corners(v[i].rect, c);
-        float x0 = c[0].x, x1 = c[0].x, y0 = c[0].y, y1 = c[0].y;
-        for (int k = 1; k < 4; ++k) {
-            x0 = std::min(x0, c[k].x); x1 = std::max(x1, c[k].x);
-            y0 = std::min(y0, c[k].y); y1 = std::max(y1, c[k].y);
+    auto geom = [&](int i0, int i1) {
+        for (int i = i0; i < i1; ++i) {
+            F2* c = &corners[(size_t)4 * i];
+            rrect_corners(v[i].rect, c);
+            float x0 = c[0].x, x1 = c[0].x, y0 = c[0].y, y1 = c[0].y;
+            for (int k = 1; k < 4; ++k) {
+                x0 = std::min(x0, c[k].x); x1 = std::max(x1, c[k].x);
+                y0 = std::min(y0, c[k].y); y1 = std::max(y1, c[k].y);
+            }
+            box[4 * i] = x0 - 1.f; box[4 * i + 1] = y0 - 1.f; box[4 * i + 2] = x1 + 1.f; box[4 * i + 3] = y1 + 1.f;
         }
-        box[4 * i] = x0 - 1.f; box[4 * i + 1] = y0 - 1.f; box[4 * i + 2] = x1 + 1.f; box[4 * i + 3] = y1 + 1.f;
-    }
-    auto pair = [&](int i, int j, std::vector<F2>& pts) {   // the reference's inner-loop body for (i, j), boxes overlapping
-        const int kind = rrect_intersection_c(v[i].rect, v[j].rect, &corners[(size_t)4 * i], &corners[(size_t)4 * j], pts);
+    };
+    if (n <= 512) geom(0, n);
+    else host_parallel((n + 511) / 512, [&](int t) { geom(t * 512, std::min(n, t * 512 + 512)); });
+    auto pair = [&](int i, int j) {   // the reference's inner-loop body for (i, j), boxes overlapping
+        F2 pts[24];
+        int np = 0;
+        const int kind = rrect_isect(v[i].rect, v[j].rect, &corners[(size_t)4 * i], &corners[(size_t)4 * j], pts, &np);
+#ifdef FPM_HOST_STATS
+        g_stats[kind]++; g_stats[3 + np]++;
+#endif
         if (kind == 0) return;
         bool drop = kind == 2;
         if (kind == 1) {
-            if (pts.size() < 3) return;
-            sort_pt_with_center(pts);
-            const double ratio = contour_area(pts) / (v[i].rect.w * v[i].rect.h);
+            if (np < 3) return;
+            sort_pts_center(pts, np);
+            const double ratio = contour_area_a(pts, np) / (v[i].rect.w * v[i].rect.h);
             drop = ratio > max_overlap;
         }
         if (drop) v[(v[i].score >= v[j].score) ? j : i].del = true;
@@ -245,7 +405,7 @@ void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
         for (int i = 0; i + 1 < n; ++i) {
             if (v[i].del) continue;
             for (int j = i + 1; j < n; ++j)
-                if (!v[j].del && overlap(i, j)) pair(i, j, pts);
+                if (!v[j].del && overlap(i, j)) pair(i, j);
         }
     } else {
         // uniform grid over the boxes (cell = the largest box extent): for each i only the j > i whose boxes
@@ -304,7 +464,7 @@ void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
             std::vector<int> fill(comp_off.begin(), comp_off.end() - 1);
             for (int i = 0; i < n; ++i) members[fill[comp_of[i]]++] = i;   // ascending within a component
         }
-        auto run_comp = [&](int c, std::vector<F2>& p, std::vector<int>& nb) {
+        auto run_comp = [&](int c, std::vector<int>& nb) {
             for (int k = comp_off[c]; k < comp_off[c + 1]; ++k) {
                 const int i = members[k];
                 if (v[i].del) continue;
@@ -318,26 +478,18 @@ void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
                 std::sort(nb.begin(), nb.end());
                 nb.erase(std::unique(nb.begin(), nb.end()), nb.end());
                 for (int j : nb)
-                    if (!v[j].del && overlap(i, j)) pair(i, j, p);
+                    if (!v[j].del && overlap(i, j)) pair(i, j);
             }
         };
-        // threads only where there is enough exact-test work to pay for them (clusters of duplicate detections)
-        int nthreads = host_threads();
-        nthreads = std::min(nthreads, std::max(1, std::min(ncomp / 4, (n - ncomp) / 256)));
-        if (nthreads <= 1) {
+        // workers only where there is exact-test work to spread (clusters of duplicate detections)
+        if (ncomp < 8 || n - ncomp < 64) {
             std::vector<int> nb;
-            for (int c = 0; c < ncomp; ++c) run_comp(c, pts, nb);
+            for (int c = 0; c < ncomp; ++c) run_comp(c, nb);
         } else {
-            std::atomic<int> next{0};
-            auto worker = [&]() {
-                std::vector<F2> p;
-                std::vector<int> nb;
-                for (int c = next.fetch_add(1); c < ncomp; c = next.fetch_add(1)) run_comp(c, p, nb);
-            };
-            std::vector<std::thread> th;
-            for (int t = 1; t < nthreads; ++t) th.emplace_back(worker);
-            worker();
-            for (std::thread& t : th) t.join();
+            host_parallel(ncomp, [&](int c) {
+                thread_local std::vector<int> nb;
+                run_comp(c, nb);
+            });
         }
     }
     v.erase(std::remove_if(v.begin(), v.end(), [](const HostMatch& m) { return m.del; }), v.end());

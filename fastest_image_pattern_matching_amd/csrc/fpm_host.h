@@ -1,5 +1,6 @@
 // fpm_host.h — host-side stages of the search that are not data-parallel.
 #pragma once
+#include <functional>
 #include <vector>
 
 #include "fpm_geom.h"
@@ -25,11 +26,14 @@ struct HostMatch {
 RRect rrect_from3(F2 p1, F2 p2, F2 p3);                              // cv::RotatedRect(p1, p2, p3)
 int rrect_intersection(const RRect& a, const RRect& b, std::vector<F2>& pts);  // rotatedRectangleIntersection
 void sort_pt_with_center(std::vector<F2>& pts);                      // TemplateMatcher.cpp:1093-1131
+void sort_pt_with_center_keyed(std::vector<F2>& pts);                // the same with explicit acos keys (checks)
 double contour_area(const std::vector<F2>& pts);                     // cv::contourArea
 void filter_with_score(std::vector<HostMatch>& v, double score);     // TemplateMatcher.cpp:984-1000
 void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap);  // :1133-1194
 void subpix_estimation(const std::vector<HostMatch>& v, double* dx, double* dy, double* dangle,
                        double angle_step, int imax);                 // :1002-1072
 bool score_big2small(const HostMatch& a, const HostMatch& b);        // compareScoreBig2Small (:14-17)
+// runs fn(0 .. ntasks-1) on the host worker pool (FPM_HOST_THREADS, default min(hardware threads, 8)), caller included
+void host_parallel(int ntasks, const std::function<void(int)>& fn);
 
 }  // namespace fpm

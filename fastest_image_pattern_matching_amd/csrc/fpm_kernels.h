@@ -155,7 +155,10 @@ struct PackArgs {
 // the carried-window path); 0 = sized for the grid
 void launch_pyr_down(const uint8_t* src, int sw, int sh, int sp, size_t s_img, uint8_t* dst, int dw, int dh,
                      int dp, size_t d_img, int nimg, hipStream_t st, int seg_chunks = 0);
-void launch_warp(const WarpJob* jobs, int njobs, int max_pixels, hipStream_t st);
+// zero / nzero: counters the search zeroes before its later kernels use them (block (0, 0) clears them), so the
+// graph carries no memset nodes
+void launch_warp(const WarpJob* jobs, int njobs, int max_pixels, hipStream_t st, int32_t* zero = nullptr,
+                 int nzero = 0);
 void launch_ncc_map(const NccJob* jobs, int njobs, int max_out, int tmpl_bytes, hipStream_t st);
 bool ncc_tile_fits(int tw, int th);   // LDS-tiled variant applies (templates up to 128 x 64)
 void launch_ncc_tile(const NccJob* jobs, int njobs, int max_ow, int max_oh, int tw, int th, hipStream_t st);

@@ -374,7 +374,9 @@ void launch_pyr_down(const uint8_t* src, int sw, int sh, int sp, size_t s_img, u
 }
 
 // ============================================================================================== K2
-__global__ __launch_bounds__(256) void k_warp(const WarpJob* __restrict__ jobs) {
+__global__ __launch_bounds__(256) void k_warp(const WarpJob* __restrict__ jobs, int32_t* zero, int nzero) {
+    if (blockIdx.x == 0 && blockIdx.y == 0)
+        for (int i = threadIdx.x; i < nzero; i += 256) zero[i] = 0;
     const WarpJob& j = jobs[blockIdx.y];
     const int total = j.dw * j.dh;
     for (int idx = blockIdx.x * 256 + threadIdx.x; idx < total; idx += gridDim.x * 256) {
@@ -387,11 +389,11 @@ __global__ __launch_bounds__(256) void k_warp(const WarpJob* __restrict__ jobs) 
     }
 }
 
-void launch_warp(const WarpJob* jobs, int njobs, int max_pixels, hipStream_t st) {
-    if (njobs <= 0 || max_pixels <= 0) return;
-    int gx = (max_pixels + 255) / 256;
+void launch_warp(const WarpJob* jobs, int njobs, int max_pixels, hipStream_t st, int32_t* zero, int nzero) {
+    if (njobs <= 0 || (max_pixels <= 0 && nzero <= 0)) return;
+    int gx = max_pixels > 0 ? (max_pixels + 255) / 256 : 1;
     if (gx > 1024) gx = 1024;
-    hipLaunchKernelGGL(k_warp, dim3(gx, njobs), dim3(256), 0, st, jobs);
+    hipLaunchKernelGGL(k_warp, dim3(gx, njobs), dim3(256), 0, st, jobs, zero, nzero);
 }
 
 // ============================================================================================== K3+K4
@@ -2515,40 +2517,52 @@ __global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
             r.on_border = border;
             for (int x = -1; x <= 1; ++x)
                 for (int y = -1; y <= 1; ++y) r.vec[(x + 1) * 3 + (y + 1)] = border ? 0.f : sc[(my + y) * 7 + (mx + x)];
+            // (the candidate step follows in k_cand_step: fusing it here as a last-arriver hand-off between
+            // workgroups, sc1 stores + one agent-scope atomic per record, cost 30 us per layer at 32 sources: every
+            // workgroup then waits for its write-through stores; measured r02)
             a.rec[(size_t)id * a.n3 + jj] = r;
         }
         STAMP(7);
     }
 }
 
-// candidate step of :329-366 from the n3 records of each live candidate (after k_roi_small)
+// candidate step of :329-366 from the scores and 7x7 argmax positions of a candidate's n3 records: best of the
+// angles, early break below vecLayerScore, back-mapping of ptLT, append to the next live list
+__device__ void cand_step_one(const RoiArgs& a, int id, const float* score, const int* mx, const int* my) {
+    CandState s = a.state[id];
+    int imax = 0;
+    double big = -1;
+    for (int k = 0; k < a.n3; ++k)
+        if ((double)score[k] > big) { imax = k; big = score[k]; }
+    if ((double)score[imax] < a.thr) {   // :331-332
+        s.alive = 0;
+        a.state[id] = s;
+        return;
+    }
+    const int child = s.node * a.n3 + imax;
+    const AngleNode nd = a.nodes[child];
+    const F2 sc = f2((a.W - 1) / 2.0f, (a.H - 1) / 2.0f);
+    const F2 r0 = rotate_pt(f2(s.lt.x * 2, s.lt.y * 2), sc, nd.c, nd.s);   // :350-353
+    const F2 pad = f2(r0.x - 3, r0.y - 3);
+    F2 p = f2((float)((double)mx[imax] + pad.x), (float)((double)my[imax] + pad.y));
+    p = rotate_pt(p, sc, nd.cn, nd.sn);
+    s.lt = p;          // :366
+    s.node = child;    // :363
+    s.reached0 = a.mark_reached0;
+    a.state[id] = s;
+    a.live_out[atomicAdd(a.live_out_count, 1)] = id;
+}
+
+// the candidate step as its own launch over the live list (after k_roi_small's equal1 records)
 __global__ __launch_bounds__(256) void k_cand_step(RoiArgs a) {
     const int n = *a.live_count;
     for (int li = blockIdx.x * 256 + threadIdx.x; li < n; li += gridDim.x * 256) {
         const int id = a.live[li];
-        CandState s = a.state[id];
         const RoiRecord* r = a.rec + (size_t)id * a.n3;
-        int imax = 0;
-        double big = -1;
-        for (int k = 0; k < a.n3; ++k)
-            if ((double)r[k].score > big) { imax = k; big = r[k].score; }
-        if ((double)r[imax].score < a.thr) {   // :331-332
-            s.alive = 0;
-            a.state[id] = s;
-            continue;
-        }
-        const int child = s.node * a.n3 + imax;
-        const AngleNode nd = a.nodes[child];
-        const F2 sc = f2((a.W - 1) / 2.0f, (a.H - 1) / 2.0f);
-        const F2 r0 = rotate_pt(f2(s.lt.x * 2, s.lt.y * 2), sc, nd.c, nd.s);   // :350-353
-        const F2 pad = f2(r0.x - 3, r0.y - 3);
-        F2 p = f2((float)((double)r[imax].mx + pad.x), (float)((double)r[imax].my + pad.y));
-        p = rotate_pt(p, sc, nd.cn, nd.sn);
-        s.lt = p;          // :366
-        s.node = child;    // :363
-        s.reached0 = a.mark_reached0;
-        a.state[id] = s;
-        a.live_out[atomicAdd(a.live_out_count, 1)] = id;
+        float score[3];
+        int mx[3], my[3];
+        for (int k = 0; k < a.n3; ++k) { score[k] = r[k].score; mx[k] = r[k].mx; my[k] = r[k].my; }
+        cand_step_one(a, id, score, mx, my);
     }
 }
 

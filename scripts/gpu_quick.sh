@@ -19,5 +19,8 @@ print("total us/step", sum(v["ms_total"] for v in d["kernels"].values()) / st * 
 PY
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d $OUT/trace_$TAG -o run --output-format csv -- python3 $ROOT/bench.py --kernel-pass-only --steps 5 > /dev/null 2> $OUT/trace_$TAG.log || exit $?
 cd $ROOT && python3 scripts/step_timeline.py $(find $OUT/trace_$TAG -name '*kernel_trace.csv' | head -1)
-if [ -x build/merge_stages ]; then FPM_HOST_THREADS=1 ./build/merge_stages build/merge_src10_180.bin | tail -1; FPM_HOST_THREADS=8 ./build/merge_stages build/merge_src10_180.bin | tail -1; fi
+for t in 1 8; do FPM_HOST_THREADS=$t python3 scripts/merge_timing.py 300; done
+lscpu | grep -i "model name"
+timeout -k 10 300 python -u scripts/bench_configs.py 20 --no-cpu > $OUT/configs_$TAG.jsonl 2> $OUT/configs_$TAG.log || exit $?
+cut -c1-330 $OUT/configs_$TAG.jsonl
 exit 0

@@ -7,6 +7,9 @@
 #include <algorithm>
 #include "../fastest_image_pattern_matching_amd/csrc/fpm_host.h"
 #include "../include/fpm.h"
+#ifdef FPM_HOST_STATS
+namespace fpm { extern long g_stats[40]; }
+#endif
 using namespace fpm;
 static double now(){return std::chrono::duration<double,std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();}
 int main(int argc,char**argv){
@@ -28,4 +31,7 @@ int main(int argc,char**argv){
   double t5=now();
   printf("n=%d sort+collect %.3f score %.3f rects %.3f rotrect %.3f final %.3f -> %zu\n",n,t1-t0,t2-t1,t3-t2,t4-t3,t5-t4,all.size());
   }
+#ifdef FPM_HOST_STATS
+  for(int k=0;k<40;++k) if(fpm::g_stats[k]) printf("stat %d: %ld\n",k,fpm::g_stats[k]/20);
+#endif
 }
