@@ -120,6 +120,7 @@ struct RoiArgs {
     uint8_t* roi;            // [slot] sampled ROI, tile-major: 32 x 32 tiles of 1 KB, row of tiles by row
     int32_t roi_pitch;       // LDS row pitch of staged ROI rows (k_roi_corr)
     size_t roi_stride;
+    int32_t nparts;          // k_roi_fused: runs of bands per ROI (work unit = (ROI, run of bands))
     uint32_t* rowsum;        // [slot][th][49] exact int32 per-row dot products
     uint32_t* wsum;          // [slot][nchunk][49] window-sum partials of I
     uint64_t* wsq;           // [slot][nchunk][49] window-sum partials of I^2
@@ -171,6 +172,9 @@ void launch_roi_tables(const RoiArgs& a, hipStream_t st);
 void launch_roi_warp(const RoiArgs& a, hipStream_t st);
 void launch_roi_corr(const RoiArgs& a, hipStream_t st);
 void launch_roi_eval(const RoiArgs& a, hipStream_t st);
+bool roi_fused_fits(int tw);           // the fused sampling + correlation kernel applies (templates <= 1024 wide)
+int roi_fused_parts(int th);           // runs of bands per ROI (work units per ROI) of k_roi_fused
+void launch_roi_fused(const RoiArgs& a, hipStream_t st);
 bool roi_small_fits(int tw, int th);   // the single-kernel small-template refinement applies
 size_t roi_small_lds(int tw, int th);
 void launch_roi_small(const RoiArgs& a, hipStream_t st);

@@ -2178,6 +2178,260 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
+// ---- K6+K7 fused (templates too large for k_roi_small): the ROI never leaves the CU.  A work unit is one ROI and
+// one run of consecutive 32-row template bands; a workgroup walks its run band by band:
+//   the band's new ROI rows are sampled straight into an LDS ring of kBandSrc rows (32x32 tiles: the tile's
+//   source footprint staged in wave-private LDS, the bilinear taps gathered from it — K6b's sampler, with the
+//   warp tables computed in LDS instead of read from HBM), their exact row sums of I and I^2 reduced on the fly;
+//   the 6 rows a band shares with the next stay in the ring (ring slot = ROI row mod kBandSrc);
+//   then K7's banded GEMM on the matrix cores (A fragments of the band in registers, loaded during the sampling)
+//   and its epilogue: the exact per-row dot products and the per-16-row window-sum partials, exactly k_roi_corr's
+//   outputs, so K8 (k_roi_eval) folds them unchanged.
+// Only the first band of a run samples its 6 leading rows again (runs of ~3.5 bands: ~4.5 % extra sampling), the
+// ~0.4 MB sampled ROI of a layer-0 Src7 candidate is neither written to nor re-read from HBM, and the per-ROI warp
+// tables / tile descriptors need no kernel of their own.
+constexpr int kFuseFt = 3072;                  // per-wave footprint: any <= 32x32 interior tile box is <= 56 x 49 B
+constexpr int kFuseFtStride = kFuseFt + 64;    // + over-read slack
+constexpr int kFuseWgs = 256 * 3;              // 3 workgroups per CU (LDS ~52 KB, <= 168 VGPRs at layer 0)
+
+struct FuseLayout {
+    int sbp, ft, tab, rt, sums, mat, total;
+};
+__host__ __device__ inline FuseLayout fuse_layout(int tw) {
+    FuseLayout L;
+    const int txn = (tw + 6 + ROI_T - 1) / ROI_T;
+    L.sbp = roi_pitch_calc(tw);
+    L.ft = kBandSrc * L.sbp;                   // ring of kBandSrc ROI rows (i8: I ^ 0x80), pitch sbp
+    L.tab = L.ft + 4 * kFuseFtStride;          // ad[32 txn], bd[32 txn] (int32)
+    L.rt = L.tab + 8 * ROI_T * txn;            // x0[32], y0[32] of the row block being sampled
+    L.sums = L.rt + 8 * ROI_T;                 // rall, rallq [kBandSrc], wi, wq [kBandSrc][7] (ring slots)
+    L.mat = L.sums + 4 * 16 * kBandSrc;        // the ROI's affine map (6 doubles)
+    L.total = L.mat + 8 * 6;
+    return L;
+}
+bool roi_fused_fits(int tw) { return (tw + 63) / 64 <= 16 && 3 * (size_t)fuse_layout(tw).total <= 160 * 1024; }
+int roi_fused_parts(int th) {
+    const int nband = (th + kBandRows - 1) / kBandRows;
+    const int p = (2 * nband + 3) / 7;         // runs of ~3.5 bands
+    return p < 1 ? 1 : p;
+}
+
+// sum over each aligned group of 8 lanes, in every lane of the group: quad_perm [1,0,3,2], [2,3,0,1], then
+// row_half_mirror (lane i <-> 7 - i of the 8) — three DPP adds, no LDS traffic
+__device__ __forceinline__ uint32_t sum8_dpp(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);
+    return v;
+}
+
+template <int NK>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_roi_fused(RoiArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int tw = a.tw, th = a.th, RW = tw + 6, W = a.W, H = a.H;
+    const FuseLayout LY = fuse_layout(tw);
+    const int SBp = LY.sbp;
+    const int txn = (RW + ROI_T - 1) / ROI_T;
+    uint8_t* SB = smem;
+    int32_t* lad = (int32_t*)(smem + LY.tab);
+    int32_t* lbd = lad + ROI_T * txn;
+    int32_t* lx0 = (int32_t*)(smem + LY.rt);
+    int32_t* ly0 = lx0 + ROI_T;
+    uint32_t* rall = (uint32_t*)(smem + LY.sums);
+    uint32_t* rallq = rall + kBandSrc;
+    uint32_t* wi = rallq + kBandSrc;
+    uint32_t* wq = wi + kBandSrc * 7;
+    double* lM = (double*)(smem + LY.mat);
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    uint8_t* FT = smem + LY.ft + wv * kFuseFtStride;
+    const int nband = (th + kBandRows - 1) / kBandRows;
+    const int nparts = a.nparts;
+    const int units = roi_count(a) * nparts;
+    const int g = lane >> 4, n = lane & 15;
+    const int mt = wv & 1, nt = mt + (wv >> 1);   // this wave's (M, N) tile pair (k_roi_corr)
+    const int lr = lane >> 3, lg = lane & 7;      // sampling: rows lr + 8i, columns 4 lg .. 4 lg + 3 of a tile
+    const uint32_t kFix = 16384u * (uint32_t)tw;
+    auto ring = [](int r) { return r % kBandSrc; };
+    const XcdSplit xs = xcd_split(units);         // an XCD group takes a contiguous run of units (an ROI's runs
+                                                  // and the candidate's other angles share source lines in L2)
+    for (int u = xs.lo + xs.k; u < xs.hi; u += xs.nk) {
+        const int slot = u / nparts, part = u - slot * nparts;
+        const int b0 = part * nband / nparts, b1 = (part + 1) * nband / nparts;
+        int id, jj;
+        roi_slot(a, slot, id, jj);
+        const uint8_t* lvl = a.level + (size_t)(id / a.per_source) * a.level_stride;
+        __syncthreads();   // the previous unit is done with every LDS array
+        {
+            double M[6];
+            const CandState st = a.state[id];
+            const AngleNode nd = a.nodes[st.node * a.n3 + jj];
+            roi_matrix(W, H, f2(st.lt.x * 2, st.lt.y * 2), nd.c, nd.s, M);   // getRotatedROI :1074-1090
+            for (int x = tid; x < ROI_T * txn; x += 256) {   // warpAffine's adelta / bdelta (k_roi_tables)
+                lad[x] = rint_i(M[0] * x * kAbScale);
+                lbd[x] = rint_i(M[3] * x * kAbScale);
+            }
+            if (tid < 6) lM[tid] = M[tid];   // the row terms are computed per row block (below)
+        }
+        uint32_t* rs_out = a.rowsum + (((size_t)th * 49 + 3) & ~(size_t)3) * slot;
+        for (int b = b0; b < b1; ++b) {
+            const int T0 = b * kBandRows, rb = min(kBandRows, th - T0), nsrc = rb + 6;
+            const int rlo = b == b0 ? 0 : 6;       // ring rows T0 .. T0 + 5 carried from the previous band
+            // new rows T0 + rlo .. T0 + nsrc - 1, in row blocks of <= 32 (one tile row each)
+            for (int rb0 = rlo; rb0 < nsrc; rb0 += ROI_T) {
+                const int nr = min(ROI_T, nsrc - rb0), R0 = T0 + rb0;   // ROI rows R0 .. R0 + nr - 1
+                __syncthreads();   // the previous block's sampling is done with x0 / y0; (first block) the previous
+                                   // band's MFMA is done with the ring rows and window sums overwritten here
+                if (tid < nr) {
+                    const int y = R0 + tid;
+                    lx0[tid] = rint_i((lM[1] * y + lM[2]) * kAbScale) + kRoundDelta;
+                    ly0[tid] = rint_i((lM[4] * y + lM[5]) * kAbScale) + kRoundDelta;
+                    rall[ring(y)] = 0u;
+                    rallq[ring(y)] = 0u;
+                }
+                __syncthreads();
+                for (int tx = wv; tx < txn; tx += 4) {
+                    const int cx0 = tx * ROI_T, cx1 = min(cx0 + ROI_T, RW) - 1;
+                    // the tile's source footprint box from its corner samples (+-1 px, see k_roi_tables)
+                    int bx0 = INT_MAX, bx1 = INT_MIN, by0 = INT_MAX, by1 = INT_MIN;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int c = (k & 1) ? cx1 : cx0, r = (k & 2) ? nr - 1 : 0;
+                        const int X = (lx0[r] + lad[c]) >> (kAbBits - kInterBits);
+                        const int Y = (ly0[r] + lbd[c]) >> (kAbBits - kInterBits);
+                        bx0 = min(bx0, X >> kInterBits); bx1 = max(bx1, X >> kInterBits);
+                        by0 = min(by0, Y >> kInterBits); by1 = max(by1, Y >> kInterBits);
+                    }
+                    const bool interior = bx0 - 1 >= 0 && bx1 + 1 <= W - 2 && by0 - 1 >= 0 && by1 + 1 <= H - 2;
+                    bx0 = max(bx0 - 1, 0); by0 = max(by0 - 1, 0);
+                    bx1 = min(bx1 + 2, W - 1); by1 = min(by1 + 2, H - 1);
+                    const bool any = bx0 <= bx1 && by0 <= by1;
+                    const int bxa = bx0 & ~3;
+                    int ftw = any ? ((bx1 - bxa + 4) & ~3) : 0;
+                    if (((ftw >> 2) & 1) == 0) ftw += 4;    // odd dword pitch: spread gather banks
+                    const int fth = any ? by1 - by0 + 1 : 0;
+                    const int wpr = ftw >> 2;
+                    const bool in_lds = wpr <= 16 && ftw * fth <= kFuseFt;
+                    wave_sync();   // the previous tile's gathers are done with FT
+                    if (any && in_lds) stage_footprint<2>(FT, ftw, wpr, fth, lvl + (size_t)by0 * a.P + bxa, a.P, bxa, a.P, lane);
+                    wave_sync();
+                    const int c0 = cx0 + 4 * lg;
+                    int adv[4], bdv[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) { adv[q] = lad[c0 + q]; bdv[q] = lbd[c0 + q]; }
+                    const int nvalid = RW - c0;
+                    const uint32_t colmask = nvalid >= 4 ? 0xffffffffu : (nvalid <= 0 ? 0u : (1u << (8 * nvalid)) - 1u);
+                    const int xo = ((int)lds_offset_of(FT) - bxa) << kAbBits, yo = -(by0 << kAbBits);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int rr = lr + 8 * i;
+                        const int rc = rr < nr ? rr : nr - 1;   // rows past the block repeat its last row, unstored
+                        uint32_t pk = 0;
+                        if (interior && in_lds) {   // folded LDS addressing, the row's 16 tap reads before arithmetic
+                            const int x0r = lx0[rc] + xo, y0r = ly0[rc] + yo;
+                            uint32_t off[4];
+                            int fxv[4], fyv[4], v[4][4];
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                const int sxv = x0r + adv[q], syv = y0r + bdv[q];
+                                fxv[q] = __builtin_amdgcn_ubfe(sxv, kAbBits - kInterBits, kInterBits);
+                                fyv[q] = __builtin_amdgcn_ubfe(syv, kAbBits - kInterBits, kInterBits);
+                                off[q] = (uint32_t)mad24(syv >> kAbBits, ftw, sxv >> kAbBits);
+                            }
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) lds_taps(off[q], ftw, v[q]);
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) pk |= (uint32_t)bilerp24(v[q], fxv[q], fyv[q]) << (8 * q);
+                        } else {
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                const int X = (lx0[rc] + adv[q]) >> (kAbBits - kInterBits);
+                                const int Y = (ly0[rc] + bdv[q]) >> (kAbBits - kInterBits);
+                                const int v = !any ? 0 : in_lds ? ft_tap_general(FT, ftw, bxa, by0, W, H, X, Y)
+                                                                : roi_tap(lvl, W, H, a.P, X, Y);
+                                pk |= (uint32_t)v << (8 * q);
+                            }
+                        }
+                        pk &= colmask;
+                        // exact row sums of I and I^2 over the row's 32 tile columns (8 lanes), one LDS atomic each
+                        uint32_t s1 = __builtin_amdgcn_udot4(pk, 0x01010101u, 0u, false);
+                        uint32_t s2 = __builtin_amdgcn_udot4(pk, pk, 0u, false);
+                        s1 = sum8_dpp(s1);
+                        s2 = sum8_dpp(s2);
+                        if (rr < nr) {
+                            const int slotr = ring(R0 + rr);
+                            *(uint32_t*)(SB + (size_t)slotr * SBp + c0) = pk ^ 0x80808080u;
+                            if (lg == 0) {
+                                atomicAdd(&rall[slotr], s1);
+                                atomicAdd(&rallq[slotr], s2);
+                            }
+                        }
+                    }
+                }
+            }
+            __syncthreads();   // the band's rows and row sums are complete
+            // this band's A fragments (L2-resident slab; rows past the template are the slab's zero padding), in
+            // flight during the edge sums
+            fpm_v4i Areg[NK];
+            {
+                const int8_t* ap = a.tmpl8 + (size_t)(T0 + kMmaRows * mt + n) * a.tp8 + 16 * g;
+#pragma unroll
+                for (int k = 0; k < NK; ++k)
+                    Areg[k] = k < a.nk ? *(const fpm_v4i*)(ap + 64 * k) : fpm_v4i{0, 0, 0, 0};
+            }
+            for (int i = tid; i < (nsrc - rlo) * 7; i += 256) {   // window [dx, dx + tw): full row minus edges
+                const int r = ring(T0 + rlo + i / 7), dx = i % 7;
+                const uint8_t* sbr = SB + (size_t)r * SBp;
+                uint32_t q1 = rall[r], q2 = rallq[r];
+                for (int c = 0; c < dx; ++c) { const uint32_t v = sbr[c] ^ 0x80u; q1 -= v; q2 -= v * v; }
+                for (int c = dx + tw; c < RW; ++c) { const uint32_t v = sbr[c] ^ 0x80u; q1 -= v; q2 -= v * v; }
+                wi[r * 7 + dx] = q1;
+                wq[r * 7 + dx] = q2;
+            }
+            __syncthreads();
+            if (kMmaRows * mt < rb && kMmaRows * nt < nsrc) {   // wave-uniform
+                int sr = kMmaRows * nt + n;
+                if (sr >= nsrc) sr = 0;   // column outside the band: computed, never stored
+                const uint8_t* bp = SB + (size_t)ring(T0 + sr) * SBp + 16 * g;
+                fpm_v4i acc[7];
+                band_mfma_regs<NK>(Areg, bp, a.nk, acc);
+                // D_dx: col = lane & 15 -> source row 16*nt + n, row = 4*(lane >> 4) + r -> template row 16*mt + 4g + r
+                const int s_ = kMmaRows * nt + n;
+                const uint32_t* wr = wi + ring(T0 + (s_ < nsrc ? s_ : 0)) * 7;
+                // element (template row tb + r, dy = s_ - tb - r, dx = d) of the band's [t][49] block sits at
+                // ob[42 r + d]: one pointer per lane, immediate offsets
+                const int tb = kMmaRows * mt + 4 * g;
+                uint32_t* ob = rs_out + (size_t)(T0 + tb) * 49 + (s_ - tb) * 7;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int t = tb + r, dy = s_ - t;
+                    if (t < rb && s_ < nsrc && dy >= 0 && dy < 7) {
+                        const uint32_t ts = (uint32_t)a.tsum[T0 + t];
+#pragma unroll
+                        for (int d = 0; d < 7; ++d) ob[42 * r + d] = (uint32_t)acc[d][r] + 128u * (wr[d] + ts) - kFix;
+                    }
+                }
+            }
+            if (tid < 2 * 49) {   // per-16-row-chunk partials of the window sums (k_roi_corr)
+                const int h = tid / 49, k = tid - h * 49;
+                const int chunk = (T0 >> 4) + h;
+                const int tlo = kMmaRows * h, thi = min(tlo + kMmaRows, rb);
+                if (chunk < a.nchunk && tlo < thi) {
+                    const int pdy = k / 7, ddx = k - pdy * 7;
+                    uint32_t s1 = 0;
+                    uint64_t s2 = 0;
+                    for (int t = tlo; t < thi; ++t) {
+                        const int r = ring(T0 + t + pdy) * 7 + ddx;
+                        s1 += wi[r];
+                        s2 += wq[r];
+                    }
+                    a.wsum[((size_t)slot * a.nchunk + chunk) * 49 + k] = s1;
+                    a.wsq[((size_t)slot * a.nchunk + chunk) * 49 + k] = s2;
+                }
+            }
+        }
+    }
+}
+
 // ---- K6-K8 for small templates: one workgroup per ROI does the whole refinement of the ROI in LDS (tables,
 // 32x32-tile sampling from wave footprints, exact row / window sums, the band-by-band banded GEMM on the matrix
 // cores, the ordered f32 fold, CCOEFF, argmax, 3x3) and writes its RoiRecord; k_cand_step then steps the
@@ -2772,6 +3026,17 @@ void launch_roi_corr(const RoiArgs& a, hipStream_t st) {
     const long items = (long)a.slot_cap * ((a.th + kBandRows - 1) / kBandRows);
     const int grid = (int)(items < 16384 ? items : 16384);
     hipLaunchKernelGGL((k_roi_corr<0, kCorrGlobalA, kCorrWaves>), dim3(grid), dim3(256), lds, st, a);
+}
+
+void launch_roi_fused(const RoiArgs& a, hipStream_t st) {
+    if (a.slot_cap <= 0 || a.equal1) return;
+    const size_t lds = (size_t)fuse_layout(a.tw).total;
+    const long units = (long)a.slot_cap * a.nparts;
+    const int grid = (int)(units < kFuseWgs ? units : kFuseWgs);
+    if (a.nk <= 4) hipLaunchKernelGGL(k_roi_fused<4>, dim3(grid), dim3(256), lds, st, a);
+    else if (a.nk <= 8) hipLaunchKernelGGL(k_roi_fused<8>, dim3(grid), dim3(256), lds, st, a);
+    else if (a.nk <= 12) hipLaunchKernelGGL(k_roi_fused<12>, dim3(grid), dim3(256), lds, st, a);
+    else hipLaunchKernelGGL(k_roi_fused<16>, dim3(grid), dim3(256), lds, st, a);
 }
 
 void launch_roi_eval(const RoiArgs& a, hipStream_t st) {

@@ -129,6 +129,17 @@ def test_src7_full_search(hip, templates):
     assert len(gpu) == 3
 
 
+def test_src7_fused_refinement(gpu_matcher_factory, templates, monkeypatch):
+    """The opt-in fused K6+K7 kernel (FPM_ROI_FUSED=1, read when a fresh context records its search) on the full
+    Src7 search: every result field and per-layer live count equal the oracle's, as with the default split chain."""
+    monkeypatch.setenv("FPM_ROI_FUSED", "1")
+    m = gpu_matcher_factory()
+    s, t = synth.src7_scene(templates["Dst7"])
+    gpu, orc, ostats, gstats = _run_both(m, s, t, max_pos=3, tolerance_angle=180.0, score=0.7)
+    assert gstats == ostats
+    assert_same_results(gpu, orc, "src7 fused")
+
+
 def test_constant_template(hip):
     t = np.full((40, 40), 90, np.uint8)
     s = synth.noise(200, 150, 90, 20, 12)
