@@ -1,7 +1,9 @@
 """Timing of the BASELINE configs other than the headline one (bench.py measures configs[1], Src7, batched):
 per config the device-resident ms per search on one GPU (sources staged in HBM, median over repeated passes of
-the staged batch) next to one oracle search on the host (the CPU restatement, one thread), plus the result
-count of each.  Writes one JSON line per config.  usage: python scripts/bench_configs.py [reps] [--no-cpu] [--only=K ...]"""
+the staged batch; latency view: one context, pass after pass), the pipelined ms per search (two contexts as a
+stream of passes, host tail overlapped: throughput view) next to one oracle search on the host (the CPU
+restatement, one thread), plus the result count of each.  Writes one JSON line per config.
+usage: python scripts/bench_configs.py [reps] [--no-cpu] [--only=K ...] [--with-64]"""
 import json
 import os
 import sys
@@ -16,6 +18,8 @@ from tests import oracle  # noqa: E402  (timed CPU baseline only)
 REPS = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 10
 CPU = "--no-cpu" not in sys.argv
 ONLY = [int(a.split("=")[1]) for a in sys.argv if a.startswith("--only=")]   # config positions to run
+ALL64 = "--with-64" in sys.argv
+PIPE = "--no-pipe" not in sys.argv   # --no-pipe: latency view only (one context: clean kernel traces)   # also the whole 64-source configs[3] at 1 deg on one GPU (~1 GB of sources)
 
 
 def configs():
@@ -28,12 +32,45 @@ def configs():
     srcs, t = synth.batch_sources(8)
     yield ("configs[3] 8 x 4096x4096 / 512x512 crop, +-180 deg (reference step), TargetNum 1", srcs, t,
            dict(max_pos=1, tolerance_angle=180.0))
+    # BASELINE configs[3] as stated: +-180 at a 1 deg top-layer step (fpm_params.top_angle_step, a flagged extension;
+    # the reference derives 7.125 deg, TemplateMatcher.cpp:130): 8 sources = one GPU's share of the 64-source,
+    # 8-GPU config; then all 64 on one GPU
+    yield ("configs[3] 8 x 4096x4096 / 512x512 crop, +-180 deg at 1 deg top step (361 angles), TargetNum 1", srcs, t,
+           dict(max_pos=1, tolerance_angle=180.0, top_angle_step=1.0))
+    if ALL64:
+        srcs64, t = synth.batch_sources(64)
+        yield ("configs[3] 64 x 4096x4096 / 512x512 crop, +-180 deg at 1 deg top step, TargetNum 1, one GPU", srcs64,
+               t, dict(max_pos=1, tolerance_angle=180.0, top_angle_step=1.0))
+        del srcs64
     srcs5, t5 = synth.src5_set(T["Dst5"])
     yield ("configs[4] Src5 rotation set 8 x 640x480 / Dst5 160x159, +-180 deg, sub-pixel", srcs5, t5,
            dict(max_pos=1, tolerance_angle=180.0, subpixel=1))
     s7, t7 = synth.src7_scene(T["Dst7"])
     yield ("configs[1] single Src7 source (latency view of the headline config)", [s7], t7,
            dict(max_pos=3, tolerance_angle=180.0, score=0.7, min_reduce_area=256, max_overlap=0.0, use_simd=1))
+
+
+def pipelined(m, srcs, t, prm):
+    """Throughput view: a second context (HIP stream) holding the same batch; the two run as a stream of passes
+    (bench.py's scheme), so one context's host tail overlaps the other's device work."""
+    m2 = TemplateMatcher(0)
+    for k, v in prm.items():
+        setattr(m2._params, k, v)
+    assert m2.learnPattern(t)
+    m2.stage(srcs)
+    m2.match_staged_array()
+    ctxs = [m, m2]
+    for c in ctxs:
+        c.match_staged_launch()
+    t0 = time.perf_counter()
+    for k in range(REPS):
+        for c in ctxs:
+            c.match_staged_finish_array()
+            if k + 1 < REPS:
+                c.match_staged_launch()
+    pipe_ms = (time.perf_counter() - t0) * 1e3 / (REPS * len(ctxs))
+    return {"pipelined_ms_per_search": round(pipe_ms / len(srcs), 3),
+            "pipelined_searches_per_s": round(1e3 * len(srcs) / pipe_ms, 1)}
 
 
 def main():
@@ -46,6 +83,7 @@ def main():
         assert m.learnPattern(t)
         m.stage(srcs)
         cnt, _ = m.match_staged_array()          # warm: plan + graph
+        cnt = cnt.copy()
         ts = []
         for _ in range(REPS):
             t0 = time.perf_counter()
@@ -57,6 +95,8 @@ def main():
                "last_pass_device_ms": round(dev_ms, 3), "last_pass_host_ms": round(host_ms, 3),
                "gpu_ms_per_search": round(ms / len(srcs), 3), "gpu_searches_per_s": round(1e3 * len(srcs) / ms, 1),
                "matches": [int(x) for x in cnt]}
+        if PIPE:
+            out.update(pipelined(m, srcs, t, prm))
         if CPU:
             o = oracle.OracleMatcher().set(**prm)
             o.learnPattern(t)
