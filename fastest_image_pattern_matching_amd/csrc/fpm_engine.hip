@@ -448,19 +448,34 @@ int build_plan(fpm_ctx* ctx) {
         const size_t per_roi = sizeof(int32_t) * 2 * (P.tabw + P.tabh) + sizeof(int4) * P.tdesc_stride + P.roi_stride + max_rows * 49 * 4 +
                                max_chunks * 49 * 12;
         // slots are sized for the worst case (every top candidate alive at every layer) so the captured graph needs
-        // no host round trip; up to a sixth of the free HBM (<= 48 GB of 288) holds them, rounds only beyond that
+        // no host round trip; up to a sixth of the free HBM (<= 48 GB of 288; FPM_SCRATCH_MB caps it) holds them,
+        // rounds only beyond that.  A floor of min(4 GB, half the free HBM) keeps a batch in few rounds when another
+        // allocator in the process holds most of the device; an allocation failure halves the slots (more rounds)
+        // instead of failing the search.
         size_t free_b = 0, total_b = 0;
-        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = (size_t)96 << 30;
-        const size_t budget = std::min((size_t)48 << 30, std::max((size_t)4 << 30, free_b / 6));
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = (size_t)16 << 30;
+        size_t budget = std::min((size_t)48 << 30, std::max(std::min((size_t)4 << 30, free_b / 2), free_b / 6));
+        if (const char* e = getenv("FPM_SCRATCH_MB")) {
+            const long mb = atol(e);
+            if (mb > 0) budget = std::min(budget, (size_t)mb << 20);
+        }
         const size_t want = (size_t)P.C * P.n3;
         // rounds hold whole candidates (k_roi_eval steps a candidate from its n3 records)
         P.slot_cap = (int)std::max<size_t>((size_t)P.n3, std::min(want, budget / per_roi) / P.n3 * P.n3);
-        HIP_TRY(P.d_tab.ensure((size_t)P.slot_cap * 2 * (P.tabw + P.tabh) * sizeof(int32_t)));
-        HIP_TRY(P.d_tdesc.ensure((size_t)P.slot_cap * P.tdesc_stride * sizeof(int4)));
-        HIP_TRY(P.d_roi.ensure((size_t)P.slot_cap * P.roi_stride));
-        HIP_TRY(P.d_rowsum.ensure((size_t)P.slot_cap * round_up(max_rows * 49, (size_t)4) * 4));
-        HIP_TRY(P.d_wsum.ensure((size_t)P.slot_cap * max_chunks * 49 * 4));
-        HIP_TRY(P.d_wsq.ensure((size_t)P.slot_cap * max_chunks * 49 * 8));
+        for (;;) {
+            hipError_t e = P.d_tab.ensure((size_t)P.slot_cap * 2 * (P.tabw + P.tabh) * sizeof(int32_t));
+            if (e == hipSuccess) e = P.d_tdesc.ensure((size_t)P.slot_cap * P.tdesc_stride * sizeof(int4));
+            if (e == hipSuccess) e = P.d_roi.ensure((size_t)P.slot_cap * P.roi_stride);
+            if (e == hipSuccess) e = P.d_rowsum.ensure((size_t)P.slot_cap * round_up(max_rows * 49, (size_t)4) * 4);
+            if (e == hipSuccess) e = P.d_wsum.ensure((size_t)P.slot_cap * max_chunks * 49 * 4);
+            if (e == hipSuccess) e = P.d_wsq.ensure((size_t)P.slot_cap * max_chunks * 49 * 8);
+            if (e == hipSuccess) break;
+            (void)hipGetLastError();   // clear the sticky allocation error
+            if (e != hipErrorOutOfMemory || P.slot_cap <= P.n3) HIP_TRY(e);
+            P.d_tab.release(); P.d_tdesc.release(); P.d_roi.release();
+            P.d_rowsum.release(); P.d_wsum.release(); P.d_wsq.release();
+            P.slot_cap = std::max(P.n3, P.slot_cap / 2 / P.n3 * P.n3);
+        }
     }
     // job tables
     std::vector<WarpJob> wj(J);

@@ -140,6 +140,23 @@ def test_src7_fused_refinement(gpu_matcher_factory, templates, monkeypatch):
     assert_same_results(gpu, orc, "src7 fused")
 
 
+@pytest.mark.parametrize("scratch_mb", [8, 64])
+def test_refinement_rounds(gpu_matcher_factory, templates, monkeypatch, scratch_mb):
+    """A capped refinement scratch (FPM_SCRATCH_MB, read when a fresh context plans its search) splits every layer's
+    ROIs into rounds of whole candidates (about 5 candidates per round at 8 MB); the batched Src7 search is
+    unchanged (scratch bounded by the free HBM, more rounds instead of a failed allocation)."""
+    monkeypatch.setenv("FPM_SCRATCH_MB", str(scratch_mb))
+    t = templates["Dst7"]
+    srcs = [synth.src7_scene(t, seed=7 + i)[0] for i in range(2)]
+    m = gpu_matcher_factory(max_pos=3, tolerance_angle=180.0, score=0.7)
+    assert m.learnPattern(t)
+    m.stage(srcs)
+    got = [[r.as_tuple() for r in rr] for rr in m.match_staged()]
+    o = oracle.OracleMatcher().set(max_pos=3, tolerance_angle=180.0, score=0.7)
+    o.learnPattern(t)
+    assert got == [o.match(s) for s in srcs]
+
+
 def test_constant_template(hip):
     t = np.full((40, 40), 90, np.uint8)
     s = synth.noise(200, 150, 90, 20, 12)
