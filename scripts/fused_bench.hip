@@ -82,6 +82,7 @@ int main(int argc, char** argv) {
     a.tdesc_stride = roi_tiles_for(TW, TH);
     CK(hipMalloc(&a.tdesc, (size_t)C * n3 * a.tdesc_stride * sizeof(int4)));
     CK(hipMalloc(&a.roi, (size_t)C * n3 * a.roi_stride));
+    CK(hipMemset(a.roi, 0x5a, (size_t)C * n3 * a.roi_stride));   // stale scratch: bytes k_roi_warp never writes
     a.nparts = roi_fused_parts(TH);
     auto timeit = [&](auto fn, const char* name) {
         hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
