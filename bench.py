@@ -5,12 +5,13 @@ A step is one full TemplateMatcher::match pass (pyramid -> top-layer rotation sw
 refinement -> host filters) over a batch of ``--batch`` synthetic Src7 sources per GPU that are already
 resident in HBM (staged before timing; the PCIe upload is not in ``value``), split over ``--contexts`` contexts
 (one HIP stream each) that run as a stream of passes: a context relaunches as soon as its previous pass is
-finished, so host post-processing overlaps device work.  ``value`` = searches/s over all
+finished, so host post-processing overlaps device work.  Defaults: 128 sources over 3 contexts (the throughput
+plateau of scripts/sweep_batch.sh: 21.5k searches/s at 32 / 2, 24.3k at 128 / 3, 24.5k at 192 / 3).  ``value`` = searches/s over all
 ranks.  Multi-GPU: one process per GPU (torchrun), every rank searches its own sources (weak scaling, no
 data-path collective); barrier + synchronize bracket the K timed steps and the max time over ranks is used.
 
 Also reported: the dominant kernel's roofline (HIP events around every launch on the library's stream, in a
-second pass of K steps so the timed pass carries no event overhead) and the CPU baseline (the oracle
+second pass of K steps over one context's share of the sources, so the timed pass carries no event overhead) and the CPU baseline (the oracle
 restatement, single thread, on a bounded sample of the same workload, rank 0 at N=1 only).
 
 Roofline bytes are SURVEY.md §8(d)'s algorithmic bytes, reported by the library per search (fpm_search_bytes) and per
@@ -139,9 +140,10 @@ def cpu_baseline(templ, src, budget_s):
 
 
 def kernel_pass(m, sources, steps, L):
-    """Kernel-level pass: one context over the whole batch, eager launches with HIP events around each kernel on the
-    library's stream (the kernels' own durations, not time shared with another context's stream).  Returns the
-    per-kernel table and the roofline object of the dominant kernel."""
+    """Kernel-level pass: one context over its share of the step's sources (the same launches as one context's pass
+    in the timed run), eager launches with HIP events around each kernel on the library's stream (the kernels' own
+    durations, not time shared with another context's stream).  Returns the per-kernel table and the roofline
+    object of the dominant kernel."""
     m.stage(sources)
     m.match_staged_array()
     m.profile(True)
@@ -202,9 +204,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=32, help="Src7 sources searched per GPU per step")
+    ap.add_argument("--batch", type=int, default=128, help="Src7 sources searched per GPU per step")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (0 = skip)")
-    ap.add_argument("--contexts", type=int, default=2, help="concurrent contexts (HIP streams) per GPU")
+    ap.add_argument("--contexts", type=int, default=3, help="concurrent contexts (HIP streams) per GPU")
     ap.add_argument("--skip-latency", action="store_true",
                     help="skip the single-search latency probe (PMC runs: only batch dispatches)")
     ap.add_argument("--dry-run", action="store_true",
@@ -251,12 +253,16 @@ def main():
     for k, v in PARAMS.items():
         setattr(m._params, k, v)
     assert m.learnPattern(templ)
-    # single-search latency (host upload included) for the record, after one warm call builds the plan
+    # G contexts (one HIP stream each) on this GPU, each holding batch / G of the sources (see run() below)
+    G = max(1, min(args.contexts, args.batch))
+    chunks = [sources[i * args.batch // G:(i + 1) * args.batch // G] for i in range(G)]
+    # the kernel pass is one context's share of the step (chunks[0]), eager: the launches of the timed run's passes
     if args.kernel_pass_only:
-        kern, roofline = kernel_pass(m, sources, args.steps, L)
-        print(json.dumps({"kernel_pass_only": True, "steps": args.steps, "sources_per_step": args.batch,
+        kern, roofline = kernel_pass(m, chunks[0], args.steps, L)
+        print(json.dumps({"kernel_pass_only": True, "steps": args.steps, "sources_per_step": len(chunks[0]),
                           "kernels": kern, "roofline": roofline}), flush=True)
         return
+    # single-search latency (host upload included) for the record, after one warm call builds the plan
     lat_e2e = None
     if not args.skip_latency:
         m.match(sources[0])
@@ -266,11 +272,8 @@ def main():
             m.match(sources[0])
             lat.append(time.perf_counter() - t0)
         lat_e2e = float(np.median(lat))
-    # G contexts (one HIP stream each) on this GPU, each holding batch / G of the sources: a step launches every
-    # context's device pass, then finishes them in order, so host post-processing and the upper pyramid layers'
-    # latency-bound kernels of one context overlap device work of the others
-    G = max(1, min(args.contexts, args.batch))
-    chunks = [sources[i * args.batch // G:(i + 1) * args.batch // G] for i in range(G)]
+    # a step launches every context's device pass, then finishes them in order, so host post-processing and the upper
+    # pyramid layers' latency-bound kernels of one context overlap device work of the others
     ctxs = [m] + [TemplateMatcher(local) for _ in range(G - 1)]
     for c, ch in zip(ctxs, chunks):
         for k, v in PARAMS.items():
@@ -335,7 +338,7 @@ def main():
                        "definition": "SURVEY.md §8(d) B_pyr + B_top + B_ref of every search in the timed region "
                                      "(fpm_search_bytes, live counts of this workload) / the timed wall time"}
 
-    kern, roofline = kernel_pass(m, sources, args.steps, L)
+    kern, roofline = kernel_pass(m, chunks[0], args.steps, L)
 
     searches = world * args.batch * args.steps
     value = searches / elapsed
