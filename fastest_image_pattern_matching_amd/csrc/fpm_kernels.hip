@@ -252,6 +252,7 @@ __global__ __launch_bounds__(256) void k_pyr_down(const uint8_t* __restrict__ sr
 // tile (the one-tile form above reaches 3.2-4.2 TB/s: its workgroups wait for their single burst).  Same integer
 // arithmetic as k_pyr_down, exact.
 constexpr int PS_NL = (PD_IH * (PD_IW / 16) + 255) / 256;   // 16-byte loads per thread for a 68-row window: 5
+typedef unsigned short fpm_u16x2 __attribute__((ext_vector_type(2)));
 
 __global__ __launch_bounds__(256) void k_pyr_down_s(const uint8_t* __restrict__ src, int sw, int sh, int sp,
                                                     size_t s_img, uint8_t* __restrict__ dst, int dw, int dh,
@@ -317,42 +318,47 @@ __global__ __launch_bounds__(256) void k_pyr_down_s(const uint8_t* __restrict__ 
         __syncthreads();
         // the next chunk's 64 new input rows (its window rows 4..67) are in flight while this chunk is filtered
         if (oyc + PD_OH < oy_end) issue(2 * oyc + 2 * PD_OH + 2, 2 * PD_OH);
-        // horizontal [1 4 6 4 1] of the new window rows: 4 consecutive outputs per item (as k_pyr_down)
+        // horizontal [1 4 6 4 1] of the new window rows: 4 consecutive outputs per item (as k_pyr_down; the 5th tap
+        // enters the v_dot4 as its accumulator)
         const int nh = nrows * (PD_OW / 4);
         for (int i = tid; i < nh; i += 256) {
             const int r = roff + i / (PD_OW / 4), g = i % (PD_OW / 4);
             const uint32_t* w = (const uint32_t*)&tin[r][8 * g + 12];
             const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
-            const uint32_t h0 = __builtin_amdgcn_udot4(PD_K, __builtin_amdgcn_alignbyte(w1, w0, 2), 0, false) + ((w1 >> 16) & 0xff);
-            const uint32_t h1 = __builtin_amdgcn_udot4(PD_K, w1, 0, false) + (w2 & 0xff);
-            const uint32_t h2 = __builtin_amdgcn_udot4(PD_K, __builtin_amdgcn_alignbyte(w2, w1, 2), 0, false) + ((w2 >> 16) & 0xff);
-            const uint32_t h3 = __builtin_amdgcn_udot4(PD_K, w2, 0, false) + (w3 & 0xff);
+            const uint32_t h0 = __builtin_amdgcn_udot4(PD_K, __builtin_amdgcn_alignbyte(w1, w0, 2), (w1 >> 16) & 0xff, false);
+            const uint32_t h1 = __builtin_amdgcn_udot4(PD_K, w1, w2 & 0xff, false);
+            const uint32_t h2 = __builtin_amdgcn_udot4(PD_K, __builtin_amdgcn_alignbyte(w2, w1, 2), (w2 >> 16) & 0xff, false);
+            const uint32_t h3 = __builtin_amdgcn_udot4(PD_K, w2, w3 & 0xff, false);
             uint2 o;
             o.x = h0 | (h1 << 16);
             o.y = h2 | (h3 << 16);
             *(uint2*)&hs[r][4 * g] = o;
         }
         __syncthreads();
-        // vertical: 4 consecutive outputs of one row per item
+        // vertical: 4 consecutive outputs of one row per item, two per register in packed u16 arithmetic — exact:
+        // a horizontal sum is <= 16 * 255, so 128 + sum_t k_t * h_t <= 65408 fits 16 bits, and (v >> 8) is the
+        // half's high byte, gathered by one v_perm
 #pragma unroll
         for (int k = 0; k < PD_OH * (PD_OW / 4) / 256; ++k) {
             const int i = tid + 256 * k;
             const int orow = i / (PD_OW / 4), g = i - orow * (PD_OW / 4);
             const int oy = oyc + orow, ox = ox0 + 4 * g;
             if (oy >= oy_end || ox >= dw) continue;
-            uint32_t acc[4] = {128, 128, 128, 128};
-            const int kw[5] = {1, 4, 6, 4, 1};
+            fpm_u16x2 a01 = {128, 128}, a23 = {128, 128};
+            constexpr unsigned short kw[5] = {1, 4, 6, 4, 1};
 #pragma unroll
             for (int tt = 0; tt < 5; ++tt) {
                 const uint2 q = *(const uint2*)&hs[2 * orow + tt][4 * g];
-                acc[0] += kw[tt] * (q.x & 0xffff); acc[1] += kw[tt] * (q.x >> 16);
-                acc[2] += kw[tt] * (q.y & 0xffff); acc[3] += kw[tt] * (q.y >> 16);
+                a01 += __builtin_bit_cast(fpm_u16x2, q.x) * kw[tt];
+                a23 += __builtin_bit_cast(fpm_u16x2, q.y) * kw[tt];
             }
+            const uint32_t packed = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, a23),
+                                                          __builtin_bit_cast(uint32_t, a01), 0x07050301u);
             uint8_t* d = dst + (size_t)oy * dp + ox;
             if (ox + 4 <= dw) {
-                *(uint32_t*)d = (acc[0] >> 8) | ((acc[1] >> 8) << 8) | ((acc[2] >> 8) << 16) | ((acc[3] >> 8) << 24);
+                *(uint32_t*)d = packed;
             } else {
-                for (int j = 0; j < dw - ox; ++j) d[j] = (uint8_t)(acc[j] >> 8);
+                for (int j = 0; j < dw - ox; ++j) d[j] = (uint8_t)(packed >> (8 * j));
             }
         }
         __syncthreads();
@@ -2463,7 +2469,7 @@ size_t roi_small_lds(int tw, int th) { return (size_t)small_layout(tw, th).total
 // 2 = + row / window sums, 3 = + bands without the fold, 5 = full with byte-gather taps, 9 = full with per-phase
 // s_memtime stamps (a.stamps)
 template <int MODE>
-__global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_roi_small(RoiArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tw = a.tw, th = a.th, RW = tw + 6, RH = th + 6, W = a.W, H = a.H;
     const SmallLayout LY = small_layout(tw, th);
@@ -2683,31 +2689,42 @@ __global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
         }
         __syncthreads();
         STAMP(3);
-        for (int i = tid; i < RH * 7; i += 256) {   // window [dx, dx + tw) of every row
-            const int r = i / 7, dx = i - r * 7;
-            const uint8_t* sbr = SB + (size_t)r * SBp;
+        for (int r = tid; r < RH; r += 256) {   // windows [dx, dx + tw) of a row: full row minus <= 6 edge pixels,
+            const uint8_t* sbr = SB + (size_t)r * SBp;   // the row's 12 edge bytes read once by one thread
+            uint32_t lv[6], rv[6];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) { lv[c] = sbr[c] ^ 0x80u; rv[c] = sbr[tw + c] ^ 0x80u; }
             uint32_t q1 = rall[r], q2 = rallq[r];
-            for (int c = 0; c < dx; ++c) { const uint32_t v = sbr[c] ^ 0x80u; q1 -= v; q2 -= v * v; }
-            for (int c = dx + tw; c < RW; ++c) { const uint32_t v = sbr[c] ^ 0x80u; q1 -= v; q2 -= v * v; }
-            wi[i] = q1;
-            wq[i] = q2;
+#pragma unroll
+            for (int c = 0; c < 6; ++c) { q1 -= rv[c]; q2 -= rv[c] * rv[c]; }   // dx = 0: columns tw .. tw + 5
+#pragma unroll
+            for (int dx = 0; dx < 7; ++dx) {
+                if (dx > 0) {   // column dx - 1 leaves on the left, column tw + dx - 1 enters on the right
+                    q1 += rv[dx - 1] - lv[dx - 1];
+                    q2 += rv[dx - 1] * rv[dx - 1] - lv[dx - 1] * lv[dx - 1];
+                }
+                wi[r * 7 + dx] = q1;
+                wq[r * 7 + dx] = q2;
+            }
         }
+        if (tid < 98) tot[tid] = 0;
         __syncthreads();
         STAMP(4);
-        if (tid < 49) {   // window totals of the 49 positions (exact)
-            const int pdy = tid / 7, ddx = tid - pdy * 7;
+        if (tid < 4 * 49) {   // window totals of the 49 positions (exact): 4 threads per position, u64 LDS adds
+            const int part = tid / 49, k = tid - part * 49, pdy = k / 7, ddx = k - pdy * 7;
+            const int t0 = part * th / 4, t1 = (part + 1) * th / 4;
             uint64_t s1 = 0, s2 = 0;
-            int t = 0;
-            for (; t + 8 <= th; t += 8) {   // 8 LDS reads of each in flight
+            int t = t0;
+            for (; t + 8 <= t1; t += 8) {   // 8 LDS reads of each in flight
                 uint32_t x[8], y[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) { x[u] = wi[(t + u + pdy) * 7 + ddx]; y[u] = wq[(t + u + pdy) * 7 + ddx]; }
 #pragma unroll
                 for (int u = 0; u < 8; ++u) { s1 += x[u]; s2 += y[u]; }
             }
-            for (; t < th; ++t) { s1 += wi[(t + pdy) * 7 + ddx]; s2 += wq[(t + pdy) * 7 + ddx]; }
-            tot[tid] = s1;
-            tot[49 + tid] = s2;
+            for (; t < t1; ++t) { s1 += wi[(t + pdy) * 7 + ddx]; s2 += wq[(t + pdy) * 7 + ddx]; }
+            atomicAdd((unsigned long long*)&tot[k], (unsigned long long)s1);
+            atomicAdd((unsigned long long*)&tot[49 + k], (unsigned long long)s2);
         }
         if (MODE == 2) continue;
         STAMP(5);
@@ -2757,11 +2774,14 @@ __global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
         }
         __syncthreads();
         STAMP(6);
-        if (tid == 0) {   // cv::minMaxLoc: first maximum in row-major order
-            float best = sc[0];
-            int bi = 0;
-            for (int k = 1; k < 49; ++k)
-                if (sc[k] > best) { best = sc[k]; bi = k; }
+        if (wv == 0) {   // cv::minMaxLoc: first maximum in row-major order, as a wave reduction
+            float v = lane < 49 ? sc[lane] : -INFINITY;
+            int bi = lane < 49 ? lane : 64;
+            if (v != v) { v = -INFINITY; bi = 64 + lane; }   // a NaN never beats the running maximum
+            wave_better_reduce(v, bi);                        // largest value, lowest index among equals
+            const float s0 = sc[0];
+            if (s0 != s0 || bi >= 64) bi = 0;                 // the scan starts at sc[0]: a NaN there stays
+            const float best = sc[bi];
             const int mx = bi % 7, my = bi / 7;
             RoiRecord r;
             r.score = best;
@@ -2772,9 +2792,9 @@ __global__ __launch_bounds__(256) void k_roi_small(RoiArgs a) {
             for (int x = -1; x <= 1; ++x)
                 for (int y = -1; y <= 1; ++y) r.vec[(x + 1) * 3 + (y + 1)] = border ? 0.f : sc[(my + y) * 7 + (mx + x)];
             // (the candidate step follows in k_cand_step: fusing it here as a last-arriver hand-off between
-            // workgroups, sc1 stores + one agent-scope atomic per record, cost 30 us per layer at 32 sources: every
-            // workgroup then waits for its write-through stores; measured r02)
-            a.rec[(size_t)id * a.n3 + jj] = r;
+            // workgroups, system-coherent stores + one agent-scope atomic per record, cost 30 us per layer at 32
+            // sources: every workgroup then waits for its write-through stores; measured r02)
+            if (lane == 0) a.rec[(size_t)id * a.n3 + jj] = r;
         }
         STAMP(7);
     }
