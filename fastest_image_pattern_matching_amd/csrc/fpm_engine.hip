@@ -98,7 +98,8 @@ struct Plan {
     std::vector<size_t> canvas_off, map_off, blk_off;
     std::vector<int> canvas_pitch, map_w, map_h, nblk;
     size_t canvas_bytes = 0, map_floats = 0, blk_count = 0;
-    int max_canvas = 0, max_map = 0, max_nblk = 0, max_cells = 0;
+    int max_canvas = 0, max_map = 0, max_nblk = 0, max_cells = 0, max_nitems = 0;
+    int off_skey = 0, nzero = 0;   // d_livecnt layout: strip keys' offset, words zeroed by k_warp
     // device buffers owned by the plan
     DevBuf d_ncand;                            // s_BlockMax candidate lists (k_nms_blocks -> k_nms_fast)
     DevBuf d_canvas, d_map, d_bmax, d_bloc, d_jobs, d_nodes, d_top, d_topn, d_peaks, d_counts, d_state,
@@ -344,7 +345,7 @@ int build_plan(fpm_ctx* ctx) {
     P.canvas_pitch.resize(P.nang); P.map_w.resize(P.nang); P.map_h.resize(P.nang); P.nblk.resize(P.nang);
     std::vector<std::array<double, 6>> mats(P.nang);
     size_t co = 0, mo = 0, bo = 0;
-    P.max_canvas = 0; P.max_map = 0; P.max_nblk = 0; P.max_cells = 0;
+    P.max_canvas = 0; P.max_map = 0; P.max_nblk = 0; P.max_cells = 0; P.max_nitems = 0;
     for (int a = 0; a < P.nang; ++a) {
         int bw, bh;
         best_rotation_size(top.w, top.h, tt.w, tt.h, P.angles[a], &bw, &bh);
@@ -376,6 +377,7 @@ int build_plan(fpm_ctx* ctx) {
             if (!mfc) nb = ncol * nrow + (rw > 0) + (rh > 0) + (rw > 0 && rh > 0);
             else nb = (ncol == 0 || nrow == 0) ? 0 : ncol * nrow + ((rw > 0 && rh > 0) ? 2 : 1);
             P.max_cells = std::max(P.max_cells, ((P.map_w[a] + tt.w - 1) / tt.w) * ((P.map_h[a] + tt.h - 1) / tt.h));
+            P.max_nitems = std::max(P.max_nitems, nms_block_items(P.map_w[a], P.map_h[a], tt.w, tt.h, mfc ? 1 : 0));
         }
         P.nblk[a] = nb;
         P.max_nblk = std::max(P.max_nblk, nb);
@@ -426,7 +428,10 @@ int build_plan(fpm_ctx* ctx) {
     HIP_TRY(P.d_state.ensure(sizeof(CandState) * (size_t)P.C));
     HIP_TRY(P.d_live.ensure(sizeof(int32_t) * (size_t)P.C * 2));
     // live counts [L + 2], then (s_BlockMax) the per-map candidate counts [J]: zeroed together by k_warp
-    HIP_TRY(P.d_livecnt.ensure(sizeof(int32_t) * ((size_t)L + 2 + (P.by_block ? J : 0))));
+    // (s_BlockMax) then the strip-block keys [J][3] (u64, 8-aligned) and chunk counts [J][3] of k_nms_blocks
+    P.off_skey = round_up(L + 2 + J, 2);
+    P.nzero = L + 2 + (P.by_block ? P.off_skey - (L + 2) + 9 * J : 0);
+    HIP_TRY(P.d_livecnt.ensure(sizeof(int32_t) * (size_t)P.nzero));
     HIP_TRY(P.d_rec.ensure(sizeof(RoiRecord) * (size_t)P.C * P.n3));
     {   // refinement scratch per ROI (tables, sampled ROI, row sums, window partials); bounded, rounds cover the rest
         size_t max_rows = 1, max_chunks = 1;
@@ -593,8 +598,7 @@ int enqueue_search(fpm_ctx* ctx) {
     {
         const int64_t bytes = (int64_t)P.nang * top.w * top.h;
         ProfScope ps(ctx, FPM_K_TOP_WARP, bytes * S);
-        launch_warp(P.d_jobs.as<WarpJob>(P.off_warp), J, P.max_canvas, st, P.d_livecnt.as<int32_t>(),
-                    L + 2 + (P.by_block ? J : 0));
+        launch_warp(P.d_jobs.as<WarpJob>(P.off_warp), J, P.max_canvas, st, P.d_livecnt.as<int32_t>(), P.nzero);
     }
     {
         int64_t bytes = 0;
@@ -619,12 +623,15 @@ int enqueue_search(fpm_ctx* ctx) {
         na.thr = P.layer_score[L]; na.overlap = ctx->prm.max_overlap;
         na.lds_blocks = 0;
         na.cand = nullptr; na.cand_cnt = nullptr; na.cand_cap = 0; na.cand_lds = 0; na.stamps = nullptr;
-        if (P.by_block) {   // (the counts were zeroed by k_warp)
+        na.skey = nullptr; na.sdone = nullptr;
+        if (P.by_block) {   // (the counts and strip keys were zeroed by k_warp)
             na.cand = P.d_ncand.as<int32_t>(); na.cand_cnt = P.d_livecnt.as<int32_t>() + L + 2; na.cand_cap = kNmsCandCap;
+            na.skey = (uint64_t*)(P.d_livecnt.as<int32_t>() + P.off_skey);
+            na.sdone = P.d_livecnt.as<int32_t>() + P.off_skey + 6 * J;
         }
         int mdim = 0;
         for (int a = 0; a < P.nang; ++a) mdim = std::max(mdim, std::max(P.map_w[a], P.map_h[a]));
-        launch_nms(na, J, P.max_nblk, mdim, P.max_cells, st);
+        launch_nms(na, J, P.max_nblk, mdim, P.max_cells, st, P.max_nitems);
     }
     int32_t* live[2] = {P.d_live.as<int32_t>(), P.d_live.as<int32_t>() + P.C};
     int32_t* livecnt = P.d_livecnt.as<int32_t>();

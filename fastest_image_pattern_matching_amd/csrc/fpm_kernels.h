@@ -61,6 +61,8 @@ struct NmsArgs {
     double thr;              // vecLayerScore[top]
     double overlap;
     uint64_t* stamps;        // profiling only (scripts/nms_probe.hip): k_nms_fast phase cycles of job 0, else null
+    uint64_t* skey;          // s_BlockMax mode: [job][3] strip-block maxima keys, zeroed before the launch
+    int32_t* sdone;          // [job][3] finished chunks of each strip block, zeroed before the launch
 };
 
 // Angle-tree node: the reference's refinement angle for one path, with glibc trig of angle*D2R.
@@ -166,7 +168,10 @@ void launch_ncc_tile(const NccJob* jobs, int njobs, int max_ow, int max_oh, int 
 constexpr int kNmsCandCap = 8192;   // s_BlockMax candidates (pixels >= the top-layer score) kept per map
 // max_blocks: s_BlockMax blocks of the largest map (block mode); max_map_dim: largest map width or height
 // max_cells: the largest ceil(mw / tw) * ceil(mh / th) over the maps (k_nms_greedy's coverage cells)
-void launch_nms(const NmsArgs& a, int njobs, int max_blocks, int max_map_dim, int max_cells, hipStream_t st);
+// max_items: the largest nms_block_items of the maps (k_nms_blocks' grid: strip blocks are scanned in chunks)
+void launch_nms(const NmsArgs& a, int njobs, int max_blocks, int max_map_dim, int max_cells, hipStream_t st,
+                int max_items = 0);
+int nms_block_items(int mw, int mh, int tw, int th, int mfc);
 void launch_cand_init(const CandInitArgs& a, hipStream_t st);
 void launch_roi_tables(const RoiArgs& a, hipStream_t st);
 void launch_roi_warp(const RoiArgs& a, hipStream_t st);

@@ -616,7 +616,7 @@ __device__ __forceinline__ void rect_max(const float* m, int mw, int x0, int y0,
 // right + bottom strips, the right strip alone, or else the full-width bottom strip (empty without any residue).
 struct BlockGeom {
     int bw, bh, ncol, nrow, rw, rh, nb, mfc;
-    __device__ void init(int mw, int mh, int tw, int th, int mfc_ = 0) {
+    __host__ __device__ void init(int mw, int mh, int tw, int th, int mfc_ = 0) {
         mfc = mfc_;
         bw = mfc ? 2 * tw : tw; bh = mfc ? 2 * th : th;
         ncol = mw / bw; nrow = mh / bh;
@@ -624,7 +624,7 @@ struct BlockGeom {
         if (!mfc) nb = ncol * nrow + (rw > 0) + (rh > 0) + (rw > 0 && rh > 0);
         else nb = (ncol == 0 || nrow == 0) ? 0 : ncol * nrow + ((rw > 0 && rh > 0) ? 2 : 1);
     }
-    __device__ void rect(int b, int mw, int mh, int& x, int& y, int& w, int& h) const {
+    __host__ __device__ void rect(int b, int mw, int mh, int& x, int& y, int& w, int& h) const {
         if (b < ncol * nrow) { x = (b % ncol) * bw; y = (b / ncol) * bh; w = bw; h = bh; return; }
         b -= ncol * nrow;
         if (mfc) {
@@ -637,7 +637,26 @@ struct BlockGeom {
         if (rh > 0) { if (b == 0) { x = 0; y = nrow * bh; w = ncol * bw; h = rh; return; } --b; }
         x = ncol * bw; y = nrow * bh; w = rw; h = rh;
     }
+    // k_nms_blocks' work items: the regular blocks, then each strip block (the right / bottom residue strips span
+    // the whole map height / width) cut into chunks of one regular block's area, scanned by separate waves
+    __host__ __device__ int nreg() const { return nb > 0 ? ncol * nrow : 0; }
+    __host__ __device__ int chunks(int b, int mw, int mh) const {
+        int x, y, w, h;
+        rect(b, mw, mh, x, y, w, h);
+        const long n = (long)w * h, e = (long)bw * bh;
+        return n <= e ? 1 : (int)((n + e - 1) / e);
+    }
+    __host__ __device__ int items(int mw, int mh) const {
+        int it = nreg();
+        for (int b = nreg(); b < nb; ++b) it += chunks(b, mw, mh);
+        return it;
+    }
 };
+int nms_block_items(int mw, int mh, int tw, int th, int mfc) {
+    BlockGeom g;
+    g.init(mw, mh, tw, th, mfc);
+    return g.items(mw, mh);
+}
 
 // wave argmax (value, key) with lowest-key tie-break, by DPP steps (no LDS round trip per step): quad swaps, row
 // half-mirror, row mirror, then row_bcast15 / row_bcast31 fold the rows into lane 63, read back to every lane
@@ -693,6 +712,67 @@ __device__ __forceinline__ void wave_rect_max(const float* m, int mw, int x0, in
 // K5a: the s_BlockMax constructor (DataStructures.h:150-213) for every top-layer map at once, one wave per block;
 // with a.cand it also lists the map's pixels >= thr (the only ones the peak loop can accept), each pixel once (the
 // corner block, which repeats the right strip's pixels, emits none)
+// s_BlockMax maxima of a key-combined strip chunk: the order-preserving u32 of a float (non-NaN), high word; the
+// complement of the map index, low word — a u64 atomicMax then keeps the largest value and, among equal values,
+// the first index (cv::minMaxLoc's rule); +-0 compare equal, so -0 enters as +0
+__device__ __forceinline__ uint64_t blockmax_key(float v, int i) {
+    uint32_t u = __float_as_uint(v == 0.f ? 0.f : v);
+    u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    return ((uint64_t)u << 32) | (uint32_t)(0xffffffffu - (uint32_t)i);
+}
+
+// one wave: maximum (first-max rule) of the elements [e0, e1) of a w-wide rectangle at (x, y) in row-major order,
+// and (cand) the pixels >= the top-layer score appended to the map's list in the same loads (k_nms_greedy sorts
+// the list, so its order is free)
+__device__ __forceinline__ void nms_scan(const NmsArgs& a, const NmsJob& j, int32_t* cand, int x, int y, int w,
+                                         int e0, int e1, int lane, float& bv, int& bi) {
+    float v = -INFINITY;
+    int i = INT_MAX;
+    const int e = e0 + lane;
+    int r = e / w, c = e - (e / w) * w;
+    const int dr = 64 / w, dc = 64 - (64 / w) * w;
+    constexpr int U = 8;   // wave-instructions of loads in flight before the first use
+    int ncand = 0;
+    for (int f0 = e0; f0 < e1; f0 += 64 * U) {
+        int idx[U];
+        float xv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            idx[u] = (y + r) * j.mw + x + c;
+            xv[u] = f0 + 64 * u + lane < e1 ? j.map[idx[u]] : -INFINITY;
+            r += dr;
+            c += dc;
+            if (c >= w) { c -= w; ++r; }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool in = f0 + 64 * u + lane < e1;
+            if (in && xv[u] > v) { v = xv[u]; i = idx[u]; }   // a lane visits increasing indices: strict > keeps the first
+            if (cand) ncand += __popcll(__ballot(in && (double)xv[u] >= a.thr));
+        }
+    }
+    wave_better_reduce(v, i);
+    if (ncand > 0) {   // one atomic per wave for its pixels >= the score, then (rare) a second pass writes them
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&a.cand_cnt[blockIdx.y], ncand);
+        base = __shfl(base, 0);
+        int rr = e / w, cc = e - (e / w) * w;
+        for (int f0 = e0; f0 < e1; f0 += 64) {
+            const int id2 = (y + rr) * j.mw + x + cc;
+            const bool take = f0 + lane < e1 && (double)j.map[id2] >= a.thr;
+            const uint64_t mk = __ballot(take);
+            const int pos = base + __popcll(mk & ((1ull << lane) - 1));
+            if (take && pos < a.cand_cap) cand[pos] = id2;
+            base += __popcll(mk);
+            rr += dr;
+            cc += dc;
+            if (cc >= w) { cc -= w; ++rr; }
+        }
+    }
+    bv = v;
+    bi = i;
+}
+
 __global__ __launch_bounds__(256) void k_nms_blocks(NmsArgs a) {
     const NmsJob& j = a.jobs[blockIdx.y];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -701,31 +781,41 @@ __global__ __launch_bounds__(256) void k_nms_blocks(NmsArgs a) {
     if (j.mw <= 0 || j.mh <= 0) return;
     const int corner = (!g.mfc && g.rw > 0 && g.rh > 0) ? g.nb - 1 : -1;   // (MFC has no corner block)
     int32_t* cand = a.cand ? a.cand + (size_t)blockIdx.y * a.cand_cap : nullptr;
-    for (int b = blockIdx.x * 4 + wv; b < g.nb; b += gridDim.x * 4) {
+    const int nreg = g.nreg();
+    int ch[3] = {0, 0, 0}, nitems = nreg;
+    for (int s = 0; s < g.nb - nreg && s < 3; ++s) {   // (no key scratch: every strip by one wave)
+        ch[s] = a.skey ? g.chunks(nreg + s, j.mw, j.mh) : 1;
+        nitems += ch[s];
+    }
+    for (int item = blockIdx.x * 4 + wv; item < nitems; item += gridDim.x * 4) {
+        int b = item, k = 0, nk = 1, s = 0;
+        if (item >= nreg) {
+            int t = item - nreg;
+            while (t >= ch[s]) { t -= ch[s]; ++s; }
+            b = nreg + s; k = t; nk = ch[s];
+        }
         int x, y, w, h;
         g.rect(b, j.mw, j.mh, x, y, w, h);
-        float v;
-        int i;
-        wave_rect_max(j.map, j.mw, x, y, w, h, lane, v, i);
-        if (lane == 0) { j.bmax[b] = v; j.bloc[b] = i >= 0 ? i : empty_loc(b); }
-        if (cand && b != corner && w * h > 0) {
-            const int n = w * h;
-            int r = lane / w, c = lane - (lane / w) * w;
-            const int dr = 64 / w, dc = 64 - (64 / w) * w;
-            for (int e0 = 0; e0 < n; e0 += 64) {
-                const int idx = (y + r) * j.mw + x + c;
-                const bool take = e0 + lane < n && (double)j.map[idx] >= a.thr;
-                const uint64_t mk = __ballot(take);
-                if (mk) {
-                    int base = 0;
-                    if (lane == 0) base = atomicAdd(&a.cand_cnt[blockIdx.y], __popcll(mk));
-                    base = __shfl(base, 0);
-                    const int pos = base + __popcll(mk & ((1ull << lane) - 1));
-                    if (take && pos < a.cand_cap) cand[pos] = idx;
-                }
-                r += dr;
-                c += dc;
-                if (c >= w) { c -= w; ++r; }
+        const int n = w * h;
+        float v = 0.f;
+        int i = -1;   // an empty rectangle: cv::minMaxLoc's 0 at (-1, -1) (wave_rect_max)
+        if (n > 0) {
+            const int e0 = nk == 1 ? 0 : k * g.bw * g.bh, e1 = nk == 1 ? n : min(n, e0 + g.bw * g.bh);
+            nms_scan(a, j, (cand && b != corner) ? cand : nullptr, x, y, w, e0, e1, lane, v, i);
+        }
+        if (nk == 1) {
+            if (lane == 0) { j.bmax[b] = v; j.bloc[b] = i >= 0 ? i : empty_loc(b); }
+            continue;
+        }
+        if (lane == 0) {   // a strip chunk: combine by key; the last chunk to finish writes the block's maximum
+            uint64_t* key = a.skey + (size_t)blockIdx.y * 3 + s;
+            atomicMax((unsigned long long*)key, (unsigned long long)blockmax_key(v, i));
+            __threadfence();
+            if (atomicAdd(a.sdone + (size_t)blockIdx.y * 3 + s, 1) == nk - 1) {
+                const uint64_t fin = atomicMax((unsigned long long*)key, 0ull);
+                const int fi = (int)(0xffffffffu - (uint32_t)fin);
+                j.bmax[b] = fi == INT_MAX ? -INFINITY : j.map[fi];
+                j.bloc[b] = fi;
             }
         }
     }
@@ -1253,11 +1343,13 @@ static size_t nms_fast_lds(int blocks, int /*cap*/, int cands) {
 constexpr int kNmsLdsBlocksMax = 12 * 1024;   // block maxima kept in LDS up to this many blocks
 constexpr int kNmsLdsBytes = 160 * 1024 - 4096;   // k_nms_fast dynamic LDS budget (statics take the rest)
 
-void launch_nms(const NmsArgs& a0, int njobs, int max_blocks, int max_map_dim, int max_cells, hipStream_t st) {
+void launch_nms(const NmsArgs& a0, int njobs, int max_blocks, int max_map_dim, int max_cells, hipStream_t st,
+                int max_items) {
     if (njobs <= 0) return;
     NmsArgs a = a0;
     if (a.by_block && max_blocks > 0) {
-        hipLaunchKernelGGL(k_nms_blocks, dim3((max_blocks + 3) / 4 < 16384 ? (max_blocks + 3) / 4 : 16384, njobs),
+        const int items = max_items > max_blocks ? max_items : max_blocks;
+        hipLaunchKernelGGL(k_nms_blocks, dim3((items + 3) / 4 < 16384 ? (items + 3) / 4 : 16384, njobs),
                            dim3(256), 0, st, a);
         // the greedy form takes what it can (thr > 0: an empty strip's stale 0 is never a peak); k_nms the rest
         const bool greedy = a.cand && !a.stamps && a.thr > 0.0 && max_map_dim < 65536 && a.cap <= 256 &&
