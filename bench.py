@@ -226,7 +226,9 @@ def main():
         log(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a wrong n_gpus")
         sys.exit(2)
     if args.dry_run:
-        print(json.dumps({"rank": rank, "world": world, "local_rank": local}), flush=True)
+        # one write of the whole line (< PIPE_BUF): the ranks share the launcher's stdout and must not interleave
+        sys.stdout.write(json.dumps({"rank": rank, "world": world, "local_rank": local}) + "\n")
+        sys.stdout.flush()
         return
     import torch
 

@@ -3,6 +3,7 @@ outside torchrun starts N ranks itself, and a WORLD_SIZE that disagrees with --g
 a wrong n_gpus."""
 import json
 import os
+import re
 import subprocess
 import sys
 
@@ -20,7 +21,7 @@ def test_gpus_2_spawns_two_ranks():
     out = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run"], capture_output=True, text=True,
                          timeout=240, env=_env())
     assert out.returncode == 0, out.stderr
-    ranks = [json.loads(line) for line in out.stdout.splitlines() if line.startswith("{")]
+    ranks = [json.loads(m) for m in re.findall(r"\{[^{}]*\}", out.stdout)]
     assert sorted((r["rank"], r["world"]) for r in ranks) == [(0, 2), (1, 2)]
 
 
