@@ -379,22 +379,27 @@ void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
     };
     if (n <= 512) geom(0, n);
     else host_parallel((n + 511) / 512, [&](int t) { geom(t * 512, std::min(n, t * 512 + 512)); });
-    auto pair = [&](int i, int j) {   // the reference's inner-loop body for (i, j), boxes overlapping
+    // the reference's inner-loop body for (i, j), boxes overlapping: the index it deletes, or -1
+    auto pair_del = [&](int i, int j) {
         F2 pts[24];
         int np = 0;
         const int kind = rrect_isect(v[i].rect, v[j].rect, &corners[(size_t)4 * i], &corners[(size_t)4 * j], pts, &np);
 #ifdef FPM_HOST_STATS
         g_stats[kind]++; g_stats[3 + np]++;
 #endif
-        if (kind == 0) return;
+        if (kind == 0) return -1;
         bool drop = kind == 2;
         if (kind == 1) {
-            if (np < 3) return;
+            if (np < 3) return -1;
             sort_pts_center(pts, np);
             const double ratio = contour_area_a(pts, np) / (v[i].rect.w * v[i].rect.h);
             drop = ratio > max_overlap;
         }
-        if (drop) v[(v[i].score >= v[j].score) ? j : i].del = true;
+        return drop ? ((v[i].score >= v[j].score) ? j : i) : -1;
+    };
+    auto pair = [&](int i, int j) {
+        const int d = pair_del(i, j);
+        if (d >= 0) v[d].del = true;
     };
     auto overlap = [&](int i, int j) {
         const float* bi = &box[4 * i];
@@ -464,10 +469,17 @@ void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
             std::vector<int> fill(comp_off.begin(), comp_off.end() - 1);
             for (int i = 0; i < n; ++i) members[fill[comp_of[i]]++] = i;   // ascending within a component
         }
-        auto run_comp = [&](int c, std::vector<int>& nb) {
-            for (int k = comp_off[c]; k < comp_off[c + 1]; ++k) {
+        // a box's position inside its component (members ascending): the components keep their deletion flags in
+        // private arrays while they run and write them back at the end, so workers never share a written cache line
+        std::vector<int> local(n);
+        for (int c = 0; c < ncomp; ++c)
+            for (int k = comp_off[c]; k < comp_off[c + 1]; ++k) local[members[k]] = k - comp_off[c];
+        auto run_comp = [&](int c, std::vector<int>& nb, std::vector<char>& del) {
+            const int m0 = comp_off[c], m1 = comp_off[c + 1];
+            del.assign(m1 - m0, 0);
+            for (int k = m0; k < m1; ++k) {
                 const int i = members[k];
-                if (v[i].del) continue;
+                if (del[k - m0]) continue;
                 nb.clear();
                 for (int cy = span[i].y; cy <= span[i].w; ++cy)
                     for (int cx = span[i].x; cx <= span[i].z; ++cx) {
@@ -478,17 +490,24 @@ void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
                 std::sort(nb.begin(), nb.end());
                 nb.erase(std::unique(nb.begin(), nb.end()), nb.end());
                 for (int j : nb)
-                    if (!v[j].del && overlap(i, j)) pair(i, j);
+                    if (!del[local[j]] && overlap(i, j)) {
+                        const int d = pair_del(i, j);
+                        if (d >= 0) del[local[d]] = 1;
+                    }
             }
+            for (int k = m0; k < m1; ++k)
+                if (del[k - m0]) v[members[k]].del = true;
         };
         // workers only where there is exact-test work to spread (clusters of duplicate detections)
         if (ncomp < 8 || n - ncomp < 64) {
             std::vector<int> nb;
-            for (int c = 0; c < ncomp; ++c) run_comp(c, nb);
+            std::vector<char> del;
+            for (int c = 0; c < ncomp; ++c) run_comp(c, nb, del);
         } else {
             host_parallel(ncomp, [&](int c) {
                 thread_local std::vector<int> nb;
-                run_comp(c, nb);
+                thread_local std::vector<char> del;
+                run_comp(c, nb, del);
             });
         }
     }
