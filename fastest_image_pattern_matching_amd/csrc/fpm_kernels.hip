@@ -245,7 +245,7 @@ __global__ __launch_bounds__(256) void k_pyr_down(const uint8_t* __restrict__ sr
     }
 }
 
-// ---- K1, streaming form (the product's): one workgroup = a strip of PD_OW output columns x a segment of output
+// ---- K1, streaming form (the product's): one workgroup = a strip of PD_OW output columns x a run of output
 // rows, walked down in chunks of PD_OH output rows.  The 4 input rows two chunks share are carried as horizontal
 // sums (no re-read), and the next chunk's 64 input rows are loaded into registers while the current chunk is
 // filtered and stored, so every workgroup keeps its loads in flight for its whole life instead of one burst per
@@ -254,129 +254,145 @@ __global__ __launch_bounds__(256) void k_pyr_down(const uint8_t* __restrict__ sr
 constexpr int PS_NL = (PD_IH * (PD_IW / 16) + 255) / 256;   // 16-byte loads per thread for a 68-row window: 5
 typedef unsigned short fpm_u16x2 __attribute__((ext_vector_type(2)));
 
-__global__ __launch_bounds__(256) void k_pyr_down_s(const uint8_t* __restrict__ src, int sw, int sh, int sp,
-                                                    size_t s_img, uint8_t* __restrict__ dst, int dw, int dh,
-                                                    int dp, size_t d_img, int seg_rows) {
+__global__ __launch_bounds__(256) void k_pyr_down_s(const uint8_t* __restrict__ src0, int sw, int sh, int sp,
+                                                    size_t s_img, uint8_t* __restrict__ dst0, int dw, int dh,
+                                                    int dp, size_t d_img, int nimg) {
     __shared__ __attribute__((aligned(16))) uint8_t tin[PD_IH][PD_IW];
     __shared__ __attribute__((aligned(16))) uint16_t hs[PD_IH][PD_OW];
-    // (strip, segment, image) in row-major order, XCD groups on contiguous ranges (neighbouring strips share the
-    // halo columns' lines)
-    const int gx = gridDim.x, gy = gridDim.y;
-    const int t = xcd_remap(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
-    const int bx = t % gx, byz = t / gx, by = byz % gy, bz = byz / gy;
-    src += (size_t)bz * s_img;
-    dst += (size_t)bz * d_img;
+    // work units = (image, strip, chunk) in row-major order; workgroup w takes the contiguous range
+    // [U*w/G, U*(w+1)/G) (equal shares: no tail round of a few workgroups), split where it crosses a strip; XCD
+    // groups take contiguous ranges of workgroups (neighbouring strips share the halo columns' lines)
+    const int gx = (dw + PD_OW - 1) / PD_OW, chunks = (dh + PD_OH - 1) / PD_OH;
+    const long U = (long)gx * chunks * nimg;
+    const int w = xcd_remap(blockIdx.x, gridDim.x);
+    long u = U * w / gridDim.x;
+    const long u_end = U * (w + 1) / gridDim.x;
     const int tid = threadIdx.x;
-    const int ox0 = bx * PD_OW;
-    const int oy_begin = by * seg_rows, oy_end = min(dh, oy_begin + seg_rows);
-    if (oy_begin >= oy_end) return;   // uniform per workgroup
-    const int ix0 = 2 * ox0 - 16;     // tin column 0 <-> source column ix0 (16-byte aligned)
-    constexpr int Q = PD_IW / 16;     // 18 uint4 per row
-    auto srow = [&](int y) {          // one reflection covers every row an output needs (-2 .. sh+1)
-        y = y < 0 ? -y : y;
-        y = y >= sh ? 2 * sh - 2 - y : y;
-        return y < 0 ? 0 : (y >= sh ? sh - 1 : y);
-    };
-    uint4 v[PS_NL];
-    // window rows [roff, roff + nrows) <- input rows iy .. iy + nrows - 1, element i = tid + 256k -> (i / Q, i % Q)
-    auto issue = [&](int iy, int nrows) {
+    while (u < u_end) {
+        const long strip = u / chunks;
+        const int c0 = (int)(u - strip * chunks);
+        const int run = (int)min(u_end - u, (long)(chunks - c0));
+        u += run;
+        const int bx = (int)(strip % gx), bz = (int)(strip / gx);
+        const uint8_t* src = src0 + (size_t)bz * s_img;
+        uint8_t* dst = dst0 + (size_t)bz * d_img;
+        const int ox0 = bx * PD_OW;
+        const int oy_begin = c0 * PD_OH, oy_end = min(dh, (c0 + run) * PD_OH);
+        __syncthreads();   // the previous run is done with tin / hs
+        const int ix0 = 2 * ox0 - 16;     // tin column 0 <-> source column ix0 (16-byte aligned)
+        constexpr int Q = PD_IW / 16;     // 18 uint4 per row
+        auto srow = [&](int y) {          // one reflection covers every row an output needs (-2 .. sh+1)
+            y = y < 0 ? -y : y;
+            y = y >= sh ? 2 * sh - 2 - y : y;
+            return y < 0 ? 0 : (y >= sh ? sh - 1 : y);
+        };
+        uint4 v[PS_NL];
+        // window rows [roff, roff + nrows) <- input rows iy .. iy + nrows - 1, element i = tid + 256k -> (i / Q, i % Q)
+        auto issue = [&](int iy, int nrows) {
 #pragma unroll
-        for (int k = 0; k < PS_NL; ++k) {
-            const int i = tid + 256 * k;
-            const int r = i / Q, c = i - r * Q;
-            const int x = ix0 + 16 * c;
-            v[k] = make_uint4(0, 0, 0, 0);
-            if (r < nrows && x >= 0 && x + 16 <= sp) v[k] = *(const uint4*)(src + (size_t)srow(iy + r) * sp + x);
-        }
-    };
-    auto commit = [&](int roff, int nrows) {
-#pragma unroll
-        for (int k = 0; k < PS_NL; ++k) {
-            const int i = tid + 256 * k;
-            const int r = i / Q, c = i - r * Q;
-            if (r < nrows) *(uint4*)&tin[roff + r][16 * c] = v[k];
-        }
-    };
-    // columns outside [0, sw) that an output of this strip reads (at most 2 on each side): reflect-101
-    const int xlo = 2 * ox0 - 2, xhi = min(2 * (ox0 + PD_OW - 1) + 2, 2 * (dw - 1) + 2);
-    const bool edge = xlo < 0 || xhi >= sw;   // uniform per workgroup
-    issue(2 * oy_begin - 2, PD_IH);
-    for (int oyc = oy_begin; oyc < oy_end; oyc += PD_OH) {
-        const bool first = oyc == oy_begin;
-        const int roff = first ? 0 : 4, nrows = first ? PD_IH : 2 * PD_OH;
-        const int iy = 2 * oyc - 2 + roff;
-        commit(roff, nrows);
-        if (edge) {
-            __syncthreads();   // the 16-byte tile stores above cover the patched bytes
-            for (int i = tid; i < nrows * 4; i += 256) {
-                const int r = i >> 2, k = i & 3;
-                const int x = k < 2 ? xlo + k : xhi - (k - 2);   // xlo, xlo+1, xhi, xhi-1
-                if ((x < 0 && k < 2) || (x >= sw && k >= 2))
-                    tin[roff + r][x - ix0] = src[(size_t)srow(iy + r) * sp + reflect101(x, sw)];
+            for (int k = 0; k < PS_NL; ++k) {
+                const int i = tid + 256 * k;
+                const int r = i / Q, c = i - r * Q;
+                const int x = ix0 + 16 * c;
+                v[k] = make_uint4(0, 0, 0, 0);
+                if (r < nrows && x >= 0 && x + 16 <= sp) v[k] = *(const uint4*)(src + (size_t)srow(iy + r) * sp + x);
             }
-        }
-        __syncthreads();
-        // the next chunk's 64 new input rows (its window rows 4..67) are in flight while this chunk is filtered
-        if (oyc + PD_OH < oy_end) issue(2 * oyc + 2 * PD_OH + 2, 2 * PD_OH);
-        // horizontal [1 4 6 4 1] of the new window rows: 4 consecutive outputs per item (as k_pyr_down; the 5th tap
-        // enters the v_dot4 as its accumulator)
-        const int nh = nrows * (PD_OW / 4);
-        for (int i = tid; i < nh; i += 256) {
-            const int r = roff + i / (PD_OW / 4), g = i % (PD_OW / 4);
-            const uint32_t* w = (const uint32_t*)&tin[r][8 * g + 12];
-            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
-            const uint32_t h0 = __builtin_amdgcn_udot4(PD_K, __builtin_amdgcn_alignbyte(w1, w0, 2), (w1 >> 16) & 0xff, false);
-            const uint32_t h1 = __builtin_amdgcn_udot4(PD_K, w1, w2 & 0xff, false);
-            const uint32_t h2 = __builtin_amdgcn_udot4(PD_K, __builtin_amdgcn_alignbyte(w2, w1, 2), (w2 >> 16) & 0xff, false);
-            const uint32_t h3 = __builtin_amdgcn_udot4(PD_K, w2, w3 & 0xff, false);
-            uint2 o;
-            o.x = h0 | (h1 << 16);
-            o.y = h2 | (h3 << 16);
-            *(uint2*)&hs[r][4 * g] = o;
-        }
-        __syncthreads();
-        // vertical: 4 consecutive outputs of one row per item, two per register in packed u16 arithmetic — exact:
-        // a horizontal sum is <= 16 * 255, so 128 + sum_t k_t * h_t <= 65408 fits 16 bits, and (v >> 8) is the
-        // half's high byte, gathered by one v_perm
+        };
+        auto commit = [&](int roff, int nrows) {
 #pragma unroll
-        for (int k = 0; k < PD_OH * (PD_OW / 4) / 256; ++k) {
-            const int i = tid + 256 * k;
-            const int orow = i / (PD_OW / 4), g = i - orow * (PD_OW / 4);
-            const int oy = oyc + orow, ox = ox0 + 4 * g;
-            if (oy >= oy_end || ox >= dw) continue;
-            fpm_u16x2 a01 = {128, 128}, a23 = {128, 128};
-            constexpr unsigned short kw[5] = {1, 4, 6, 4, 1};
+            for (int k = 0; k < PS_NL; ++k) {
+                const int i = tid + 256 * k;
+                const int r = i / Q, c = i - r * Q;
+                if (r < nrows) *(uint4*)&tin[roff + r][16 * c] = v[k];
+            }
+        };
+        // columns outside [0, sw) that an output of this strip reads (at most 2 on each side): reflect-101
+        const int xlo = 2 * ox0 - 2, xhi = min(2 * (ox0 + PD_OW - 1) + 2, 2 * (dw - 1) + 2);
+        const bool edge = xlo < 0 || xhi >= sw;   // uniform per workgroup
+        issue(2 * oy_begin - 2, PD_IH);
+        for (int oyc = oy_begin; oyc < oy_end; oyc += PD_OH) {
+            const bool first = oyc == oy_begin;
+            const int roff = first ? 0 : 4, nrows = first ? PD_IH : 2 * PD_OH;
+            const int iy = 2 * oyc - 2 + roff;
+            commit(roff, nrows);
+            if (edge) {
+                __syncthreads();   // the 16-byte tile stores above cover the patched bytes
+                for (int i = tid; i < nrows * 4; i += 256) {
+                    const int r = i >> 2, k = i & 3;
+                    const int x = k < 2 ? xlo + k : xhi - (k - 2);   // xlo, xlo+1, xhi, xhi-1
+                    if ((x < 0 && k < 2) || (x >= sw && k >= 2))
+                        tin[roff + r][x - ix0] = src[(size_t)srow(iy + r) * sp + reflect101(x, sw)];
+                }
+            }
+            __syncthreads();
+            // the next chunk's 64 new input rows (its window rows 4..67) are in flight while this chunk is filtered
+            if (oyc + PD_OH < oy_end) issue(2 * oyc + 2 * PD_OH + 2, 2 * PD_OH);
+            // horizontal [1 4 6 4 1] of the new window rows: 4 consecutive outputs per item (as k_pyr_down; the 5th tap
+            // enters the v_dot4 as its accumulator)
+            const int nh = nrows * (PD_OW / 4);
+            for (int i = tid; i < nh; i += 256) {
+                const int r = roff + i / (PD_OW / 4), g = i % (PD_OW / 4);
+                const uint32_t* w = (const uint32_t*)&tin[r][8 * g + 12];
+                const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
+                const uint32_t h0 = __builtin_amdgcn_udot4(PD_K, __builtin_amdgcn_alignbyte(w1, w0, 2), (w1 >> 16) & 0xff, false);
+                const uint32_t h1 = __builtin_amdgcn_udot4(PD_K, w1, w2 & 0xff, false);
+                const uint32_t h2 = __builtin_amdgcn_udot4(PD_K, __builtin_amdgcn_alignbyte(w2, w1, 2), (w2 >> 16) & 0xff, false);
+                const uint32_t h3 = __builtin_amdgcn_udot4(PD_K, w2, w3 & 0xff, false);
+                uint2 o;
+                o.x = h0 | (h1 << 16);
+                o.y = h2 | (h3 << 16);
+                *(uint2*)&hs[r][4 * g] = o;
+            }
+            __syncthreads();
+            // vertical: 4 consecutive outputs of one row per item, two per register in packed u16 arithmetic — exact:
+            // a horizontal sum is <= 16 * 255, so 128 + sum_t k_t * h_t <= 65408 fits 16 bits, and (v >> 8) is the
+            // half's high byte, gathered by one v_perm
 #pragma unroll
-            for (int tt = 0; tt < 5; ++tt) {
-                const uint2 q = *(const uint2*)&hs[2 * orow + tt][4 * g];
-                a01 += __builtin_bit_cast(fpm_u16x2, q.x) * kw[tt];
-                a23 += __builtin_bit_cast(fpm_u16x2, q.y) * kw[tt];
+            for (int k = 0; k < PD_OH * (PD_OW / 4) / 256; ++k) {
+                const int i = tid + 256 * k;
+                const int orow = i / (PD_OW / 4), g = i - orow * (PD_OW / 4);
+                const int oy = oyc + orow, ox = ox0 + 4 * g;
+                if (oy >= oy_end || ox >= dw) continue;
+                fpm_u16x2 a01 = {128, 128}, a23 = {128, 128};
+                constexpr unsigned short kw[5] = {1, 4, 6, 4, 1};
+#pragma unroll
+                for (int tt = 0; tt < 5; ++tt) {
+                    const uint2 q = *(const uint2*)&hs[2 * orow + tt][4 * g];
+                    a01 += __builtin_bit_cast(fpm_u16x2, q.x) * kw[tt];
+                    a23 += __builtin_bit_cast(fpm_u16x2, q.y) * kw[tt];
+                }
+                const uint32_t packed = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, a23),
+                                                              __builtin_bit_cast(uint32_t, a01), 0x07050301u);
+                uint8_t* d = dst + (size_t)oy * dp + ox;
+                if (ox + 4 <= dw) {
+                    *(uint32_t*)d = packed;
+                } else {
+                    for (int j = 0; j < dw - ox; ++j) d[j] = (uint8_t)(packed >> (8 * j));
+                }
             }
-            const uint32_t packed = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, a23),
-                                                          __builtin_bit_cast(uint32_t, a01), 0x07050301u);
-            uint8_t* d = dst + (size_t)oy * dp + ox;
-            if (ox + 4 <= dw) {
-                *(uint32_t*)d = packed;
-            } else {
-                for (int j = 0; j < dw - ox; ++j) d[j] = (uint8_t)(packed >> (8 * j));
-            }
+            __syncthreads();
+            // carry: window rows 64..67 (input rows 2 * (oyc + PD_OH) - 2 .. + 1) are the next window's rows 0..3
+            ((uint32_t*)hs[tid >> 6])[tid & 63] = ((uint32_t*)hs[2 * PD_OH + (tid >> 6)])[tid & 63];
+            __syncthreads();
         }
-        __syncthreads();
-        // carry: window rows 64..67 (input rows 2 * (oyc + PD_OH) - 2 .. + 1) are the next window's rows 0..3
-        ((uint32_t*)hs[tid >> 6])[tid & 63] = ((uint32_t*)hs[2 * PD_OH + (tid >> 6)])[tid & 63];
-        __syncthreads();
     }
 }
 
+static const int kPyrWGs = [] {   // FPM_PYR_WGS: profiling override
+    const char* e = getenv("FPM_PYR_WGS");
+    return e && atoi(e) > 0 ? atoi(e) : 4096;
+}();
 void launch_pyr_down(const uint8_t* src, int sw, int sh, int sp, size_t s_img, uint8_t* dst, int dw, int dh,
                      int dp, size_t d_img, int nimg, hipStream_t st, int seg_chunks) {
-    // segments of whole chunks, as many chunks per workgroup as keeps ~2048 workgroups (2 rounds of 4 per CU)
+    // equal shares of the (image, strip, chunk) units over kPyrWGs workgroups (4 rounds of 4 per CU; measured
+    // 2048 / 4096 / 8192: 37.1 / 35.7 / 36.0 µs per launch averaged over the Src7 levels), or
+    // seg_chunks units each
+    if (dw <= 0 || dh <= 0 || nimg <= 0) return;
     const int gx = (dw + PD_OW - 1) / PD_OW, chunks = (dh + PD_OH - 1) / PD_OH;
     const long units = (long)gx * chunks * nimg;
-    const int per = seg_chunks > 0 ? seg_chunks : (int)std::max(1L, std::min((long)chunks, units / 2048));
-    const int seg_rows = per * PD_OH;
-    dim3 grid(gx, (dh + seg_rows - 1) / seg_rows, nimg);
-    hipLaunchKernelGGL(k_pyr_down_s, grid, dim3(256), 0, st, src, sw, sh, sp, s_img, dst, dw, dh, dp, d_img, seg_rows);
+    const long g = seg_chunks > 0 ? (units + seg_chunks - 1) / seg_chunks : std::min(units, (long)kPyrWGs);
+    hipLaunchKernelGGL(k_pyr_down_s, dim3((unsigned)g), dim3(256), 0, st, src, sw, sh, sp, s_img, dst, dw, dh, dp,
+                       d_img, nimg);
 }
 
 // ============================================================================================== K2
