@@ -2576,8 +2576,8 @@ size_t roi_small_lds(int tw, int th) { return (size_t)small_layout(tw, th).total
 // MODE (profiling ablations in scripts/roi_microbench.hip; the product uses 0): 1 = tables + sampling only,
 // 2 = + row / window sums, 3 = + bands without the fold, 5 = full with byte-gather taps, 9 = full with per-phase
 // s_memtime stamps (a.stamps)
-template <int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_roi_small(RoiArgs a) {
+template <int MODE, int WPE = 3>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_small(RoiArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tw = a.tw, th = a.th, RW = tw + 6, RH = th + 6, W = a.W, H = a.H;
     const SmallLayout LY = small_layout(tw, th);
@@ -3174,6 +3174,7 @@ void launch_roi_eval(const RoiArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_roi_eval, dim3(grid), dim3(64 * a.n3), 0, st, a);
 }
 
+constexpr size_t kLdsPerCu = 160 * 1024;   // MI355X (gfx950) LDS per CU
 void launch_roi_small(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0) return;
     if (a.equal1) {   // records of ones (CCOEFF_Denominator :529-533); the step follows in k_cand_step
@@ -3183,8 +3184,15 @@ void launch_roi_small(const RoiArgs& a, hipStream_t st) {
         return;
     }
     const size_t lds = (size_t)small_layout(a.tw, a.th).total;
-    ensure_lds_attr((const void*)k_roi_small<0>, lds);
     const int grid = a.slot_cap < 8192 ? a.slot_cap : 8192;
+    // 4 waves per SIMD where 4 workgroups' LDS fit a CU (Src7 layers 5 and 4: 46.8 -> 42.4 and 54.7 -> 47.4 us per
+    // 43-source launch despite a 48-byte spill; 5 waves spill 176 bytes and measured slower), else 3
+    if (lds * 4 <= kLdsPerCu) {
+        ensure_lds_attr((const void*)k_roi_small<0, 4>, lds);
+        hipLaunchKernelGGL((k_roi_small<0, 4>), dim3(grid), dim3(256), lds, st, a);
+        return;
+    }
+    ensure_lds_attr((const void*)k_roi_small<0>, lds);
     hipLaunchKernelGGL(k_roi_small<0>, dim3(grid), dim3(256), lds, st, a);
 }
 
