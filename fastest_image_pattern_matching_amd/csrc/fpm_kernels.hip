@@ -3118,6 +3118,7 @@ void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_roi_warp<kWarpFootBatch>, dim3(grid), dim3(256), 0, st, a);
 }
 
+constexpr size_t kLdsPerCu = 160 * 1024;   // MI355X (gfx950) LDS per CU
 constexpr bool kCorrGlobalA = true;   // measured in scripts/roi_microbench.hip
 constexpr int kCorrWaves = 3;
 // register-A form at 13-16 k-steps: 2 waves per SIMD (A fragments + prefetched rows: 221 VGPRs), one workgroup per
@@ -3129,6 +3130,13 @@ static void launch_corr_regs(const RoiArgs& a, long items, size_t lds, hipStream
     if constexpr (NK <= 12) {
         // up to 12 k-steps the A fragments fit 3 waves per SIMD (166 VGPRs) without the row prefetch; measured
         // faster than the prefetching 2-wave form (occupancy hides the staging latency better)
+        // at 4 k-steps 4 waves per SIMD pay despite a 28-byte spill (Src7 layer 2: 68.2 -> 58.0 us per 43-source
+        // launch); at 8 / 12 k-steps the larger spills lose (136.5 -> 145.2, 301.1 -> 403.2 us)
+        if (NK == 4 && lds * 4 <= kLdsPerCu) {
+            const int grid = (int)(items < 256 * 4 ? items : 256 * 4);
+            hipLaunchKernelGGL((k_roi_corr<0, true, 4, NK, false>), dim3(grid), dim3(256), lds, st, a);
+            return;
+        }
         const int grid = (int)(items < 256 * kCorrWaves ? items : 256 * kCorrWaves);
         hipLaunchKernelGGL((k_roi_corr<0, true, kCorrWaves, NK, false>), dim3(grid), dim3(256), lds, st, a);
     } else {
@@ -3174,7 +3182,6 @@ void launch_roi_eval(const RoiArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_roi_eval, dim3(grid), dim3(64 * a.n3), 0, st, a);
 }
 
-constexpr size_t kLdsPerCu = 160 * 1024;   // MI355X (gfx950) LDS per CU
 void launch_roi_small(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0) return;
     if (a.equal1) {   // records of ones (CCOEFF_Denominator :529-533); the step follows in k_cand_step
