@@ -19,7 +19,10 @@ kernel (fpm_profile_get): B_pyr + B_top + B_ref, where a refinement ROI costs it
 level and the 7x7 f32 scores; scratch this design writes between its kernels (sampled ROIs, row sums) is not
 algorithmic and shows up only in `traffic` (PMC HBM bytes), so traffic / algorithmic bytes measures that overhead.
 ``roofline`` is the dominant kernel's (its §8(d) share per launch / its average launch time); ``roofline_search``
-is the whole search's (bytes of all searches of the timed region / its wall time).
+is the whole search's (bytes of all searches of the timed region / its wall time).  §8(d) also asks for the MAC
+view: ``roofline_mac`` = the §8(d) MACs of every search of the timed region (top-layer maps x top template +
+49 w_l h_l per live refinement ROI) / the wall time against the i8 MFMA dense peak, and ``roofline_corr`` = the
+refinement correlation kernel's useful MACs per launch / its average launch time on the same peak.
 
 ``python bench.py --gpus N`` with no torchrun environment starts N ranks itself (torch.distributed.run, one process
 per GPU) before anything touches a GPU; under torchrun, --gpus must equal WORLD_SIZE.
@@ -168,6 +171,37 @@ def kernel_pass(m, sources, steps, L):
                 "bytes_definition": "SURVEY.md §8(d) share of this kernel per launch (fpm_profile_get)",
                 "traffic_source": TRAFFIC_SOURCE if traffic is not None else None}
     return kern, roofline
+
+
+I8_MFMA_PEAK_TOPS = 5000.0           # MI355X_MICROARCH.md matrix-core table: I8 at 2x the BF16 rate (~2.5 PF dense)
+
+
+def level_sizes(w, h, n):
+    """(w_l, h_l) of pyramid levels 0..n (cv::pyrDown: ((w + 1) / 2, (h + 1) / 2))."""
+    out = [(w, h)]
+    for _ in range(n):
+        w, h = (w + 1) // 2, (h + 1) // 2
+        out.append((w, h))
+    return out
+
+
+def search_macs(ctx, src_wh, tmpl_wh, n_sources):
+    """SURVEY.md §8(d) MACs of the context's last search pass (all its sources), from its live counts:
+    MAC = sum_angles |R_a| w_L h_L + sum_l sum_live n_ang_l 49 w_l h_l.  |R_a| (top-layer map sizes) and n_ang_l come
+    back out of the same pass's B_top and B_ref (fpm_search_bytes), so nothing is re-derived from the plan.
+    Returns (mac_top, [mac_ref per refinement layer, top-most first])."""
+    st = ctx.search_stats()
+    nang, L = st[0], len(st) - 2
+    live = st[2:2 + L]
+    src = level_sizes(*src_wh, L)
+    tm = level_sizes(*tmpl_wh, L)
+    _, b_top, b_ref = ctx.search_bytes()
+    sum_r = (b_top - n_sources * nang * src[L][0] * src[L][1]) // 4
+    mac_top = sum_r * tm[L][0] * tm[L][1]
+    layers = [tm[L - 1 - d] for d in range(L)]
+    denom = sum(n * ((w + 6) * (h + 6) + w * h + 49 * 4) for n, (w, h) in zip(live, layers))
+    n3 = round(b_ref / denom) if denom else 0
+    return mac_top, [n * n3 * 49 * w * h for n, (w, h) in zip(live, layers)]
 
 
 def cpu_identity():
@@ -340,7 +374,40 @@ def main():
                        "definition": "SURVEY.md §8(d) B_pyr + B_top + B_ref of every search in the timed region "
                                      "(fpm_search_bytes, live counts of this workload) / the timed wall time"}
 
+    # the same search on the §8(d) MAC count, against the i8 MFMA peak (the top-layer NCC runs on v_dot4, the
+    # refinement correlation on the matrix cores)
+    src_wh = (sources[0].shape[1], sources[0].shape[0])
+    tmpl_wh = (templ.shape[1], templ.shape[0])
+    step_macs = 0
+    for c, ch in zip(ctxs, chunks):
+        mt, mr = search_macs(c, src_wh, tmpl_wh, len(ch))
+        step_macs += mt + sum(mr)
+    if dist is not None:
+        t = torch.tensor([float(step_macs)], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t)
+        step_macs = float(t.item())
+    search_tops = 2.0 * step_macs * args.steps / elapsed / 1e12
+    roofline_mac = {"bound": "mfma", "achieved": round(search_tops, 3), "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS",
+                    "frac": round(search_tops / I8_MFMA_PEAK_TOPS, 5),
+                    "mac_per_search": int(step_macs // (args.batch * world)),
+                    "definition": "SURVEY.md §8(d) MAC of every search in the timed region (top-layer |R_a| w_L h_L + "
+                                  "49 w_l h_l per live refinement ROI; 2 ops per MAC) / the timed wall time, vs the "
+                                  "i8 MFMA dense peak"}
+
     kern, roofline = kernel_pass(m, chunks[0], args.steps, L)
+    # the refinement correlation kernel (k_roi_corr: the layers whose template is too large for k_roi_small, the
+    # lowest ones) on its useful MACs per launch -- the banded GEMM also computes the (t, s) pairs outside the band
+    roofline_corr = None
+    if "roi_corr" in kern:
+        n_corr = kern["roi_corr"]["launches"] // args.steps
+        _, mr = search_macs(m, src_wh, tmpl_wh, len(chunks[0]))
+        if n_corr > 0:
+            corr_macs = sum(mr[len(mr) - n_corr:]) / n_corr
+            avg_s = kern["roi_corr"]["ms_total"] / kern["roi_corr"]["launches"] * 1e-3
+            tops = 2.0 * corr_macs / avg_s / 1e12
+            roofline_corr = {"bound": "mfma", "achieved": round(tops, 3), "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS",
+                             "frac": round(tops / I8_MFMA_PEAK_TOPS, 5), "kernel": "roi_corr",
+                             "avg_launch_us": round(avg_s * 1e6, 3), "useful_mac_per_launch": int(corr_macs)}
 
     searches = world * args.batch * args.steps
     value = searches / elapsed
@@ -376,6 +443,8 @@ def main():
         "kernels": kern,
         "roofline": roofline,
         "roofline_search": roofline_search,
+        "roofline_mac": roofline_mac,
+        "roofline_corr": roofline_corr,
     }
     if world == 1 and rank == 0 and args.cpu_budget > 0:
         log("[rank 0] CPU baseline (oracle restatement: 1 thread, fast-math 1 thread, all cores)")
