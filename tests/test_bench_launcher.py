@@ -34,3 +34,37 @@ def test_gpus_mismatch_is_refused():
 def test_default_is_one_rank():
     out = subprocess.run([sys.executable, BENCH, "--dry-run"], capture_output=True, text=True, timeout=60, env=_env())
     assert out.returncode == 0 and json.loads(out.stdout) == {"rank": 0, "world": 1, "local_rank": 0}
+
+
+def _bench_module():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_search_macs_follow_survey_formula():
+    """roofline_mac's MAC count: |R_a| and n_ang come back out of B_top / B_ref exactly (a fake context whose
+    stats and bytes are built from known map sizes and live counts)."""
+    b = _bench_module()
+    assert b.level_sizes(762, 521, 2) == [(762, 521), (381, 261), (191, 131)]
+    src_wh, tmpl_wh, S, L, n3 = (4024, 3036), (762, 521), 2, 6, 3
+    src, tm = b.level_sizes(*src_wh, L), b.level_sizes(*tmpl_wh, L)
+    maps = [(70, 66), (71, 64), (69, 69)]                  # per angle, per source
+    live = [60, 56, 48, 22, 22, 22]                         # batch totals entering layers L-1 .. 0
+    b_top = S * sum(src[L][0] * src[L][1] + 4 * w * h for w, h in maps)
+    layers = [tm[L - 1 - d] for d in range(L)]
+    b_ref = sum(n * n3 * ((w + 6) * (h + 6) + w * h + 49 * 4) for n, (w, h) in zip(live, layers))
+
+    class Ctx:
+        def search_stats(self):
+            return [len(maps), 99] + live
+
+        def search_bytes(self):
+            return 0, b_top, b_ref
+
+    mt, mr = b.search_macs(Ctx(), src_wh, tmpl_wh, S)
+    assert mt == S * sum(w * h for w, h in maps) * tm[L][0] * tm[L][1]
+    assert mr == [n * n3 * 49 * w * h for n, (w, h) in zip(live, layers)]
