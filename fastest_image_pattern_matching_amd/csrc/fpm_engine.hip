@@ -593,14 +593,40 @@ int enqueue_search(fpm_ctx* ctx) {
     }
     const SrcLevel& top = ctx->src[L];
     const TmplLevel& tt = ctx->tmpl[L];
+    // small canvases with the plain peak path: the whole top layer as one kernel (k_top_fused), canvas and map in
+    // LDS; FPM_TOP_FUSED=0 keeps the three-kernel form (profiling comparisons)
+    size_t fused_lds = 0;
+    if (!P.by_block && ncc_tile_fits(tt.w, tt.h) && J > 0) {
+        for (int a = 0; a < P.nang; ++a)
+            fused_lds = std::max(fused_lds, top_fused_lds(P.top[a].bw, P.top[a].bh, tt.w, tt.h));
+        static const bool off = getenv("FPM_TOP_FUSED") && atoi(getenv("FPM_TOP_FUSED")) == 0;
+        if (off || fused_lds > 64 * 1024) fused_lds = 0;
+    }
+    NmsArgs na;
+    na.jobs = P.d_jobs.as<NmsJob>(P.off_nms);
+    na.peaks = P.d_peaks.as<Peak>();
+    na.counts = P.d_counts.as<int32_t>();
+    na.tw = tt.w; na.th = tt.h; na.cap = P.cap; na.by_block = P.by_block ? 1 : 0;
+    na.mfc = ctx->prm.semantics == FPM_SEMANTICS_MFC ? 1 : 0;
+    na.thr = P.layer_score[L]; na.overlap = ctx->prm.max_overlap;
+    na.lds_blocks = 0;
+    na.cand = nullptr; na.cand_cnt = nullptr; na.cand_cap = 0; na.cand_lds = 0; na.stamps = nullptr;
+    na.skey = nullptr; na.sdone = nullptr;
+    if (fused_lds > 0) {
+        int64_t bytes = (int64_t)P.nang * top.w * top.h;
+        for (int a = 0; a < P.nang; ++a) bytes += 4LL * P.map_w[a] * P.map_h[a];
+        ProfScope ps(ctx, FPM_K_TOP_NCC, bytes * S);
+        launch_top_fused(P.d_jobs.as<WarpJob>(P.off_warp), P.d_jobs.as<NccJob>(P.off_ncc), na, J, fused_lds,
+                         P.d_livecnt.as<int32_t>(), P.nzero, st);
+    }
     // profiling bytes: each kernel's share of §8(d)'s B_top = sum_angles (W_L H_L + 4 |R_a|): the rotation reads the
     // top level, the correlation writes the map (the rotated canvases are this design's scratch)
-    {
+    if (fused_lds == 0) {
         const int64_t bytes = (int64_t)P.nang * top.w * top.h;
         ProfScope ps(ctx, FPM_K_TOP_WARP, bytes * S);
         launch_warp(P.d_jobs.as<WarpJob>(P.off_warp), J, P.max_canvas, st, P.d_livecnt.as<int32_t>(), P.nzero);
     }
-    {
+    if (fused_lds == 0) {
         int64_t bytes = 0;
         for (int a = 0; a < P.nang; ++a) bytes += 4LL * P.map_w[a] * P.map_h[a];
         ProfScope ps(ctx, FPM_K_TOP_NCC, bytes * S);
@@ -612,18 +638,8 @@ int enqueue_search(fpm_ctx* ctx) {
             launch_ncc_map(P.d_jobs.as<NccJob>(P.off_ncc), J, P.max_map, tt.w * tt.h, st);
         }
     }
-    {
+    if (fused_lds == 0) {
         ProfScope ps(ctx, FPM_K_TOP_NMS, 0);   // (reads the maps counted once in B_top)
-        NmsArgs na;
-        na.jobs = P.d_jobs.as<NmsJob>(P.off_nms);
-        na.peaks = P.d_peaks.as<Peak>();
-        na.counts = P.d_counts.as<int32_t>();
-        na.tw = tt.w; na.th = tt.h; na.cap = P.cap; na.by_block = P.by_block ? 1 : 0;
-        na.mfc = ctx->prm.semantics == FPM_SEMANTICS_MFC ? 1 : 0;
-        na.thr = P.layer_score[L]; na.overlap = ctx->prm.max_overlap;
-        na.lds_blocks = 0;
-        na.cand = nullptr; na.cand_cnt = nullptr; na.cand_cap = 0; na.cand_lds = 0; na.stamps = nullptr;
-        na.skey = nullptr; na.sdone = nullptr;
         if (P.by_block) {   // (the counts and strip keys were zeroed by k_warp)
             na.cand = P.d_ncand.as<int32_t>(); na.cand_cnt = P.d_livecnt.as<int32_t>() + L + 2; na.cand_cap = kNmsCandCap;
             na.skey = (uint64_t*)(P.d_livecnt.as<int32_t>() + P.off_skey);

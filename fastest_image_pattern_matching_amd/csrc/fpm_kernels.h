@@ -173,6 +173,11 @@ void launch_nms(const NmsArgs& a, int njobs, int max_blocks, int max_map_dim, in
                 int max_items = 0);
 int nms_block_items(int mw, int mh, int tw, int th, int mfc);
 void launch_cand_init(const CandInitArgs& a, hipStream_t st);
+// K2-K5 fused for small canvases (plain peak path): LDS bytes of one (source, angle) job, and the launch (one
+// workgroup per job; zero / nzero as launch_warp)
+size_t top_fused_lds(int bw, int bh, int tw, int th);
+void launch_top_fused(const WarpJob* wjobs, const NccJob* njobs, const NmsArgs& a, int njobs_n, size_t lds,
+                      int32_t* zero, int nzero, hipStream_t st);
 void launch_roi_tables(const RoiArgs& a, hipStream_t st);
 void launch_roi_warp(const RoiArgs& a, hipStream_t st);
 void launch_roi_corr(const RoiArgs& a, hipStream_t st);

@@ -1438,6 +1438,160 @@ void launch_cand_init(const CandInitArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_cand_init, dim3((a.total + 255) / 256), dim3(256), 0, st, b, mark);
 }
 
+// ============================================================================================== K2-K5 fused
+// The top layer of a small-canvas search (the Src7 case: ~80 x 80 canvases, a 12 x 9 template, plain
+// getNextMaxLoc) as ONE workgroup per (source, angle): the rotated canvas (k_warp's fixed-point warp, same
+// integers), its NCC map (k_ncc_tile's exact integer sums per 4 outputs by v_dot4 on funnel-shifted words, same
+// TM_CCORR rounding and f64 CCOEFF) and the peak loop (k_nms's plain path: painted rectangle + first-max argmax)
+// all in LDS -- no canvas or map round trip through HBM and two launches fewer per search.  The engine uses it when
+// the plain peak path applies and the largest canvas + map fit top_fused_lds() <= 64 KB; block 0 also zeroes the
+// search's counters (as k_warp does on the split path).  Src7, 43 sources (1763 jobs): 75.5 us per launch against
+// 106.4 for k_warp + k_ncc_tile + k_nms; ablations (abl, profiling only: 1 no taps, 2 no correlation, 4 no peak
+// loop) put 21 us in the taps, 19 in the correlation, 3 in the peak loop.
+constexpr int kTopThreads = 256;   // k_top_fused workgroup (measured: 512 threads per job no faster)
+__global__ __launch_bounds__(kTopThreads) void k_top_fused(const WarpJob* __restrict__ wjobs,
+                                                           const NccJob* __restrict__ njobs,
+                                                           NmsArgs a, int32_t* zero, int nzero, int abl) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t tf_lds[];
+    __shared__ float sv[kTopThreads / 64];
+    __shared__ int si[kTopThreads / 64];
+    const int tid = threadIdx.x;
+    if (blockIdx.x == 0)
+        for (int i = tid; i < nzero; i += kTopThreads) zero[i] = 0;
+    const WarpJob& w = wjobs[blockIdx.x];
+    const NccJob& j = njobs[blockIdx.x];
+    const int dw = w.dw, dh = w.dh, cpw = ((dw + 3) >> 2) + 1;   // canvas words per row (+1: the funnel reads)
+    const int tw = j.tw, th = j.th, ntw = (tw + 3) >> 2, ow = j.ow, oh = j.oh, n = ow * oh;
+    if (n <= 0) {   // uniform: no map for this angle (TemplateMatcher.cpp:176-178)
+        if (tid == 0) a.counts[blockIdx.x] = 0;
+        return;
+    }
+    uint32_t* Cw = tf_lds;                        // [dh][cpw] canvas, zero past dw
+    float* Mp = (float*)(Cw + dh * cpw);          // [oh][ow] map
+    uint32_t* Tw = (uint32_t*)(Mp + n);           // [th][ntw] template, zero past tw
+    uint32_t* Mw = Tw + th * ntw;                 // [ntw] byte masks of the template width
+    int32_t* tab = (int32_t*)(Mw + ntw);          // warpAffine's tables: adelta, bdelta [dw], X0, Y0 [dh]
+
+    for (int x = tid; x < dw; x += kTopThreads) {
+        tab[x] = rint_i(w.M[0] * x * kAbScale);
+        tab[dw + x] = rint_i(w.M[3] * x * kAbScale);
+    }
+    for (int y = tid; y < dh; y += kTopThreads) {
+        tab[2 * dw + y] = rint_i((w.M[1] * y + w.M[2]) * kAbScale) + kRoundDelta;
+        tab[2 * dw + dh + y] = rint_i((w.M[4] * y + w.M[5]) * kAbScale) + kRoundDelta;
+    }
+    __syncthreads();
+    // K2: the rotated canvas, four pixels (one word) per item
+    for (int i = tid; i < dh * cpw; i += kTopThreads) {
+        const int y = i / cpw, k = i - y * cpw;
+        const int X0 = tab[2 * dw + y], Y0 = tab[2 * dw + dh + y];
+        uint32_t word = 0;
+        for (int b = 0; b < 4; ++b) {   // (measured: branch-free taps with clamped loads are slower, 75 -> 80 us:
+            const int x = 4 * k + b;    // the canvas corners outside the image then load too)
+            if (x >= dw) break;
+            const int ad = tab[x], bd = tab[dw + x];
+            const int X = (X0 + ad) >> (kAbBits - kInterBits), Y = (Y0 + bd) >> (kAbBits - kInterBits);
+            word |= (uint32_t)(abl & 1 ? 0 : warp_tap(w.src, w.sw, w.sh, w.sp, X, Y, w.border)) << (8 * b);
+        }
+        Cw[i] = word;
+    }
+    for (int i = tid; i < th * ntw; i += kTopThreads) {
+        const int r = i / ntw, k = i - r * ntw;
+        uint32_t t = 0;
+        for (int b = 0; b < 4; ++b)
+            if (4 * k + b < tw) t |= (uint32_t)j.tmpl[(size_t)r * j.tp + 4 * k + b] << (8 * b);
+        Tw[i] = t;
+    }
+    if (tid < ntw) {
+        uint32_t m = 0;
+        for (int b = 0; b < 4; ++b)
+            if (4 * tid + b < tw) m |= 1u << (8 * b);
+        Mw[tid] = m;
+    }
+    __syncthreads();
+    // K3+K4: 4 adjacent outputs per item, the window sums alongside the correlation (measured: sharing them per
+    // band of rows through LDS costs the occupancy it saves in VALU, 75 -> 108 us per 43-source launch); exact u32
+    // sums (<= 128 * 64 * 255^2 < 2^32)
+    const int ngx = (ow + 3) >> 2;
+    for (int it = tid; it < oh * ngx; it += kTopThreads) {
+        if (abl & 2) { const int y = it / ngx, q = it - y * ngx; for (int u = 0; u < 4 && 4 * q + u < ow; ++u) Mp[y * ow + 4 * q + u] = 0.5f + 1e-3f * (float)((y * 7 + q * 3 + u) % 97); continue; }
+        const int y = it / ngx, q = it - y * ngx;
+        uint32_t d[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+        for (int r = 0; r < th; ++r) {
+            const uint32_t* ir = Cw + (y + r) * cpw + q;
+            const uint32_t* tr = Tw + r * ntw;
+            uint32_t w0 = ir[0];
+            for (int k = 0; k < ntw; ++k) {
+                const uint32_t w1 = ir[k + 1], t = tr[k], m = Mw[k], mff = m * 0xffu;
+                const uint32_t sh[4] = {w0, __builtin_amdgcn_alignbyte(w1, w0, 1),
+                                        __builtin_amdgcn_alignbyte(w1, w0, 2), __builtin_amdgcn_alignbyte(w1, w0, 3)};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    d[u] = __builtin_amdgcn_udot4(t, sh[u], d[u], false);
+                    s1[u] = __builtin_amdgcn_udot4(m, sh[u], s1[u], false);
+                    s2[u] = __builtin_amdgcn_udot4(sh[u] & mff, sh[u], s2[u], false);
+                }
+                w0 = w1;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int x = 4 * q + u;
+            if (x >= ow) break;
+            const double num = (double)(float)(double)(uint64_t)d[u];   // TM_CCORR's f32 result (fold == 0)
+            Mp[y * ow + x] = j.equal1 ? 1.f : ccoeff(num, (double)s1[u], (double)s2[u], j.mean, j.norm, j.inv_area);
+        }
+    }
+    __syncthreads();
+    // K5 (plain getNextMaxLoc, TemplateMatcher.cpp:197-212 / :1196-1206) on the LDS map
+    Peak* out = a.peaks + (size_t)blockIdx.x * a.cap;
+    const double ov = a.overlap;
+    float v = -INFINITY;
+    int i = INT_MAX;
+    for (int k = tid; k < n; k += kTopThreads) { const float x = Mp[k]; if (x > v) { v = x; i = k; } }
+    wg_argmax(v, i, sv, si);
+    if ((double)v < a.thr) { if (tid == 0) a.counts[blockIdx.x] = 0; return; }
+    int cnt = 0;
+    int px = i % ow, py = i / ow;
+    if (tid == 0) { out[0].x = px; out[0].y = py; out[0].score = v; }
+    ++cnt;
+    for (int itn = 0; itn < ((abl & 4) ? 0 : a.cap - 1); ++itn) {
+        const int sx = (int)(px - a.tw * (1 - ov)), sy = (int)(py - a.th * (1 - ov));
+        const int rw = (int)(2 * a.tw * (1 - ov)), rh = (int)(2 * a.th * (1 - ov));
+        if (rw > 0 && rh > 0) {
+            const int x1 = sx > 0 ? sx : 0, y1 = sy > 0 ? sy : 0;
+            const int x2 = min(sx + rw - 1, ow - 1), y2 = min(sy + rh - 1, oh - 1);
+            const int cw = x2 - x1 + 1, ch = y2 - y1 + 1;
+            if (cw > 0 && ch > 0)
+                for (int k = tid; k < cw * ch; k += kTopThreads) Mp[(y1 + k / cw) * ow + x1 + k % cw] = -1.f;
+        }
+        __syncthreads();
+        v = -INFINITY;
+        i = INT_MAX;
+        for (int k = tid; k < n; k += kTopThreads) { const float x = Mp[k]; if (x > v) { v = x; i = k; } }
+        wg_argmax(v, i, sv, si);
+        if ((double)v < a.thr) break;
+        px = i % ow;
+        py = i / ow;
+        if (tid == 0) { out[cnt].x = px; out[cnt].y = py; out[cnt].score = v; }
+        ++cnt;
+    }
+    if (tid == 0) a.counts[blockIdx.x] = cnt;
+}
+
+size_t top_fused_lds(int bw, int bh, int tw, int th) {
+    const int cpw = ((bw + 3) >> 2) + 1, ntw = (tw + 3) >> 2;
+    const size_t map = (size_t)std::max(bw - tw + 1, 0) * std::max(bh - th + 1, 0);
+    return 4 * ((size_t)bh * cpw + map + (size_t)th * ntw + ntw + 2 * ((size_t)bw + bh));
+}
+
+void launch_top_fused(const WarpJob* wjobs, const NccJob* njobs, const NmsArgs& a, int njobs_n, size_t lds,
+                      int32_t* zero, int nzero, hipStream_t st) {
+    if (njobs_n <= 0) return;
+    static const int abl = getenv("FPM_TOP_ABL") ? atoi(getenv("FPM_TOP_ABL")) : 0;   // profiling ablations only
+    hipLaunchKernelGGL(k_top_fused, dim3(njobs_n), dim3(kTopThreads), lds, st, wjobs, njobs, a, zero, nzero, abl);
+}
+
 // ============================================================================================== K6+K7+K8
 // Refinement ROIs (getRotatedROI + MatchTemplate(bUseSIMD) + minMaxLoc, TemplateMatcher.cpp:309-328), per layer
 // as four kernels over the device-compacted list of live (candidate, angle) ROIs:
