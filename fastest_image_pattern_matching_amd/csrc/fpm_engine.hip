@@ -599,7 +599,8 @@ int enqueue_search(fpm_ctx* ctx) {
     if (!P.by_block && ncc_tile_fits(tt.w, tt.h) && J > 0) {
         for (int a = 0; a < P.nang; ++a)
             fused_lds = std::max(fused_lds, top_fused_lds(P.top[a].bw, P.top[a].bh, tt.w, tt.h));
-        static const bool off = getenv("FPM_TOP_FUSED") && atoi(getenv("FPM_TOP_FUSED")) == 0;
+        const char* top_env = getenv("FPM_TOP_FUSED");   // read when the search is recorded (once per plan)
+        const bool off = top_env && atoi(top_env) == 0;
         if (off || fused_lds > 64 * 1024) fused_lds = 0;
     }
     NmsArgs na;

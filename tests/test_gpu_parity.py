@@ -140,6 +140,26 @@ def test_src7_fused_refinement(gpu_matcher_factory, templates, monkeypatch):
     assert_same_results(gpu, orc, "src7 fused")
 
 
+@pytest.mark.parametrize("top_fused", ["0", "1"])
+def test_src7_top_layer_forms(gpu_matcher_factory, templates, monkeypatch, top_fused):
+    """The top layer as one kernel (k_top_fused, default where the canvases fit LDS) and as the split
+    k_warp -> k_ncc_tile -> k_nms chain (FPM_TOP_FUSED=0, read when a fresh context records its search) on a batch
+    of two Src7 sources: both equal the oracle, result fields and per-layer live counts."""
+    monkeypatch.setenv("FPM_TOP_FUSED", top_fused)
+    t = templates["Dst7"]
+    srcs = [synth.src7_scene(t, seed=11 + i)[0] for i in range(2)]
+    m = gpu_matcher_factory(max_pos=3, tolerance_angle=180.0, score=0.7)
+    assert m.learnPattern(t)
+    m.stage(srcs)
+    got = [[r.as_tuple() for r in rr] for rr in m.match_staged()]
+    o = oracle.OracleMatcher().set(max_pos=3, tolerance_angle=180.0, score=0.7)
+    o.learnPattern(t)
+    assert got == [o.match(s) for s in srcs]
+    gpu, orc, ostats, gstats = _run_both(m, srcs[0], t, max_pos=3, tolerance_angle=180.0, score=0.7)
+    assert gstats == ostats
+    assert_same_results(gpu, orc, f"src7 top_fused={top_fused}")
+
+
 @pytest.mark.parametrize("scratch_mb", [8, 64])
 def test_refinement_rounds(gpu_matcher_factory, templates, monkeypatch, scratch_mb):
     """A capped refinement scratch (FPM_SCRATCH_MB, read when a fresh context plans its search) splits every layer's
