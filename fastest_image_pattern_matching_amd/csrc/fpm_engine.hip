@@ -584,24 +584,46 @@ int enqueue_search(fpm_ctx* ctx) {
     const int L = P.L, S = P.S, J = S * P.nang;
     hipStream_t st = ctx->stream;
     uint8_t* dsrc = ctx->d_src.as<uint8_t>();
+    const SrcLevel& top = ctx->src[L];
+    const TmplLevel& tt = ctx->tmpl[L];
+    // small canvases with the plain peak path: the whole top layer as one kernel (k_top_fused), canvas and map in
+    // LDS, when there are enough (source, angle) jobs to fill the chip: one workgroup runs a job's warp, map and
+    // peak loop serially (33 us for a single Src7 source's 41 jobs against 24 us for the three split kernels; 75.5
+    // against 106.4 us at 1763 jobs, profiles/r02_z/lat_r02_z.txt).  FPM_TOP_FUSED=0 keeps the three-kernel form,
+    // FPM_TOP_FUSED=1 forces the fused one whatever the job count (tests, profiling comparisons)
+    size_t fused_lds = 0;
+    const char* top_env = getenv("FPM_TOP_FUSED");   // read when the search is recorded (once per plan)
+    const int top_mode = top_env ? atoi(top_env) : -1;
+    if (!P.by_block && ncc_tile_fits(tt.w, tt.h) && J > 0 && (J >= kTopFusedMinJobs || top_mode == 1)) {
+        for (int a = 0; a < P.nang; ++a)
+            fused_lds = std::max(fused_lds, top_fused_lds(P.top[a].bw, P.top[a].bh, tt.w, tt.h));
+        if (top_mode == 0 || fused_lds > 64 * 1024) fused_lds = 0;
+    }
+    int32_t* live[2] = {P.d_live.as<int32_t>(), P.d_live.as<int32_t>() + P.C};
+    int32_t* livecnt = P.d_livecnt.as<int32_t>();
+    CandInitArgs ca;   // the top peaks -> candidate states and the first live list (k_cand_init, or fused in k_nms)
+    ca.peaks = P.d_peaks.as<Peak>();
+    ca.counts = P.d_counts.as<int32_t>();
+    ca.angles = P.d_top.as<TopAngle>();
+    ca.top_nodes = P.d_topn.as<AngleNode>();
+    ca.state = P.d_state.as<CandState>();
+    ca.live = live[0];
+    ca.live_count = livecnt + 0;
+    ca.nang = P.nang; ca.cap = P.cap; ca.total = P.C;
+    ca.center = P.center;
+    ca.refine = L > 0 ? (L == 1 ? 2 : 1) : 0;
+    bool cand_fused = false;
+    // the fused top layer also initialises the candidates (cand_init_job) when the peaks fit its LDS list; its
+    // live-list atomics then need the counters zeroed by an earlier launch: the first pyramid level's
+    const bool top_init = fused_lds > 0 && P.cap <= kNmsInitCap && (size_t)J * P.cap == (size_t)P.C;
+    const bool pyr_zero = top_init && L >= 1;
     // K1: source pyramid (all staged sources per launch)
     for (int l = 1; l <= L; ++l) {
         const SrcLevel& a = ctx->src[l - 1];
         const SrcLevel& b = ctx->src[l];
         ProfScope ps(ctx, FPM_K_PYR, (int64_t)S * ((int64_t)a.w * a.h + (int64_t)b.w * b.h));
-        launch_pyr_down(dsrc + a.off, a.w, a.h, a.pitch, a.img_bytes, dsrc + b.off, b.w, b.h, b.pitch, b.img_bytes, S, st);
-    }
-    const SrcLevel& top = ctx->src[L];
-    const TmplLevel& tt = ctx->tmpl[L];
-    // small canvases with the plain peak path: the whole top layer as one kernel (k_top_fused), canvas and map in
-    // LDS; FPM_TOP_FUSED=0 keeps the three-kernel form (profiling comparisons)
-    size_t fused_lds = 0;
-    if (!P.by_block && ncc_tile_fits(tt.w, tt.h) && J > 0) {
-        for (int a = 0; a < P.nang; ++a)
-            fused_lds = std::max(fused_lds, top_fused_lds(P.top[a].bw, P.top[a].bh, tt.w, tt.h));
-        const char* top_env = getenv("FPM_TOP_FUSED");   // read when the search is recorded (once per plan)
-        const bool off = top_env && atoi(top_env) == 0;
-        if (off || fused_lds > 64 * 1024) fused_lds = 0;
+        launch_pyr_down(dsrc + a.off, a.w, a.h, a.pitch, a.img_bytes, dsrc + b.off, b.w, b.h, b.pitch, b.img_bytes, S, st,
+                        0, l == 1 && pyr_zero ? P.d_livecnt.as<int32_t>() : nullptr, l == 1 && pyr_zero ? P.nzero : 0);
     }
     NmsArgs na;
     na.jobs = P.d_jobs.as<NmsJob>(P.off_nms);
@@ -618,7 +640,9 @@ int enqueue_search(fpm_ctx* ctx) {
         for (int a = 0; a < P.nang; ++a) bytes += 4LL * P.map_w[a] * P.map_h[a];
         ProfScope ps(ctx, FPM_K_TOP_NCC, bytes * S);
         launch_top_fused(P.d_jobs.as<WarpJob>(P.off_warp), P.d_jobs.as<NccJob>(P.off_ncc), na, J, fused_lds,
-                         P.d_livecnt.as<int32_t>(), P.nzero, st);
+                         pyr_zero ? nullptr : P.d_livecnt.as<int32_t>(), pyr_zero ? 0 : P.nzero, st,
+                         top_init ? &ca : nullptr);
+        cand_fused = top_init;
     }
     // profiling bytes: each kernel's share of §8(d)'s B_top = sum_angles (W_L H_L + 4 |R_a|): the rotation reads the
     // top level, the correlation writes the map (the rotated canvases are this design's scratch)
@@ -648,22 +672,11 @@ int enqueue_search(fpm_ctx* ctx) {
         }
         int mdim = 0;
         for (int a = 0; a < P.nang; ++a) mdim = std::max(mdim, std::max(P.map_w[a], P.map_h[a]));
-        launch_nms(na, J, P.max_nblk, mdim, P.max_cells, st, P.max_nitems);
+        // plain path: k_nms also initialises the candidates (the live counter was zeroed by k_warp)
+        cand_fused = !P.by_block && P.cap <= kNmsInitCap && (size_t)J * P.cap == (size_t)P.C;
+        launch_nms(na, J, P.max_nblk, mdim, P.max_cells, st, P.max_nitems, cand_fused ? &ca : nullptr);
     }
-    int32_t* live[2] = {P.d_live.as<int32_t>(), P.d_live.as<int32_t>() + P.C};
-    int32_t* livecnt = P.d_livecnt.as<int32_t>();
-    {
-        CandInitArgs ca;
-        ca.peaks = P.d_peaks.as<Peak>();
-        ca.counts = P.d_counts.as<int32_t>();
-        ca.angles = P.d_top.as<TopAngle>();
-        ca.top_nodes = P.d_topn.as<AngleNode>();
-        ca.state = P.d_state.as<CandState>();
-        ca.live = live[0];
-        ca.live_count = livecnt + 0;
-        ca.nang = P.nang; ca.cap = P.cap; ca.total = P.C;
-        ca.center = P.center;
-        ca.refine = L > 0 ? (L == 1 ? 2 : 1) : 0;
+    if (!cand_fused) {
         ProfScope ps(ctx, FPM_K_CAND_INIT, 0);
         launch_cand_init(ca, st);
     }

@@ -156,8 +156,11 @@ struct PackArgs {
 // launchers (stream-ordered, no synchronisation)
 // seg_chunks > 0 forces that many 32-row chunks per workgroup (the op entry point uses it so single images exercise
 // the carried-window path); 0 = sized for the grid
+// zero / nzero: as launch_warp (the search's first pyramid launch clears the counters when the top layer's kernel
+// also writes the live list)
 void launch_pyr_down(const uint8_t* src, int sw, int sh, int sp, size_t s_img, uint8_t* dst, int dw, int dh,
-                     int dp, size_t d_img, int nimg, hipStream_t st, int seg_chunks = 0);
+                     int dp, size_t d_img, int nimg, hipStream_t st, int seg_chunks = 0, int32_t* zero = nullptr,
+                     int nzero = 0);
 // zero / nzero: counters the search zeroes before its later kernels use them (block (0, 0) clears them), so the
 // graph carries no memset nodes
 void launch_warp(const WarpJob* jobs, int njobs, int max_pixels, hipStream_t st, int32_t* zero = nullptr,
@@ -169,15 +172,21 @@ constexpr int kNmsCandCap = 8192;   // s_BlockMax candidates (pixels >= the top-
 // max_blocks: s_BlockMax blocks of the largest map (block mode); max_map_dim: largest map width or height
 // max_cells: the largest ceil(mw / tw) * ceil(mh / th) over the maps (k_nms_greedy's coverage cells)
 // max_items: the largest nms_block_items of the maps (k_nms_blocks' grid: strip blocks are scanned in chunks)
+// ci (plain getNextMaxLoc path only, cap <= kNmsInitCap): k_nms also does k_cand_init's work for its job's
+// candidate slots (one launch fewer); the live counter must have been zeroed by an earlier launch
+constexpr int kNmsInitCap = 128;
 void launch_nms(const NmsArgs& a, int njobs, int max_blocks, int max_map_dim, int max_cells, hipStream_t st,
-                int max_items = 0);
+                int max_items = 0, const CandInitArgs* ci = nullptr);
 int nms_block_items(int mw, int mh, int tw, int th, int mfc);
 void launch_cand_init(const CandInitArgs& a, hipStream_t st);
 // K2-K5 fused for small canvases (plain peak path): LDS bytes of one (source, angle) job, and the launch (one
 // workgroup per job; zero / nzero as launch_warp)
 size_t top_fused_lds(int bw, int bh, int tw, int th);
+constexpr int kTopFusedMinJobs = 256;   // fewer jobs than CUs: the three split kernels finish sooner
+// ci (cap <= kNmsInitCap): the candidate init fused as in k_nms; the live counter must be zero before the launch
+// (zero / nzero are then 0: block 0's clearing would race with the other blocks' atomics)
 void launch_top_fused(const WarpJob* wjobs, const NccJob* njobs, const NmsArgs& a, int njobs_n, size_t lds,
-                      int32_t* zero, int nzero, hipStream_t st);
+                      int32_t* zero, int nzero, hipStream_t st, const CandInitArgs* ci = nullptr);
 void launch_roi_tables(const RoiArgs& a, hipStream_t st);
 void launch_roi_warp(const RoiArgs& a, hipStream_t st);
 void launch_roi_corr(const RoiArgs& a, hipStream_t st);

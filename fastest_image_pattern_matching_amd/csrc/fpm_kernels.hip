@@ -256,8 +256,10 @@ typedef unsigned short fpm_u16x2 __attribute__((ext_vector_type(2)));
 
 __global__ __launch_bounds__(256) void k_pyr_down_s(const uint8_t* __restrict__ src0, int sw, int sh, int sp,
                                                     size_t s_img, uint8_t* __restrict__ dst0, int dw, int dh,
-                                                    int dp, size_t d_img, int nimg) {
+                                                    int dp, size_t d_img, int nimg, int32_t* zero, int nzero) {
     __shared__ __attribute__((aligned(16))) uint8_t tin[PD_IH][PD_IW];
+    if (blockIdx.x == 0)
+        for (int i = threadIdx.x; i < nzero; i += 256) zero[i] = 0;
     __shared__ __attribute__((aligned(16))) uint16_t hs[PD_IH][PD_OW];
     // work units = (image, strip, chunk) in row-major order; workgroup w takes the contiguous range
     // [U*w/G, U*(w+1)/G) (equal shares: no tail round of a few workgroups), split where it crosses a strip; XCD
@@ -383,7 +385,7 @@ static const int kPyrWGs = [] {   // FPM_PYR_WGS: profiling override
     return e && atoi(e) > 0 ? atoi(e) : 4096;
 }();
 void launch_pyr_down(const uint8_t* src, int sw, int sh, int sp, size_t s_img, uint8_t* dst, int dw, int dh,
-                     int dp, size_t d_img, int nimg, hipStream_t st, int seg_chunks) {
+                     int dp, size_t d_img, int nimg, hipStream_t st, int seg_chunks, int32_t* zero, int nzero) {
     // equal shares of the (image, strip, chunk) units over kPyrWGs workgroups (4 rounds of 4 per CU; measured
     // 2048 / 4096 / 8192: 37.1 / 35.7 / 36.0 µs per launch averaged over the Src7 levels), or
     // seg_chunks units each
@@ -392,7 +394,7 @@ void launch_pyr_down(const uint8_t* src, int sw, int sh, int sp, size_t s_img, u
     const long units = (long)gx * chunks * nimg;
     const long g = seg_chunks > 0 ? (units + seg_chunks - 1) / seg_chunks : std::min(units, (long)kPyrWGs);
     hipLaunchKernelGGL(k_pyr_down_s, dim3((unsigned)g), dim3(256), 0, st, src, sw, sh, sp, s_img, dst, dw, dh, dp,
-                       d_img, nimg);
+                       d_img, nimg, zero, nzero);
 }
 
 // ============================================================================================== K2
@@ -861,11 +863,48 @@ __device__ __forceinline__ void block_loc_xy(const BlockGeom& g, int loc, int mw
 // s_BlockMax form when k_nms_fast's LDS cannot hold the map's blocks (block maxima from k_nms_blocks in global
 // scratch; after each painted rectangle the intersecting blocks are re-scanned one wave per block,
 // TemplateMatcher.cpp:1208-1221, DataStructures.h:215-246)
-__global__ __launch_bounds__(256) void k_nms(NmsArgs a) {
+// k_cand_init's work for the cap candidate slots of one job, done by the workgroup that found the job's cnt peaks
+// (spk, in LDS): the same CandState per slot; the job's live candidates take one contiguous range of the live list
+// (one atomic per job; the list's order never reaches a result: records are indexed by candidate id).
+// mode 1: states only (no refinement), 2: live, 3: live and the first refinement layer is layer 0.  Workgroup-
+// uniform call.
+__device__ void cand_init_job(const CandInitArgs& c, int mode, int job, int cnt, const Peak* spk, int* sbase) {
+    const int tid = threadIdx.x;
+    if (tid == 0) *sbase = (mode >= 2 && cnt > 0) ? atomicAdd(c.live_count, cnt) : 0;
+    __syncthreads();
+    const int ang = job % c.nang, base = *sbase;
+    for (int r = tid; r < c.cap; r += 256) {
+        const int id = job * c.cap + r;
+        CandState s;
+        s.lt = f2(0.f, 0.f);
+        s.node = ang;
+        s.alive = 0;
+        s.reached0 = 0;
+        s.pad = 0;
+        if (r < cnt) {
+            const Peak pk = spk[r];
+            // s_MatchParameter(Point2f(ptMaxLoc.x - fTranslationX, ...)) (TemplateMatcher.cpp:186/193/201/208),
+            // ptRotatePt2f(pt, ptCenter, -angle * D2R) (:265-266)
+            const F2 pt = f2((float)pk.x - c.angles[ang].tx, (float)pk.y - c.angles[ang].ty);
+            s.lt = rotate_pt(pt, c.center, c.top_nodes[ang].cn, c.top_nodes[ang].sn);
+            if (mode >= 2) {
+                s.alive = 1;
+                s.reached0 = mode == 3 ? 1 : 0;
+                c.live[base + r] = id;
+            }
+        }
+        c.state[id] = s;
+    }
+}
+
+// ci_mode 0: peaks only; 1-3: also the job's candidate slots (cand_init_job; plain path, cap <= kNmsInitCap)
+__global__ __launch_bounds__(256) void k_nms(NmsArgs a, CandInitArgs ci, int ci_mode) {
     __shared__ float sv[4];
     __shared__ int si[4];
     __shared__ int naff;
     __shared__ int aff[256];
+    __shared__ Peak spk[kNmsInitCap];
+    __shared__ int sbase;
     const NmsJob& j = a.jobs[blockIdx.x];
     if (a.cand && a.cand_cnt[blockIdx.x] < 0) return;   // taken by k_nms_greedy
     float* m = j.map;
@@ -878,7 +917,11 @@ __global__ __launch_bounds__(256) void k_nms(NmsArgs a) {
     const bool last = g.mfc != 0;
     float v = -INFINITY;
     int i = INT_MAX;
-    if (n <= 0) { if (tid == 0) a.counts[blockIdx.x] = 0; return; }
+    if (n <= 0) {
+        if (tid == 0) a.counts[blockIdx.x] = 0;
+        if (ci_mode) cand_init_job(ci, ci_mode, blockIdx.x, 0, spk, &sbase);
+        return;
+    }
     float* bm = j.bmax;
     int* bl = j.bloc;
     if (blocks) {
@@ -887,11 +930,18 @@ __global__ __launch_bounds__(256) void k_nms(NmsArgs a) {
         for (int k = tid; k < n; k += 256) { const float x = m[k]; if (x > v) { v = x; i = k; } }
         wg_argmax(v, i, sv, si);
     }
-    if ((double)v < a.thr) { if (tid == 0) a.counts[blockIdx.x] = 0; return; }
+    if ((double)v < a.thr) {
+        if (tid == 0) a.counts[blockIdx.x] = 0;
+        if (ci_mode) cand_init_job(ci, ci_mode, blockIdx.x, 0, spk, &sbase);
+        return;
+    }
     int cnt = 0;
     int px, py;
     block_loc_xy(g, i, mw, mh, px, py);
-    if (tid == 0) { out[0].x = px; out[0].y = py; out[0].score = v; }
+    if (tid == 0) {
+        out[0].x = px; out[0].y = py; out[0].score = v;
+        if (ci_mode) { spk[0].x = px; spk[0].y = py; spk[0].score = v; }
+    }
     ++cnt;
     for (int it = 0; it < a.cap - 1; ++it) {
         // rect of getNextMaxLoc (TemplateMatcher.cpp:1198-1201 / :1211-1214): int truncation of f64
@@ -949,10 +999,14 @@ __global__ __launch_bounds__(256) void k_nms(NmsArgs a) {
         }
         if ((double)v < a.thr) break;
         block_loc_xy(g, i, mw, mh, px, py);
-        if (tid == 0) { out[cnt].x = px; out[cnt].y = py; out[cnt].score = v; }
+        if (tid == 0) {
+            out[cnt].x = px; out[cnt].y = py; out[cnt].score = v;
+            if (ci_mode) { spk[cnt].x = px; spk[cnt].y = py; spk[cnt].score = v; }
+        }
         ++cnt;
     }
     if (tid == 0) a.counts[blockIdx.x] = cnt;
+    if (ci_mode) cand_init_job(ci, ci_mode, blockIdx.x, cnt, spk, &sbase);
 }
 
 // K5 (s_BlockMax, fast form): the same sequence of peaks as k_nms's block mode with the map left untouched.  A
@@ -1360,9 +1414,14 @@ constexpr int kNmsLdsBlocksMax = 12 * 1024;   // block maxima kept in LDS up to 
 constexpr int kNmsLdsBytes = 160 * 1024 - 4096;   // k_nms_fast dynamic LDS budget (statics take the rest)
 
 void launch_nms(const NmsArgs& a0, int njobs, int max_blocks, int max_map_dim, int max_cells, hipStream_t st,
-                int max_items) {
+                int max_items, const CandInitArgs* ci) {
     if (njobs <= 0) return;
     NmsArgs a = a0;
+    CandInitArgs cz{};
+    if (!a.by_block && ci && a.cap <= kNmsInitCap) {   // plain path with the candidate init fused
+        hipLaunchKernelGGL(k_nms, dim3(njobs), dim3(256), 0, st, a, *ci, ci->refine == 0 ? 1 : (ci->refine == 2 ? 3 : 2));
+        return;
+    }
     if (a.by_block && max_blocks > 0) {
         const int items = max_items > max_blocks ? max_items : max_blocks;
         hipLaunchKernelGGL(k_nms_blocks, dim3((items + 3) / 4 < 16384 ? (items + 3) / 4 : 16384, njobs),
@@ -1378,7 +1437,7 @@ void launch_nms(const NmsArgs& a0, int njobs, int max_blocks, int max_map_dim, i
                 hipLaunchKernelGGL(k_nms_greedy, dim3(njobs), dim3(256), nms_greedy_lds(max_cells), st, gA);
             }
             a.lds_blocks = 0;
-            hipLaunchKernelGGL(k_nms, dim3(njobs), dim3(256), 0, st, a);
+            hipLaunchKernelGGL(k_nms, dim3(njobs), dim3(256), 0, st, a, cz, 0);
             return;
         }
         const size_t fixed = nms_fast_lds(max_blocks, a.cap, 0);
@@ -1399,7 +1458,7 @@ void launch_nms(const NmsArgs& a0, int njobs, int max_blocks, int max_map_dim, i
         }
     }
     a.lds_blocks = 0;
-    hipLaunchKernelGGL(k_nms, dim3(njobs), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_nms, dim3(njobs), dim3(256), 0, st, a, cz, 0);
 }
 
 // ============================================================================================== init
@@ -1451,10 +1510,13 @@ void launch_cand_init(const CandInitArgs& a, hipStream_t st) {
 constexpr int kTopThreads = 256;   // k_top_fused workgroup (measured: 512 threads per job no faster)
 __global__ __launch_bounds__(kTopThreads) void k_top_fused(const WarpJob* __restrict__ wjobs,
                                                            const NccJob* __restrict__ njobs,
-                                                           NmsArgs a, int32_t* zero, int nzero, int abl) {
+                                                           NmsArgs a, int32_t* zero, int nzero, int abl,
+                                                           CandInitArgs ci, int ci_mode) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tf_lds[];
     __shared__ float sv[kTopThreads / 64];
     __shared__ int si[kTopThreads / 64];
+    __shared__ Peak spk[kNmsInitCap];   // ci_mode != 0: the job's peaks for cand_init_job
+    __shared__ int sbase;
     const int tid = threadIdx.x;
     if (blockIdx.x == 0)
         for (int i = tid; i < nzero; i += kTopThreads) zero[i] = 0;
@@ -1464,6 +1526,7 @@ __global__ __launch_bounds__(kTopThreads) void k_top_fused(const WarpJob* __rest
     const int tw = j.tw, th = j.th, ntw = (tw + 3) >> 2, ow = j.ow, oh = j.oh, n = ow * oh;
     if (n <= 0) {   // uniform: no map for this angle (TemplateMatcher.cpp:176-178)
         if (tid == 0) a.counts[blockIdx.x] = 0;
+        if (ci_mode) cand_init_job(ci, ci_mode, blockIdx.x, 0, spk, &sbase);
         return;
     }
     uint32_t* Cw = tf_lds;                        // [dh][cpw] canvas, zero past dw
@@ -1550,10 +1613,17 @@ __global__ __launch_bounds__(kTopThreads) void k_top_fused(const WarpJob* __rest
     int i = INT_MAX;
     for (int k = tid; k < n; k += kTopThreads) { const float x = Mp[k]; if (x > v) { v = x; i = k; } }
     wg_argmax(v, i, sv, si);
-    if ((double)v < a.thr) { if (tid == 0) a.counts[blockIdx.x] = 0; return; }
+    if ((double)v < a.thr) {
+        if (tid == 0) a.counts[blockIdx.x] = 0;
+        if (ci_mode) cand_init_job(ci, ci_mode, blockIdx.x, 0, spk, &sbase);
+        return;
+    }
     int cnt = 0;
     int px = i % ow, py = i / ow;
-    if (tid == 0) { out[0].x = px; out[0].y = py; out[0].score = v; }
+    if (tid == 0) {
+        out[0].x = px; out[0].y = py; out[0].score = v;
+        if (ci_mode) { spk[0].x = px; spk[0].y = py; spk[0].score = v; }
+    }
     ++cnt;
     for (int itn = 0; itn < ((abl & 4) ? 0 : a.cap - 1); ++itn) {
         const int sx = (int)(px - a.tw * (1 - ov)), sy = (int)(py - a.th * (1 - ov));
@@ -1573,10 +1643,14 @@ __global__ __launch_bounds__(kTopThreads) void k_top_fused(const WarpJob* __rest
         if ((double)v < a.thr) break;
         px = i % ow;
         py = i / ow;
-        if (tid == 0) { out[cnt].x = px; out[cnt].y = py; out[cnt].score = v; }
+        if (tid == 0) {
+            out[cnt].x = px; out[cnt].y = py; out[cnt].score = v;
+            if (ci_mode) { spk[cnt].x = px; spk[cnt].y = py; spk[cnt].score = v; }
+        }
         ++cnt;
     }
     if (tid == 0) a.counts[blockIdx.x] = cnt;
+    if (ci_mode) cand_init_job(ci, ci_mode, blockIdx.x, cnt, spk, &sbase);
 }
 
 size_t top_fused_lds(int bw, int bh, int tw, int th) {
@@ -1586,10 +1660,14 @@ size_t top_fused_lds(int bw, int bh, int tw, int th) {
 }
 
 void launch_top_fused(const WarpJob* wjobs, const NccJob* njobs, const NmsArgs& a, int njobs_n, size_t lds,
-                      int32_t* zero, int nzero, hipStream_t st) {
+                      int32_t* zero, int nzero, hipStream_t st, const CandInitArgs* ci) {
     if (njobs_n <= 0) return;
     static const int abl = getenv("FPM_TOP_ABL") ? atoi(getenv("FPM_TOP_ABL")) : 0;   // profiling ablations only
-    hipLaunchKernelGGL(k_top_fused, dim3(njobs_n), dim3(kTopThreads), lds, st, wjobs, njobs, a, zero, nzero, abl);
+    CandInitArgs cz{};
+    const bool fuse = ci && a.cap <= kNmsInitCap;
+    const int mode = !fuse ? 0 : (ci->refine == 0 ? 1 : (ci->refine == 2 ? 3 : 2));
+    hipLaunchKernelGGL(k_top_fused, dim3(njobs_n), dim3(kTopThreads), lds, st, wjobs, njobs, a, zero, nzero, abl,
+                       fuse ? *ci : cz, mode);
 }
 
 // ============================================================================================== K6+K7+K8

@@ -142,9 +142,9 @@ def test_src7_fused_refinement(gpu_matcher_factory, templates, monkeypatch):
 
 @pytest.mark.parametrize("top_fused", ["0", "1"])
 def test_src7_top_layer_forms(gpu_matcher_factory, templates, monkeypatch, top_fused):
-    """The top layer as one kernel (k_top_fused, default where the canvases fit LDS) and as the split
-    k_warp -> k_ncc_tile -> k_nms chain (FPM_TOP_FUSED=0, read when a fresh context records its search) on a batch
-    of two Src7 sources: both equal the oracle, result fields and per-layer live counts."""
+    """The top layer as one kernel (k_top_fused, FPM_TOP_FUSED=1 forces it below its job-count threshold) and as
+    the split k_warp -> k_ncc_tile -> k_nms chain (FPM_TOP_FUSED=0; read when a fresh context records its search) on
+    a batch of two Src7 sources and on one alone: both equal the oracle, result fields and per-layer live counts."""
     monkeypatch.setenv("FPM_TOP_FUSED", top_fused)
     t = templates["Dst7"]
     srcs = [synth.src7_scene(t, seed=11 + i)[0] for i in range(2)]
