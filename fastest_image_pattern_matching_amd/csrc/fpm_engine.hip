@@ -597,7 +597,9 @@ int enqueue_search(fpm_ctx* ctx) {
     if (!P.by_block && ncc_tile_fits(tt.w, tt.h) && J > 0 && (J >= kTopFusedMinJobs || top_mode == 1)) {
         for (int a = 0; a < P.nang; ++a)
             fused_lds = std::max(fused_lds, top_fused_lds(P.top[a].bw, P.top[a].bh, tt.w, tt.h));
-        if (top_mode == 0 || fused_lds > 64 * 1024) fused_lds = 0;
+        // <= 60 KB of dynamic LDS: with the kernel's static arrays (peaks, reduction slots) the workgroup stays within the
+        // default 64 KB launch limit
+        if (top_mode == 0 || fused_lds > 60 * 1024) fused_lds = 0;
     }
     int32_t* live[2] = {P.d_live.as<int32_t>(), P.d_live.as<int32_t>() + P.C};
     int32_t* livecnt = P.d_livecnt.as<int32_t>();

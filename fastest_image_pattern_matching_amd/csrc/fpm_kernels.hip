@@ -1503,7 +1503,7 @@ void launch_cand_init(const CandInitArgs& a, hipStream_t st) {
 // integers), its NCC map (k_ncc_tile's exact integer sums per 4 outputs by v_dot4 on funnel-shifted words, same
 // TM_CCORR rounding and f64 CCOEFF) and the peak loop (k_nms's plain path: painted rectangle + first-max argmax)
 // all in LDS -- no canvas or map round trip through HBM and two launches fewer per search.  The engine uses it when
-// the plain peak path applies and the largest canvas + map fit top_fused_lds() <= 64 KB; block 0 also zeroes the
+// the plain peak path applies and the largest canvas + map fit top_fused_lds() <= 60 KB; block 0 also zeroes the
 // search's counters (as k_warp does on the split path).  Src7, 43 sources (1763 jobs): 75.5 us per launch against
 // 106.4 for k_warp + k_ncc_tile + k_nms; ablations (abl, profiling only: 1 no taps, 2 no correlation, 4 no peak
 // loop) put 21 us in the taps, 19 in the correlation, 3 in the peak loop.
