@@ -160,6 +160,18 @@ def test_src7_top_layer_forms(gpu_matcher_factory, templates, monkeypatch, top_f
     assert_same_results(gpu, orc, f"src7 top_fused={top_fused}")
 
 
+@pytest.mark.parametrize("max_pos", [100, 150])
+def test_plain_peaks_many(hip, templates, max_pos):
+    """Plain getNextMaxLoc path (top map / template area <= 500) with ~80 peaks per map: MaxPos 100 (cap 105) runs the
+    candidate init inside k_nms from its LDS peak list, MaxPos 150 (cap 155 > kNmsInitCap) the separate
+    k_cand_init; both equal the oracle."""
+    s, t = _grid_scene(templates["Dst4"], 400, 300, 20, 6)
+    gpu, orc, ostats, gstats = _run_both(hip, s, t, max_pos=max_pos, tolerance_angle=10.0, max_overlap=0.5, score=0.6)
+    assert gstats == ostats, (gstats, ostats)
+    assert_same_results(gpu, orc, f"plain_many_{max_pos}")
+    assert ostats[1] > 400
+
+
 @pytest.mark.parametrize("scratch_mb", [8, 64])
 def test_refinement_rounds(gpu_matcher_factory, templates, monkeypatch, scratch_mb):
     """A capped refinement scratch (FPM_SCRATCH_MB, read when a fresh context plans its search) splits every layer's
