@@ -465,7 +465,12 @@ struct SearchStats {
     std::vector<int> live_per_layer;  // entering layer L-1 .. 0
     std::vector<MatchParam> top_list; // vecMatchParameter before the sort (reference push order)
     std::vector<fpm_candidate> cands; // per push-order candidate: top score, angle index, peak rank, refined pose
+    // per-layer refinement decisions (only when Matcher::trace is set; a diagnostic, no reference counterpart):
+    // rows of kTraceCols doubles = origin, layer, n3, imax, then (angle, score, mx, my, runner-up score of the
+    // map) for j = 0..2
+    std::vector<double> trace;
 };
+static const int kTraceCols = 19;
 
 class Matcher {
 public:
@@ -473,6 +478,7 @@ public:
     TemplData T;
     double last_seconds = 0.0;
     SearchStats stats;
+    bool trace = false;
 
     Matcher() { fpm_params_default(&prm); }
 
@@ -956,6 +962,7 @@ public:
                 P2f sc((spyr[l].w - 1) / 2.0f, (spyr[l].h - 1) / 2.0f);
                 int n3 = (int)a3.size();
                 std::vector<MatchParam> nm(n3);
+                double second[3] = {0, 0, 0};
                 int imax = 0;
                 double big = -1;
                 for (int j = 0; j < n3; ++j) {
@@ -966,12 +973,25 @@ public:
                     double vmax;
                     int mx, my;
                     max_loc(res, 0, 0, res.w, res.h, &vmax, &mx, &my);
+                    if (trace) {
+                        second[j] = -2;
+                        for (int k = 0; k < (int)res.px.size(); ++k)
+                            if (k != my * res.w + mx) second[j] = std::max(second[j], (double)res.px[k]);
+                    }
                     nm[j] = MatchParam(P2f((float)mx, (float)my), vmax, a3[j]);
                     if (nm[j].score > big) { imax = j; big = nm[j].score; }
                     if (mx == 0 || my == 0 || mx == res.w - 1 || my == res.h - 1) nm[j].on_border = true;
                     if (!nm[j].on_border)
                         for (int y = -1; y <= 1; ++y)
                             for (int x = -1; x <= 1; ++x) nm[j].vecResult[x + 1][y + 1] = res.at(my + y, mx + x);
+                }
+                if (trace) {
+                    double row[kTraceCols] = {(double)cand[i].origin, (double)l, (double)n3, (double)imax};
+                    for (int j = 0; j < n3; ++j) {
+                        row[4 + 5 * j] = nm[j].angle; row[5 + 5 * j] = nm[j].score;
+                        row[6 + 5 * j] = nm[j].pt.x; row[7 + 5 * j] = nm[j].pt.y; row[8 + 5 * j] = second[j];
+                    }
+                    stats.trace.insert(stats.trace.end(), row, row + kTraceCols);
                 }
                 if (nm[imax].score < layer_score[l]) break;
                 if (subpixel && l == 0 && !nm[imax].on_border && imax != 0 && imax != 2) {
@@ -1108,6 +1128,17 @@ int orc_candidates(void* h, fpm_candidate* out, int cap) {
     auto* m = (orc::Matcher*)h;
     int n = (int)m->stats.cands.size();
     for (int i = 0; i < n && i < cap; ++i) out[i] = m->stats.cands[i];
+    return n;
+}
+
+// refinement decision trace of the next matches (diagnostic): rows of 19 doubles, see SearchStats::trace
+void orc_set_trace(void* h, int on) { ((orc::Matcher*)h)->trace = on != 0; }
+int orc_trace(void* h, double* out, int cap_rows) {
+    auto* m = (orc::Matcher*)h;
+    int n = (int)(m->stats.trace.size() / orc::kTraceCols);
+    for (int i = 0; i < n && i < cap_rows; ++i)
+        std::memcpy(out + (size_t)i * orc::kTraceCols, &m->stats.trace[(size_t)i * orc::kTraceCols],
+                    sizeof(double) * orc::kTraceCols);
     return n;
 }
 

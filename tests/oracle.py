@@ -20,6 +20,9 @@ ORACLE_LIB = os.path.join(ORACLE_DIR, "build", "liboracle_fpm.so")
 ORACLE_LIB_FAST = os.path.join(ORACLE_DIR, "build", "liboracle_fpm_fast.so")
 _U8P = C.POINTER(C.c_uint8)
 _libs = {}
+TRACE_DTYPE = np.dtype([("origin", "<i4"), ("layer", "<i4"), ("n3", "<i4"), ("imax", "<i4"),
+                        ("angle", "<f8", 3), ("score", "<f8", 3), ("x", "<f8", 3), ("y", "<f8", 3),
+                        ("second", "<f8", 3)])
 
 
 def load(path: str = ORACLE_LIB):
@@ -38,6 +41,8 @@ def load(path: str = ORACLE_LIB):
     lib.orc_search_stats.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.c_int]
     lib.orc_candidates.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
     lib.orc_top_candidates.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_int]
+    lib.orc_set_trace.argtypes = [C.c_void_p, C.c_int]
+    lib.orc_trace.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_int]
     lib.orc_template_info.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     lib.orc_template_level.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
                                        C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double),
@@ -149,6 +154,24 @@ class OracleMatcher:
         out = np.zeros(n, CANDIDATE_DTYPE)
         if n:
             self._lib.orc_candidates(self._h, out.ctypes.data_as(C.c_void_p), n)
+        return out
+
+    def set_trace(self, on: bool = True):
+        self._lib.orc_set_trace(self._h, 1 if on else 0)
+        return self
+
+    def trace(self) -> np.ndarray:
+        """Refinement decisions of the last match (after set_trace): one structured row per (candidate, layer)
+        with the candidate's push-order index, the layer, the chosen angle slot and the (angle, score, x, y) of
+        each of the up to 3 angles (TemplateMatcher.cpp:279-332), plus the runner-up value of each angle's map."""
+        n = self._lib.orc_trace(self._h, None, 0)
+        buf = np.zeros((max(n, 1), 19), np.float64)
+        self._lib.orc_trace(self._h, buf.ctypes.data_as(C.POINTER(C.c_double)), n)
+        buf = buf[:n]
+        out = np.zeros(n, TRACE_DTYPE)
+        out["origin"], out["layer"], out["n3"], out["imax"] = (buf[:, k].astype(np.int32) for k in range(4))
+        for f, k in (("angle", 4), ("score", 5), ("x", 6), ("y", 7), ("second", 8)):
+            out[f] = buf[:, k:19:5]
         return out
 
     def top_candidates(self):
