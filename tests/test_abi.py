@@ -58,40 +58,3 @@ def test_library_is_gfx950_code_object():
     blob = open(_lib.LIB_PATH, "rb").read()
     assert b"gfx950" in blob
     assert b"gfx942" not in blob and b"gfx90a" not in blob
-
-
-def test_cpp_mirror_header_compiles_and_links(tmp_path, fpm_lib):
-    """include/fpm_template_matcher.hpp (C++ TemplateMatcher mirror) compiles with g++ and links libfpm_hip.so;
-    on a host without a gfx950 device its constructor throws (no CPU fallback)."""
-    import shutil
-    import subprocess
-
-    from fastest_image_pattern_matching_amd import _lib
-
-    if shutil.which("g++") is None:
-        pytest.skip("g++ not available")
-    src = tmp_path / "mirror.cpp"
-    src.write_text(r'''
-#include "fpm_template_matcher.hpp"
-#include <cstdio>
-int main() {
-    try {
-        fpm::TemplateMatcher m(0);
-        m.setToleranceAngle(180); m.setMaxPositions(3);
-        m.setAngleShard(0, 2);
-        std::vector<fpm_candidate> c = m.lastCandidates(0);
-        std::vector<fpm::SingleTargetMatch> r = m.mergeCandidates(c);
-        std::printf("device %d\n", m.getMaxPositions() + (int)r.size() * 0);
-    } catch (const std::runtime_error& e) {
-        std::printf("nodevice\n");
-    }
-    return 0;
-}
-''')
-    exe = tmp_path / "mirror"
-    libdir = os.path.dirname(_lib.LIB_PATH)
-    subprocess.check_call(["g++", "-std=c++17", "-Wall", "-Werror", "-I", os.path.join(REPO, "include"), str(src),
-                           "-o", str(exe), "-L", libdir, "-lfpm_hip", f"-Wl,-rpath,{libdir}"])
-    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
-    assert out.returncode == 0, out.stderr
-    assert out.stdout.strip() in ("nodevice", "device 3")
