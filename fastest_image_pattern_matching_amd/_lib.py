@@ -98,6 +98,7 @@ SIGNATURES = {
     "fpm_set_angle_shard": (C.c_int, [_P, C.c_int32, C.c_int32]),
     "fpm_get_angle_shard": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "fpm_last_candidates": (C.c_int, [_P, C.c_int32, C.POINTER(Candidate), C.c_int32, C.POINTER(C.c_int32)]),
+    "fpm_last_results": (C.c_int, [_P, C.POINTER(Result), C.c_int32, C.POINTER(C.c_int32)]),
     "fpm_merge_candidates": (C.c_int, [C.POINTER(Params), C.c_int32, C.c_int32, C.POINTER(Candidate), C.c_int32,
                                        C.POINTER(Result), C.c_int32, C.POINTER(C.c_int32)]),
     "fpm_search_stats": (C.c_int, [_P, C.POINTER(C.c_int64), C.c_int32]),

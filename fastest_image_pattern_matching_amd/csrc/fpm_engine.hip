@@ -171,6 +171,7 @@ struct fpm_ctx {
     fpm_params run_prm{};    // parameters of the search in flight (snapshot at launch; the host tail reads these)
     // per-source candidate records of the last search (collect_candidates; fpm_match_*candidates)
     std::vector<std::vector<fpm_candidate>> cands;
+    std::vector<std::vector<fpm_result>> results;   // of the last search, per source (fpm_last_results)
 };
 
 #define HIP_TRY(expr)                                                                   \
@@ -1344,10 +1345,10 @@ int fpm_match_staged_launch(fpm_ctx* ctx) {
 int fpm_match_staged_finish(fpm_ctx* ctx, fpm_result* out, int32_t cap, int32_t* n_results) {
     if (!ctx || !n_results) return FPM_E_INVALID_ARG;
     HIP_TRY(hipSetDevice(ctx->device));
-    std::vector<std::vector<fpm_result>> res;
-    const int rc = complete_staged(ctx, res, out != nullptr);
+    ctx->results.clear();
+    const int rc = complete_staged(ctx, ctx->results, out != nullptr);
     if (rc != FPM_OK) return rc;
-    return copy_results(res, out, cap, n_results);
+    return copy_results(ctx->results, out, cap, n_results);
 }
 
 int fpm_match_staged(fpm_ctx* ctx, fpm_result* out, int32_t cap, int32_t* n_results) {
@@ -1366,6 +1367,7 @@ int fpm_match(fpm_ctx* ctx, const uint8_t* gray, int32_t w, int32_t h, size_t st
     // a failed call leaves no stale candidate records behind (fpm_last_candidates of a sharded search)
     ctx->cands.clear();
     ctx->stats.clear();
+    ctx->results.clear();
     if (!gray || w <= 0 || h <= 0 || stride < (size_t)w) { ctx->err = "empty source"; return FPM_E_INVALID_ARG; }
     int rc = check_sizes(ctx, w, h);
     if (rc != FPM_OK) return rc;
@@ -1377,15 +1379,20 @@ int fpm_match(fpm_ctx* ctx, const uint8_t* gray, int32_t w, int32_t h, size_t st
     if (rc != FPM_OK) return rc;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     const auto t0 = std::chrono::high_resolution_clock::now();
-    std::vector<std::vector<fpm_result>> res;
-    rc = run_staged(ctx, res);
+    rc = run_staged(ctx, ctx->results);
     if (rc != FPM_OK) return rc;
     const auto t1 = std::chrono::high_resolution_clock::now();
-    const std::vector<fpm_result>& r = res[0];
+    const std::vector<fpm_result>& r = ctx->results[0];
     *n_results = (int32_t)r.size();
     if (!r.empty() && seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
     for (int i = 0; i < (int)r.size() && i < cap && out; ++i) out[i] = r[i];
     return (int)r.size() > cap ? FPM_E_CAPACITY : FPM_OK;
+}
+
+int fpm_last_results(const fpm_ctx* ctx, fpm_result* out, int32_t cap, int32_t* n_results) {
+    if (!ctx || !n_results) return FPM_E_INVALID_ARG;
+    if (ctx->pending) return FPM_E_INVALID_ARG;
+    return copy_results(ctx->results, out, cap, n_results);
 }
 
 // --- angle sharding of one search ---------------------------------------------------------

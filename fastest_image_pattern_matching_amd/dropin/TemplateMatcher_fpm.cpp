@@ -148,10 +148,9 @@ std::vector<s_SingleTargetMatch> TemplateMatcher::match(const cv::Mat& sourceIma
     double seconds = m_dLastExecutionTime;
     int rc = fpm_match(s->ctx, sourceImage.data, sourceImage.cols, sourceImage.rows, sourceImage.step[0], s->buf.data(),
                        (int32_t)s->buf.size(), &n, &seconds);
-    if (rc == FPM_E_CAPACITY) {
+    if (rc == FPM_E_CAPACITY) {   // more results than the buffer: fetch the ones just computed, no second search
         s->buf.resize((size_t)n);
-        rc = fpm_match(s->ctx, sourceImage.data, sourceImage.cols, sourceImage.rows, sourceImage.step[0], s->buf.data(),
-                       (int32_t)s->buf.size(), &n, &seconds);
+        rc = fpm_last_results(s->ctx, s->buf.data(), (int32_t)s->buf.size(), &n);
     }
     if (rc != FPM_OK) return out;
     m_dLastExecutionTime = seconds;   // unchanged by fpm_match when there is no result (:398-404)

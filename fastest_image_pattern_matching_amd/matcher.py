@@ -142,19 +142,19 @@ class TemplateMatcher:
             return []
         g = _gray(a)
         self._push()
-        while True:
+        out = (L.Result * self._cap)()
+        n = C.c_int32()
+        sec = C.c_double(self._last_time)
+        rc = self._check(self._lib.fpm_match(self._ctx, L.u8ptr(g), g.shape[1], g.shape[0], g.strides[0], out,
+                                             self._cap, C.byref(n), C.byref(sec)), "match")
+        if rc == L.FPM_E_CAPACITY:   # fetch the results already computed into a larger buffer (no second search)
+            self._cap = max(self._cap * 2, n.value)
             out = (L.Result * self._cap)()
-            n = C.c_int32()
-            sec = C.c_double(self._last_time)
-            rc = self._check(self._lib.fpm_match(self._ctx, L.u8ptr(g), g.shape[1], g.shape[0], g.strides[0], out,
-                                                 self._cap, C.byref(n), C.byref(sec)), "match")
-            if rc == L.FPM_E_CAPACITY:
-                self._cap = max(self._cap * 2, n.value)
-                continue
-            if rc != L.FPM_OK:
-                return []
-            self._last_time = sec.value
-            return [SingleTargetMatch.from_c(out[i]) for i in range(n.value)]
+            rc = self._check(self._lib.fpm_last_results(self._ctx, out, self._cap, C.byref(n)), "last_results")
+        if rc != L.FPM_OK:
+            return []
+        self._last_time = sec.value
+        return [SingleTargetMatch.from_c(out[i]) for i in range(n.value)]
 
     def match_batch(self, sources: Sequence[np.ndarray]) -> List[List[SingleTargetMatch]]:
         """Extension: all sources (same size) searched in one device pass (fpm_stage_sources + fpm_match_staged)."""
@@ -200,18 +200,18 @@ class TemplateMatcher:
 
     def match_staged_finish_array(self):
         """Wait for the launched pass and post-process it (fpm_match_staged_finish); array views as
-        match_staged_array.  On a full result buffer the search is re-run with a larger one."""
+        match_staged_array.  On a full result buffer the results already computed are fetched into a larger one
+        (fpm_last_results), without searching again."""
         n_src = self._staged
-        while True:
+        _, out, n, views = self._views(n_src)
+        rc = self._check(self._lib.fpm_match_staged_finish(self._ctx, out, self._cap, n), "match_staged_finish")
+        if rc == L.FPM_E_CAPACITY:
+            self._cap = max(self._cap * 2, max(n))
             _, out, n, views = self._views(n_src)
-            rc = self._check(self._lib.fpm_match_staged_finish(self._ctx, out, self._cap, n), "match_staged_finish")
-            if rc == L.FPM_E_CAPACITY:
-                self._cap = max(self._cap * 2, max(n))
-                self.match_staged_launch()
-                continue
-            if rc != L.FPM_OK:
-                raise RuntimeError(f"fpm_match_staged_finish failed with {rc}: {self.last_error()}")
-            return views
+            rc = self._check(self._lib.fpm_last_results(self._ctx, out, self._cap, n), "last_results")
+        if rc != L.FPM_OK:
+            raise RuntimeError(f"fpm_match_staged_finish failed with {rc}: {self.last_error()}")
+        return views
 
     # -- angle sharding of one search (fpm_set_angle_shard / fpm_last_candidates; sharding.match_angle_sharded) ----
     def setAngleShard(self, shard: int, shards: int):

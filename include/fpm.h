@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define FPM_ABI_VERSION 8
+#define FPM_ABI_VERSION 9
 
 /* status codes */
 #define FPM_OK 0
@@ -123,6 +123,11 @@ int fpm_match_staged_launch(fpm_ctx* ctx);
 /* out == NULL skips the host tail (sort, filters, conversion; n_results[s] = 0): for an angle-sharded context whose
  * candidate records (fpm_last_candidates) are merged elsewhere. */
 int fpm_match_staged_finish(fpm_ctx* ctx, fpm_result* out, int32_t cap_per_source, int32_t* n_results);
+/* The results of the last fpm_match / fpm_match_staged(_finish) call once more, laid out as fpm_match_staged's
+ * output ([sources][cap_per_source], counts in n_results[sources]; one source after fpm_match).  No reference
+ * equivalent (match() returns a growing std::vector): after FPM_E_CAPACITY the caller grows its buffer and fetches
+ * the results already computed instead of searching again. */
+int fpm_last_results(const fpm_ctx* ctx, fpm_result* out, int32_t cap_per_source, int32_t* n_results);
 
 /* --- angle sharding of one search (no reference equivalent: the reference loops over the
  * whole angle list on one thread, TemplateMatcher.cpp:157-211) ----------------------------------------------

@@ -40,7 +40,9 @@ int main(int argc, char** argv) {
     std::printf("CHECK empty_learn %d\n", m.learnPattern(cv::Mat()) ? 1 : 0);
     m.setUserDefinedRect(cv::Rect(3, 4, 50, 60));
     std::printf("CHECK rect_set %d\n", (m.hasUserDefinedRect() && m.getUserDefinedRect() == cv::Rect(3, 4, 50, 60)) ? 1 : 0);
-    // MatchToolDialog order: learn on template load (:358), the 6 setters then match on Execute (:265-286)
+    // MatchToolDialog order: learn on template load (:358) with the object's MinReduceArea at that time (the
+    // constructor's 256 before the first Execute), then on Execute the setters (:265-271, MinReduceArea included)
+    // and match (:286) -- no re-learn: match() takes its top layer from the current MinReduceArea (TemplateMatcher.cpp:120)
     std::printf("CHECK learn %d\n", m.learnPattern(tmpl) ? 1 : 0);
     std::printf("CHECK rect_reset_by_learn %d\n", m.hasUserDefinedRect() ? 0 : 1);   // m_TemplData.clear() (:51)
     m.setMaxPositions(std::atoi(argv[7]));
@@ -50,7 +52,6 @@ int main(int argc, char** argv) {
     m.setMinReduceArea(std::atoi(argv[11]));
     m.setUseSIMD(std::atoi(argv[12]) != 0);
     m.setSubPixelEstimation(std::atoi(argv[13]) != 0);
-    if (m.getMinReduceArea() != 256) m.learnPattern(tmpl);   // the UI re-learns after a MinReduceArea change
     std::vector<s_SingleTargetMatch> results = m.match(src);
     print_results("R", results);
     const double t1 = m.getLastExecutionTime();

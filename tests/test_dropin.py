@@ -82,6 +82,15 @@ EXPECTED_CHECKS = {"learned_before": 0, "empty_learn": 0, "rect_set": 1, "learn"
                    "time_positive": 1, "copy_same": 1, "again_same": 1, "none_found": 1, "time_kept": 1,
                    "rect_cleared": 1, "cleared": 1, "color_refused": 1}
 
+def _oracle_ui_sequence(t, s, p):
+    """The oracle driven as MatchToolDialog drives the class: learnPattern at template load with the constructor's
+    parameters (MinReduceArea 256, src/MatchToolDialog.cpp:358), then the setters and match on Execute (:265-286)."""
+    o = oracle.OracleMatcher()
+    assert o.learnPattern(t)
+    o.set(**p)
+    return o.match(s)
+
+
 DROPIN_CASES = {
     "dst10_multi": CASES["dst10_multi"],
     "dst5_subpixel": CASES["dst5_subpixel"],
@@ -99,20 +108,32 @@ def test_dropin_search_parity(templates, case):
     p.update(prm)
     got, checks = _run_driver(t, s, p["max_pos"], p["max_overlap"], p["score"], p["tolerance_angle"],
                               p["min_reduce_area"], p["use_simd"], p["subpixel"])
-    o = oracle.OracleMatcher().set(**p)
-    assert o.learnPattern(t)
-    exp = o.match(s)
+    exp = _oracle_ui_sequence(t, s, p)
     assert got == exp, (case, got, exp)
     assert len(got) >= 1
     assert checks == EXPECTED_CHECKS, checks
 
 
 @pytest.mark.gpu
-def test_dropin_src7_full_size(templates):
-    """BASELINE configs[1] through the C++ class: 4024x3036 Src7 surrogate, Dst7, +-180, TargetNum 3."""
+@pytest.mark.parametrize("mra", [256, 1024])
+def test_dropin_src7_full_size(templates, mra):
+    """BASELINE configs[1] through the C++ class: 4024x3036 Src7 surrogate, Dst7, +-180, TargetNum 3; also the
+    UI's learn at MinReduceArea 256 followed by an Execute at 1024 (one pyramid level fewer at match time)."""
     s, t = synth.src7_scene(templates["Dst7"])
-    got, checks = _run_driver(t, s, 3, 0.0, 0.7, 180.0)
-    o = oracle.OracleMatcher().set(max_pos=3, tolerance_angle=180.0, score=0.7)
-    assert o.learnPattern(t)
-    assert got == o.match(s) and len(got) == 3
+    got, checks = _run_driver(t, s, 3, 0.0, 0.7, 180.0, mra)
+    exp = _oracle_ui_sequence(t, s, dict(max_pos=3, tolerance_angle=180.0, score=0.7, min_reduce_area=mra))
+    assert got == exp and len(got) == 3
+    assert checks == EXPECTED_CHECKS, checks
+
+
+@pytest.mark.gpu
+def test_dropin_more_results_than_buffer(templates):
+    """437 detections (the Qt class does not cap at MaxPos): more than the drop-in's first 256-entry buffer, so the
+    rest is fetched with fpm_last_results (no second search) and still equals the oracle."""
+    from tests.cases import _grid_scene
+
+    s, t = _grid_scene(templates["Dst4"], 900, 600, 30, 11)
+    got, checks = _run_driver(t, s, 500, 0.0, 0.7, 0.0)
+    exp = _oracle_ui_sequence(t, s, dict(max_pos=500, score=0.7))
+    assert len(exp) > 256 and got == exp
     assert checks == EXPECTED_CHECKS, checks
