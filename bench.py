@@ -299,15 +299,22 @@ def main():
                           "kernels": kern, "roofline": roofline}), flush=True)
         return
     # single-search latency (host upload included) for the record, after one warm call builds the plan
-    lat_e2e = None
+    lat_e2e = lat_split = None
     if not args.skip_latency:
         m.match(sources[0])
-        lat = []
-        for _ in range(5):
+        lat, splits = [], []
+        for _ in range(9):
             t0 = time.perf_counter()
             m.match(sources[0])
             lat.append(time.perf_counter() - t0)
-        lat_e2e = float(np.median(lat))
+            splits.append(m.profile_last())
+        i = int(np.argsort(lat)[len(lat) // 2])
+        lat_e2e = lat[i]
+        dev, host, call = splits[i]
+        # fpm_profile_last: device = events around the device pass, host = the reference-order tail, call = launch to
+        # finish; the rest of the end-to-end time is the 12.2 MB host->HBM upload and the call overhead
+        lat_split = {"device": round(dev, 4), "host_tail": round(host, 4),
+                     "upload_and_call": round(lat_e2e * 1e3 - call, 4)}
     # a step launches every context's device pass, then finishes them in order, so host post-processing and the upper
     # pyramid layers' latency-bound kernels of one context overlap device work of the others
     ctxs = [m] + [TemplateMatcher(local) for _ in range(G - 1)]
@@ -323,23 +330,37 @@ def main():
 
     def run(k_steps):
         # K passes per context as a stream: each context relaunches its next pass as soon as it has finished (host
-        # post-processing) the previous one, so the device never waits for the host between steps
+        # post-processing) the previous one, so the device never waits for the host between steps.  Returns every
+        # context's last (counts, results) views (valid until that context's next pass).
+        last = [None] * len(ctxs)
         for c in ctxs:
             c.match_staged_launch()
         for k in range(k_steps):
-            for c in ctxs:
-                c.match_staged_finish_array()
+            for i, c in enumerate(ctxs):
+                last[i] = c.match_staged_finish_array()
                 if k + 1 < k_steps:
                     c.match_staged_launch()
+        return last
+
+    def verify(last):
+        """Every source's results of the last timed pass equal the reference pass's, field for field."""
+        got = []
+        for cnt, arr in last:
+            got += [[tuple(float(v) for v in arr[s_, i]) for i in range(int(cnt[s_]))] for s_ in range(len(cnt))]
+        return got == [[r.as_tuple() for r in rr] for rr in ref]
 
     run(args.warmup)
     log(f"[rank {rank}] warm; timing {args.steps} steps x {args.batch} sources over {G} context(s)")
 
     barrier_sync()
     t0 = time.perf_counter()
-    run(args.steps)   # K complete device passes + host finishes (C++) per context
+    last = run(args.steps)   # K complete device passes + host finishes (C++) per context
     barrier_sync()
     elapsed = time.perf_counter() - t0
+    # the work just timed must be the work reported: its last pass per context equals the reference pass
+    if not verify(last):
+        log(f"[rank {rank}] timed pass results differ from the reference pass")
+        sys.exit(3)
     res = ref
     dev_ms, host_ms, call_ms = m.profile_last()
     if dist is not None:
@@ -439,6 +460,10 @@ def main():
         "last_step_split_ms_ctx0": {"device": round(dev_ms, 4), "host_finish": round(host_ms, 4),
                                     "launch_to_finish": round(call_ms, 4)},
         "single_search_ms_end_to_end": round(lat_e2e * 1e3, 3) if lat_e2e is not None else None,
+        "single_search_split_ms": lat_split,
+        # the README's 76 ms is one search's latency: this ratio compares like with like (vs_baseline is throughput)
+        "vs_baseline_latency": round(README_MS_PER_SEARCH / (lat_e2e * 1e3), 2) if lat_e2e is not None else None,
+        "timed_results_verified": True,
         "matches_per_search": n_matches,
         "kernels": kern,
         "roofline": roofline,

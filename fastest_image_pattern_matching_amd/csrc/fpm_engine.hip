@@ -298,6 +298,25 @@ bool same_search_params(const fpm_params& a, const fpm_params& b) {
            a.top_angle_step == b.top_angle_step && std::equal(a.tolerance, a.tolerance + 4, b.tolerance);
 }
 
+// Input guard of the angle list (TemplateMatcher.cpp:130-144 accumulates `a += step` until the tolerance): a non-finite
+// tolerance or step, or a step so small that the list would exceed kMaxTopAngles, is refused up front (the oracle
+// applies the same rule) instead of looping without end / growing the list until memory runs out.
+constexpr double kMaxTopAngles = 100000;
+static bool angle_list_ok(const fpm_params& prm, double step, bool mfc) {
+    if (!std::isfinite(step) || step <= 0) return false;
+    auto span = [&](double lo, double hi) { return (hi - lo) / step + 2; };
+    double n;
+    if (mfc && prm.tolerance_range) {
+        for (double t : prm.tolerance)
+            if (!std::isfinite(t)) return false;
+        n = span(prm.tolerance[0], prm.tolerance[1]) + span(prm.tolerance[2], prm.tolerance[3]);
+    } else {
+        if (!std::isfinite(prm.tolerance_angle)) return false;
+        n = prm.tolerance_angle < kVisionTol ? 1 : 2 * span(0, prm.tolerance_angle);
+    }
+    return n <= kMaxTopAngles;
+}
+
 int build_plan(fpm_ctx* ctx) {
     Plan& P = ctx->plan;
     const int L = ctx->src_L;
@@ -313,6 +332,10 @@ int build_plan(fpm_ctx* ctx) {
     const double step = prm.top_angle_step > 0 ? prm.top_angle_step : std::atan(2.0 / std::max(tt.w, tt.h)) * kR2D;
     const bool mfc = prm.semantics == FPM_SEMANTICS_MFC;
     P.angles.clear();
+    if (!angle_list_ok(prm, step, mfc)) {   // the reference would loop without end or exhaust memory on these
+        ctx->err = "angle list: non-finite tolerance or step, or more than 100000 top-layer angles";
+        return FPM_E_INVALID_ARG;
+    }
     if (mfc && prm.tolerance_range) {   // MFC angle ranges (MatchToolDlg.cpp:805-815)
         const double* t = prm.tolerance;
         if (t[0] >= t[1] || t[2] >= t[3]) { ctx->err = "angle ranges need tolerance[0] < [1] and [2] < [3]"; return FPM_E_INVALID_ARG; }
@@ -598,9 +621,9 @@ int enqueue_search(fpm_ctx* ctx) {
     if (!P.by_block && ncc_tile_fits(tt.w, tt.h) && J > 0 && (J >= kTopFusedMinJobs || top_mode == 1)) {
         for (int a = 0; a < P.nang; ++a)
             fused_lds = std::max(fused_lds, top_fused_lds(P.top[a].bw, P.top[a].bh, tt.w, tt.h));
-        // <= 60 KB of dynamic LDS: with the kernel's static arrays (peaks, reduction slots) the workgroup stays within the
-        // default 64 KB launch limit
-        if (top_mode == 0 || fused_lds > 60 * 1024) fused_lds = 0;
+        // the dynamic LDS plus the kernel's static arrays (peaks, reduction slots, as compiled) within the default 64 KB
+        // launch limit (tests/test_gpu_parity.py::test_top_fused_lds_threshold runs canvases either side of it)
+        if (top_mode == 0 || fused_lds > top_fused_lds_limit()) fused_lds = 0;
     }
     int32_t* live[2] = {P.d_live.as<int32_t>(), P.d_live.as<int32_t>() + P.C};
     int32_t* livecnt = P.d_livecnt.as<int32_t>();
@@ -619,6 +642,9 @@ int enqueue_search(fpm_ctx* ctx) {
     // the fused top layer also initialises the candidates (cand_init_job) when the peaks fit its LDS list; its
     // live-list atomics then need the counters zeroed by an earlier launch: the first pyramid level's
     const bool top_init = fused_lds > 0 && P.cap <= kNmsInitCap && (size_t)J * P.cap == (size_t)P.C;
+    // L >= 1: the first pyrDown launch zeroes the counters before the top kernel's live-list atomics.  L == 0: no
+    // pyramid launch precedes it, so its block 0 zeroes them -- safe only because the candidate init then runs in
+    // mode 1 (refine == 0: states and live list written directly, no live-count atomics); launch_top_fused checks it
     const bool pyr_zero = top_init && L >= 1;
     // K1: source pyramid (all staged sources per launch)
     for (int l = 1; l <= L; ++l) {

@@ -15,7 +15,6 @@
 #include <functional>
 #include <mutex>
 #include <thread>
-#include <immintrin.h>
 
 namespace fpm {
 #ifdef FPM_HOST_STATS
@@ -44,6 +43,15 @@ static int host_threads() {
 // a caller that finds the pool busy (another context finishing on another host thread) runs its tasks inline.
 // Results never depend on which thread runs a task.
 namespace {
+// spin-wait hint: the x86 pause instruction where there is one, a scheduler yield elsewhere
+inline void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_pause();
+#else
+    std::this_thread::yield();
+#endif
+}
+
 struct Pool {
     std::mutex m, region;
     std::condition_variable cv;
@@ -61,7 +69,7 @@ struct Pool {
                     std::unique_lock<std::mutex> lk(m);
                     cv.wait(lk, [&] { return gen.load(std::memory_order_acquire) != seen; });
                 } else {
-                    _mm_pause();
+                    cpu_relax();
                 }
             }
             const std::function<void(int)>* f;
@@ -83,7 +91,9 @@ struct Pool {
     }
 };
 
-Pool* pool_instance(int workers) {   // leaked on purpose: workers block forever, nothing to tear down at exit
+// Leaked on purpose: the detached workers block forever, nothing is torn down at exit -- so libfpm_hip.so must not be
+// dlclose'd while the process lives (ctypes never unloads it; the drop-in links it)
+Pool* pool_instance(int workers) {
     static Pool* p = [&] {
         Pool* q = new Pool;
         for (int i = 0; i < workers; ++i) std::thread([q] { q->worker(); }).detach();
@@ -118,12 +128,12 @@ void host_parallel(int ntasks, const std::function<void(int)>& fn) {
         fn(t);
         p->done.fetch_add(1, std::memory_order_acq_rel);
     }
-    while (p->done.load(std::memory_order_acquire) < ntasks) _mm_pause();
+    while (p->done.load(std::memory_order_acquire) < ntasks) cpu_relax();
     {
         std::lock_guard<std::mutex> lk(p->m);
         p->fn = nullptr;   // workers that wake from here on skip this region
     }
-    while (p->active.load(std::memory_order_acquire) > 0) _mm_pause();
+    while (p->active.load(std::memory_order_acquire) > 0) cpu_relax();
 }
 
 static inline double len2(float x, float y) { return std::sqrt((double)x * x + (double)y * y); }

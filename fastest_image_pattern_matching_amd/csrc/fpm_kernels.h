@@ -182,6 +182,7 @@ void launch_cand_init(const CandInitArgs& a, hipStream_t st);
 // K2-K5 fused for small canvases (plain peak path): LDS bytes of one (source, angle) job, and the launch (one
 // workgroup per job; zero / nzero as launch_warp)
 size_t top_fused_lds(int bw, int bh, int tw, int th);
+size_t top_fused_lds_limit();   // 64 KB minus k_top_fused's static LDS (hipFuncGetAttributes, per device)
 constexpr int kTopFusedMinJobs = 256;   // fewer jobs than CUs: the three split kernels finish sooner
 // ci (cap <= kNmsInitCap): the candidate init fused as in k_nms; the live counter must be zero before the launch
 // (zero / nzero are then 0: block 0's clearing would race with the other blocks' atomics)

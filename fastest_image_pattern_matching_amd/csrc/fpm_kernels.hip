@@ -14,6 +14,8 @@
 // int32 -> f32 fold is sequential in template-row order; the normalisation is IEEE f64 in the reference's
 // operation order.  Results are bit-identical to oracle/fpm_oracle.cpp.
 #include <float.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <limits.h>
 
 #include <map>
@@ -1503,7 +1505,7 @@ void launch_cand_init(const CandInitArgs& a, hipStream_t st) {
 // integers), its NCC map (k_ncc_tile's exact integer sums per 4 outputs by v_dot4 on funnel-shifted words, same
 // TM_CCORR rounding and f64 CCOEFF) and the peak loop (k_nms's plain path: painted rectangle + first-max argmax)
 // all in LDS -- no canvas or map round trip through HBM and two launches fewer per search.  The engine uses it when
-// the plain peak path applies and the largest canvas + map fit top_fused_lds() <= 60 KB; block 0 also zeroes the
+// the plain peak path applies and the largest canvas + map fit top_fused_lds() <= top_fused_lds_limit(); block 0 zeroes the
 // search's counters (as k_warp does on the split path).  Src7, 43 sources (1763 jobs): 75.5 us per launch against
 // 106.4 for k_warp + k_ncc_tile + k_nms; ablations (abl, profiling only: 1 no taps, 2 no correlation, 4 no peak
 // loop) put 21 us in the taps, 19 in the correlation, 3 in the peak loop.
@@ -1659,6 +1661,24 @@ size_t top_fused_lds(int bw, int bh, int tw, int th) {
     return 4 * ((size_t)bh * cpw + map + (size_t)th * ntw + ntw + 2 * ((size_t)bw + bh));
 }
 
+// The dynamic LDS a k_top_fused job may use without raising the kernel's 64 KB default launch limit: 64 KB minus
+// the kernel's static LDS (peak list, reduction slots), read from the code object once per device
+size_t top_fused_lds_limit() {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    static std::mutex mu;
+    static std::map<int, size_t> lim;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = lim.find(dev);
+    if (it != lim.end()) return it->second;
+    hipFuncAttributes fa{};
+    size_t stat = 8192;   // conservative if the query fails
+    if (hipFuncGetAttributes(&fa, (const void*)k_top_fused) == hipSuccess) stat = fa.sharedSizeBytes;
+    const size_t l = stat < 65536 ? 65536 - stat : 0;
+    lim[dev] = l;
+    return l;
+}
+
 void launch_top_fused(const WarpJob* wjobs, const NccJob* njobs, const NmsArgs& a, int njobs_n, size_t lds,
                       int32_t* zero, int nzero, hipStream_t st, const CandInitArgs* ci) {
     if (njobs_n <= 0) return;
@@ -1666,6 +1686,13 @@ void launch_top_fused(const WarpJob* wjobs, const NccJob* njobs, const NmsArgs& 
     CandInitArgs cz{};
     const bool fuse = ci && a.cap <= kNmsInitCap;
     const int mode = !fuse ? 0 : (ci->refine == 0 ? 1 : (ci->refine == 2 ? 3 : 2));
+    if (fuse && zero && nzero > 0 && mode != 1) {
+        // block 0's clearing would race the other blocks' live-count atomics: the counters must be zeroed by an
+        // earlier launch (the engine passes zero = nullptr then)
+        std::fprintf(stderr, "fpm: launch_top_fused contract violated (counter zeroing with candidate-init mode %d)\n",
+                     mode);
+        std::abort();
+    }
     hipLaunchKernelGGL(k_top_fused, dim3(njobs_n), dim3(kTopThreads), lds, st, wjobs, njobs, a, zero, nzero, abl,
                        fuse ? *ci : cz, mode);
 }

@@ -864,6 +864,19 @@ public:
         double step = std::atan(2.0 / std::max(T.pyr[L].w, T.pyr[L].h)) * R2D;
         if (prm.top_angle_step > 0) step = prm.top_angle_step;   // extension (fpm.h): the top-layer step override
         const bool mfc = prm.semantics == FPM_SEMANTICS_MFC;
+        {   // input guard (no reference counterpart: it would loop without end or exhaust memory), as the engine's
+            auto span = [&](double lo, double hi) { return (hi - lo) / step + 2; };
+            bool ok = std::isfinite(step) && step > 0;
+            double n = 0;
+            if (ok && mfc && prm.tolerance_range) {
+                for (double t : prm.tolerance) ok = ok && std::isfinite(t);
+                n = span(prm.tolerance[0], prm.tolerance[1]) + span(prm.tolerance[2], prm.tolerance[3]);
+            } else if (ok) {
+                ok = std::isfinite(prm.tolerance_angle);
+                n = prm.tolerance_angle < VISION_TOLERANCE ? 1 : 2 * span(0, prm.tolerance_angle);
+            }
+            if (!ok || !(n <= 100000)) return FPM_E_INVALID_ARG;
+        }
         std::vector<double> angles;
         if (mfc && prm.tolerance_range) {   // MatchToolDlg.cpp:805-815
             const double* t = prm.tolerance;

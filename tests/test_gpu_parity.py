@@ -160,6 +160,34 @@ def test_src7_top_layer_forms(gpu_matcher_factory, templates, monkeypatch, top_f
     assert_same_results(gpu, orc, f"src7 top_fused={top_fused}")
 
 
+def test_top_fused_lds_threshold(gpu_matcher_factory, templates, monkeypatch):
+    """k_top_fused forced (FPM_TOP_FUSED=1) on top canvases either side of its LDS limit (64 KB minus the kernel's
+    static LDS, read with hipFuncGetAttributes): Dst10 at +-180 over square sources whose largest rotated top canvas
+    needs 56.5 KB (364 px) up to ~67 KB (396 px) of dynamic LDS.  Below the limit the fused kernel runs, above it the
+    engine falls back to the split top layer (no fused launch beyond the limit); every search equals the oracle."""
+    from fastest_image_pattern_matching_amd import _lib as L
+
+    monkeypatch.setenv("FPM_TOP_FUSED", "1")
+    t = templates["Dst10"]
+    fused = {}
+    for size in (364, 372, 376, 380, 388, 396):
+        s = synth.noise(size, size, 128, 10, size)
+        synth.paste_rotated(s, t, size // 2, size // 2, 30.0)
+        m = gpu_matcher_factory(max_pos=3, tolerance_angle=180.0)
+        assert m.learnPattern(t)
+        m.profile(True)
+        m.profile_reset()
+        got = [r.as_tuple() for r in m.match(s)]
+        fused[size] = m.profile_get(L.KERNEL_NAMES.index("top_warp"))[1] == 0   # the split form launches k_warp
+        m.profile(False)
+        o = oracle.OracleMatcher().set(max_pos=3, tolerance_angle=180.0)
+        assert o.learnPattern(t)
+        assert got == o.match(s), size
+    forms = [fused[k] for k in sorted(fused)]
+    assert forms[0] and not forms[-1], fused
+    assert forms == sorted(forms, reverse=True), fused   # one threshold
+
+
 @pytest.mark.parametrize("max_pos", [100, 150])
 def test_plain_peaks_many(hip, templates, max_pos):
     """Plain getNextMaxLoc path (top map / template area <= 500) with ~80 peaks per map: MaxPos 100 (cap 105) runs the
