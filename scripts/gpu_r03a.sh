@@ -1,6 +1,11 @@
+#!/bin/bash
+# Round-3 GPU pass: full GPU test suite, smoke, default bench.  usage: scripts/gpu_r03a.sh tag
+TAG=${1:-r03a}
 cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_r03a.log 2>&1; rc=$?
-tail -5 gpurun_out/pytest_gpu_r03a.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1; rc=$?
+tail -5 gpurun_out/pytest_gpu_$TAG.log
 [ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_r03a.log 2>&1 || exit $?
-tail -2 gpurun_out/smoke_r03a.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || exit $?
+tail -1 gpurun_out/smoke_$TAG.log
+timeout -k 10 400 python -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.log || exit $?
+cut -c1-600 gpurun_out/bench_$TAG.json
