@@ -2019,118 +2019,126 @@ __global__ __launch_bounds__(256) void k_roi_tables(RoiArgs a) {
     }
 }
 
-// ---- K6b: ROI sampling.  One wave = one 32x32 ROI tile: its descriptor and the lane's table entries are loaded
-// together; the tile's source footprint is staged into wave-private LDS with dword loads; every lane produces
-// 4 rows x 4 pixels by gathering the bilinear taps from LDS and stores them as dwords.  Interior tiles take a
-// branch-free path (ft_tap_interior); others follow remapBilinear's BORDER_CONSTANT(0) rules per pixel.  No
-// workgroup barrier.
-// Per-task inputs of k_roi_warp (descriptor, the lane's table entries, the source level), loaded one task ahead.
-struct WarpTask {
-    int4 dsc, A, B;
-    int X0r[4], Y0r[4];
-    const uint8_t* lvl;
-};
-__device__ __forceinline__ void warp_task_load(const RoiArgs& a, int task, int tasks, int per_roi, int txn, int RW,
-                                               int RH, int lr, int lg, WarpTask& w) {
-    if (task >= tasks) return;
-    const int slot = task / per_roi;
-    const int rem = task - slot * per_roi;
-    const int ty = rem / txn, tx = rem - ty * txn;
-    w.dsc = a.tdesc[(size_t)slot * a.tdesc_stride + rem];
-    const int32_t* t = a.tab + (size_t)slot * 2 * (a.tabw + a.tabh);
-    const int cx0 = tx * ROI_T, cx1 = min(cx0 + ROI_T, RW) - 1;
-    const int ry0 = ty * ROI_T, ry1 = min(ry0 + ROI_T, RH) - 1;
-    const int cc = min(cx0 + 4 * lg, cx1 & ~3);   // tables are read in bounds even for idle lanes
-    w.A = *(const int4*)(t + cc);
-    w.B = *(const int4*)(t + a.tabw + cc);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r = min(ry0 + lr + 8 * i, ry1);
-        w.X0r[i] = t[2 * a.tabw + r];
-        w.Y0r[i] = t[2 * a.tabw + a.tabh + r];
-    }
-    int id, jj;
-    roi_slot(a, slot, id, jj);
-    w.lvl = a.level + (size_t)(id / a.per_source) * a.level_stride;
+// ---- K6b: ROI sampling.  One wave = one 32x32 ROI tile at a time: the tile's source footprint is staged into
+// wave-private LDS with dword loads; every lane produces 4 rows x 4 pixels by gathering the bilinear taps from LDS and
+// stores them as dwords.  Interior tiles take a branch-free path; others follow remapBilinear's BORDER_CONSTANT(0)
+// rules per pixel.  No workgroup barrier.
+// The task bookkeeping is wave-uniform and stays off the VALU: each wave walks ONE contiguous run of its XCD group's
+// tile range (consecutive tiles of an ROI: neighbouring footprints), so (slot, tile row, tile column) are found by one
+// division per wave and then advanced by counting; the per-ROI data (source level, table base) is refreshed only when
+// the slot changes; footprint loads and ROI stores address a uniform base plus 32-bit lane offsets.  (Round 2's form
+// decoded every task with three integer divisions and built 64-bit addresses per lane: ~180 of the ~630 VALU
+// instructions a layer-0 tile cost, in a kernel that issue-bound.)
+// loads / stores at a wave-uniform base + a 32-bit lane byte offset (the saddr + voffset form: no 64-bit address
+// arithmetic per lane)
+template <typename T>
+__device__ __forceinline__ T ld_at(const void* base, uint32_t byte_off) {
+    return *(const T*)((const char*)base + (size_t)byte_off);
+}
+template <typename T>
+__device__ __forceinline__ void st_at(void* base, uint32_t byte_off, T v) {
+    *(T*)((char*)base + (size_t)byte_off) = v;
 }
 
-// FB: footprint rows in flight per lane (0 = LDS-DMA); ABL (profiling ablations, product 0): 1 = no footprint
-// staging, 2 = no gathers (stores zeros), 3 = tables + descriptor only, 4 = dot-product interior taps
-// (ft_tap_interior), 9 = per-wave phase cycles into a.stamps (task loads / footprint staging / gathers + stores); PF: load the next task's inputs during
-// the current task's gathers
-template <int FB, int ABL = 0, bool PF = false>
+// the footprint box of a tile: rows from lane >> 4 in steps of 4, dword column lane & 15 (< wpr), B rows in flight;
+// gsrc is the wave-uniform box origin in the source level (pitch gpitch)
+template <int B>
+__device__ __forceinline__ void stage_footprint32(uint8_t* FT, int ftw, int wpr, int fth, const uint8_t* gsrc,
+                                                  int gpitch, int lane) {
+    const int c = lane & 15;
+    if (c >= wpr) return;
+    // columns past the box read the row's pitch slack or the next row (the level images carry one spare row): those
+    // bytes land in footprint columns no tap reads (the box already holds the +2 tap margin)
+    uint32_t go = 4u * c + (uint32_t)(lane >> 4) * (uint32_t)gpitch;
+    uint32_t lo = 4u * c + (uint32_t)(lane >> 4) * (uint32_t)ftw;
+    const uint32_t gstep = 4u * gpitch, lstep = 4u * ftw;
+    for (int r0 = lane >> 4; r0 < fth; r0 += 4 * B) {
+        uint32_t v[B];
+#pragma unroll
+        for (int i = 0; i < B; ++i) v[i] = r0 + 4 * i < fth ? ld_at<uint32_t>(gsrc, go + i * gstep) : 0u;
+#pragma unroll
+        for (int i = 0; i < B; ++i)
+            if (r0 + 4 * i < fth) *(uint32_t*)(FT + lo + i * lstep) = v[i];
+        go += B * gstep;
+        lo += B * lstep;
+    }
+}
+
+// FB: footprint rows in flight per lane (0 = LDS-DMA).  ABL (profiling ablations, product 0): 1 = no footprint
+// staging, 2 = no gathers (stores zeros), 3 = tables + descriptor only, 4 = dot-product interior taps (ft_tap_interior)
+template <int FB, int ABL = 0>
 __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t ft_all[4 * ROI_FT + 16];   // + slack for ft_tap_interior
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint8_t* FT = ft_all + wv * ROI_FT;
     const int RW = a.tw + 6, RH = a.th + 6, W = a.W, H = a.H;
     const int txn = (RW + ROI_T - 1) / ROI_T, tyn = (RH + ROI_T - 1) / ROI_T;
     const int per_roi = txn * tyn;
     const int tasks = roi_count(a) * per_roi;
     const int lr = lane >> 3, lg = lane & 7;   // lane -> rows lr + 8i, columns 4*lg .. 4*lg+3
-    // XCD groups take contiguous task ranges: a tile's neighbours (overlapping footprints) and the candidate's other
-    // angle ROIs (nearly the same source region) are staged through one L2
+    // XCD groups take contiguous task ranges (a tile's neighbours and the candidate's other angle ROIs -- nearly the
+    // same source region -- are staged through one L2); inside a group every wave takes one contiguous run
     const XcdSplit xs = xcd_split(tasks);
-    const int tstride = xs.nk * 4;
-    WarpTask nxt;
-    uint64_t st_acc[3] = {0, 0, 0}, st_t = 0;   // ABL 9: per-wave cycles in task loads / staging / gathers
-    int st_n = 0;
-    if (PF) warp_task_load(a, xs.lo + xs.k * 4 + wv, xs.hi, per_roi, txn, RW, RH, lr, lg, nxt);
-    for (int task = xs.lo + xs.k * 4 + wv; task < xs.hi; task += tstride) {
-        if (ABL == 9) {   // the previous task's gathers + stores end here
-            const uint64_t t = __builtin_readcyclecounter();
-            if (st_n > 0) st_acc[2] += t - st_t;
-            st_t = t;
-            ++st_n;
+    const int nw = xs.nk * 4, w = xs.k * 4 + wv;
+    const int span = xs.hi - xs.lo;
+    const int t0 = xs.lo + (int)((int64_t)span * w / nw), t1 = xs.lo + (int)((int64_t)span * (w + 1) / nw);
+    if (t0 >= t1) return;
+    int slot = t0 / per_roi;
+    int rem = t0 - slot * per_roi;
+    int ty = rem / txn;
+    int tx = rem - ty * txn;
+    int cur = -1;
+    const int32_t* tb = nullptr;     // this ROI's warp tables
+    const uint8_t* lvl = nullptr;    // its source level
+    const uint32_t st_lane = 4u * lg + 32u * lr;   // the lane's byte offset in a 1 KB ROI tile (row lr, column 4*lg)
+    for (int task = t0; task < t1; ++task) {
+        if (slot != cur) {
+            cur = slot;
+            int id, jj;
+            roi_slot(a, slot, id, jj);
+            id = __builtin_amdgcn_readfirstlane(id);   // uniform: the division below runs on the SALU
+            lvl = a.level + (size_t)(id / a.per_source) * a.level_stride;
+            tb = a.tab + (size_t)slot * 2 * (a.tabw + a.tabh);
         }
-        const int slot = task / per_roi;
-        const int rem = task - slot * per_roi;
-        const int ty = rem / txn, tx = rem - ty * txn;
         const int cx0 = tx * ROI_T, cx1 = min(cx0 + ROI_T, RW) - 1;
         const int ry0 = ty * ROI_T, ry1 = min(ry0 + ROI_T, RH) - 1;
         const int c0 = cx0 + 4 * lg;
-        WarpTask cur;
-        if (PF) {
-            cur = nxt;
-            warp_task_load(a, task + tstride, xs.hi, per_roi, txn, RW, RH, lr, lg, nxt);
-            asm volatile("" ::: "memory");   // keep the prefetch here, ahead of this task's work
-        } else {
-            warp_task_load(a, task, xs.hi, per_roi, txn, RW, RH, lr, lg, cur);
+        const int4 dsc = a.tdesc[(size_t)slot * a.tdesc_stride + rem];
+        const int cc = min(c0, cx1 & ~3);   // tables are read in bounds even for idle lanes
+        const int4 A = ld_at<int4>(tb, 4u * cc);
+        const int4 B = ld_at<int4>(tb, 4u * (a.tabw + cc));
+        int X0r[4], Y0r[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t r = min(ry0 + lr + 8 * i, ry1);
+            X0r[i] = ld_at<int>(tb, 4u * (2 * a.tabw + r));
+            Y0r[i] = ld_at<int>(tb, 4u * (2 * a.tabw + a.tabh + r));
         }
-        const int4 dsc = cur.dsc, A = cur.A, B = cur.B;
-        const int* X0r = cur.X0r;
-        const int* Y0r = cur.Y0r;
-        const uint8_t* lvl = cur.lvl;
-        const int bxa = dsc.x, by0 = dsc.y, ftw = dsc.z & 0xffff, fth = dsc.z >> 16, flags = dsc.w;
+        uint8_t* tile = a.roi + (size_t)slot * a.roi_stride + ((size_t)rem << 10);   // tile-major: (ty, tx) = rem
+        // next task
+        ++rem;
+        if (++tx == txn) { tx = 0; ++ty; }
+        if (rem == per_roi) { rem = 0; ty = 0; tx = 0; ++slot; }
+
+        const int bxa = __builtin_amdgcn_readfirstlane(dsc.x), by0 = __builtin_amdgcn_readfirstlane(dsc.y);
+        const int dz = __builtin_amdgcn_readfirstlane(dsc.z), flags = __builtin_amdgcn_readfirstlane(dsc.w);
+        const int ftw = dz & 0xffff, fth = dz >> 16;
         const bool in_lds = (flags & kTileLds) != 0;
         const int wpr = ftw >> 2;
-        if (ABL == 9) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const uint64_t t = __builtin_readcyclecounter();
-            st_acc[0] += t - st_t;
-            st_t = t;
-        }
         wave_sync();   // previous task's gathers are done with FT
         if (ABL != 1 && ABL != 3 && (flags & kTileAny) && in_lds) {
             if constexpr (FB == 0) stage_footprint_dma(FT, wpr, fth, lvl + (size_t)by0 * a.P + bxa, a.P, lane);
-            else stage_footprint<FB>(FT, ftw, wpr, fth, lvl + (size_t)by0 * a.P + bxa, a.P, bxa, a.P, lane);
+            else stage_footprint32<FB>(FT, ftw, wpr, fth, lvl + (size_t)by0 * a.P + bxa, a.P, lane);
         }
         wave_sync();
-        if (ABL == 9) {
-            const uint64_t t = __builtin_readcyclecounter();
-            st_acc[1] += t - st_t;
-            st_t = t;
-        }
         if (c0 > cx1) continue;
         // tile-major ROI scratch: tile (ty, tx) is a contiguous 32 x 32 block, so one store instruction of the wave
         // (8 rows x 8 lanes x 4 bytes) writes 256 contiguous bytes
-        uint8_t* dst = a.roi + (size_t)slot * a.roi_stride + ((size_t)(ty * txn + tx) << 10) + 4 * lg - (size_t)ry0 * ROI_T;
         if (ABL == 3) continue;
         if (ABL == 2) {
-            for (int i = 0; i < 4; ++i) {
-                const int r = ry0 + lr + 8 * i;
-                if (r <= ry1) *(uint32_t*)(dst + (size_t)r * ROI_T) = (uint32_t)(X0r[i] ^ Y0r[i] ^ A.x ^ B.w);
-            }
+            for (int i = 0; i < 4; ++i)
+                if (ry0 + lr + 8 * i <= ry1) st_at<uint32_t>(tile, st_lane + 256u * i, (uint32_t)(X0r[i] ^ Y0r[i] ^ A.x ^ B.w));
             continue;
         }
         const int adv[4] = {A.x, A.y, A.z, A.w}, bdv[4] = {B.x, B.y, B.z, B.w};
@@ -2140,8 +2148,7 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
             const uint32_t colmask = nvalid >= 4 ? 0xffffffffu : (1u << (8 * nvalid)) - 1u;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int r = ry0 + lr + 8 * i;
-                if (r > ry1) break;
+                if (ry0 + lr + 8 * i > ry1) break;
                 uint32_t pk = 0;
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
@@ -2150,7 +2157,7 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
                     const int off = mad24(Y >> kInterBits, ftw, (X >> kInterBits) - obase);
                     pk |= (uint32_t)ft_tap_interior(FT, off, ftw, X, Y) << (8 * u);
                 }
-                *(uint32_t*)(dst + (size_t)r * ROI_T) = pk & colmask;
+                st_at<uint32_t>(tile, st_lane + 256u * i, pk & colmask);
             }
             continue;
         }
@@ -2164,7 +2171,6 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
             // past the tile repeat its last row's coordinates and are not stored)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int r = ry0 + lr + 8 * i;
                 const int x0r = X0r[i] + xo, y0r = Y0r[i] + yo;
                 uint32_t off[4];
                 int fxv[4], fyv[4], v[4][4];
@@ -2180,14 +2186,13 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
                 uint32_t pk = 0;
 #pragma unroll
                 for (int u = 0; u < 4; ++u) pk |= (uint32_t)bilerp24(v[u], fxv[u], fyv[u]) << (8 * u);
-                if (r <= ry1) *(uint32_t*)(dst + (size_t)r * ROI_T) = pk & colmask;
+                if (ry0 + lr + 8 * i <= ry1) st_at<uint32_t>(tile, st_lane + 256u * i, pk & colmask);
             }
             continue;
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int r = ry0 + lr + 8 * i;
-            if (r > ry1) break;
+            if (ry0 + lr + 8 * i > ry1) break;
             uint32_t pk = 0;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -2219,13 +2224,8 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
                 if (c0 + u >= RW) v = 0;
                 pk |= (uint32_t)v << (8 * u);
             }
-            *(uint32_t*)(dst + (size_t)r * ROI_T) = pk;
+            st_at<uint32_t>(tile, st_lane + 256u * i, pk);
         }
-    }
-    if (ABL == 9 && lane == 0 && blockIdx.x < 64) {
-        if (st_n > 0) st_acc[2] += __builtin_readcyclecounter() - st_t;
-        uint64_t* o = a.stamps + (size_t)(blockIdx.x * 4 + wv) * 4;
-        o[0] = st_acc[0]; o[1] = st_acc[1]; o[2] = st_acc[2]; o[3] = (uint64_t)st_n;
     }
 }
 

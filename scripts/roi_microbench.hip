@@ -114,27 +114,9 @@ int main(int argc, char** argv) {
         timeit([&] { hipLaunchKernelGGL(k_roi_warp<2>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 2");
         timeit([&] { hipLaunchKernelGGL(k_roi_warp<4>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 4");
         timeit([&] { hipLaunchKernelGGL(k_roi_warp<8>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 8");
-        timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 0, true>), dim3(grid), dim3(256), 0, 0, a); }, "warp prefetch b2");
-        timeit([&] { hipLaunchKernelGGL((k_roi_warp<1, 0, true>), dim3(grid), dim3(256), 0, 0, a); }, "warp prefetch b1");
         timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 1>), dim3(grid), dim3(256), 0, 0, a); }, "warp no staging");
         timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 2>), dim3(grid), dim3(256), 0, 0, a); }, "warp no gathers");
         timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 4>), dim3(grid), dim3(256), 0, 0, a); }, "warp dot4 taps");
-        {   // per-wave phase cycles of the product warp (ABL 9): first 64 workgroups
-            uint64_t* d_st;
-            CK(hipMalloc(&d_st, 256 * 4 * 8));
-            CK(hipMemset(d_st, 0, 256 * 4 * 8));
-            RoiArgs b = a;
-            b.stamps = d_st;
-            for (int rep = 0; rep < 3; ++rep) hipLaunchKernelGGL((k_roi_warp<2, 9>), dim3(grid), dim3(256), 0, 0, b);
-            CK(hipDeviceSynchronize());
-            std::vector<uint64_t> h(256 * 4);
-            CK(hipMemcpy(h.data(), d_st, h.size() * 8, hipMemcpyDeviceToHost));
-            double acc[3] = {0, 0, 0}, nt = 0;
-            for (int w = 0; w < 256; ++w) { for (int k = 0; k < 3; ++k) acc[k] += (double)h[w * 4 + k]; nt += (double)h[w * 4 + 3]; }
-            printf("warp phases (cycles per task, %0.f tasks in 256 waves): loads %.0f staging %.0f gathers+stores %.0f\n",
-                   nt, acc[0] / nt, acc[1] / nt, acc[2] / nt);
-            CK(hipFree(d_st));
-        }
         timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 3>), dim3(grid), dim3(256), 0, 0, a); }, "warp tables only");
         printf("tiles %ld\n", tiles);
     }
