@@ -1155,6 +1155,39 @@ int orc_trace(void* h, double* out, int cap_rows) {
     return n;
 }
 
+// The top layer's peak sequence on a given f32 map (TemplateMatcher.cpp:179-210; MFC MatchToolDlg.cpp:860-888):
+// s_BlockMax + getNextMaxLoc when by_block, else minMaxLoc + the painting getNextMaxLoc; at most 1 + iters peaks,
+// stopping below thr.  out: (value, x, y) per peak; returns the count.  The map is copied (it gets painted).
+int orc_peak_sequence(const float* map, int w, int h, int tw, int th, int by_block, int mfc, double overlap, int iters,
+                      double thr, double* out) {
+    orc::MatF m(w, h, 0.f);
+    std::memcpy(m.px.data(), map, sizeof(float) * (size_t)w * h);
+    int n = 0, px, py;
+    double v;
+    auto push = [&](double val, int x, int y) { out[3 * n] = val; out[3 * n + 1] = x; out[3 * n + 2] = y; ++n; };
+    if (by_block) {
+        orc::BlockMax bm(m, tw, th, mfc != 0);
+        bm.get_max(&v, &px, &py);
+        if (v < thr) return 0;
+        push(v, px, py);
+        for (int j = 0; j < iters; ++j) {
+            orc::Matcher::next_max_loc_block(m, px, py, tw, th, v, overlap, bm);
+            if (v < thr) break;
+            push(v, px, py);
+        }
+    } else {
+        orc::max_loc(m, 0, 0, w, h, &v, &px, &py);
+        if (v < thr) return 0;
+        push(v, px, py);
+        for (int j = 0; j < iters; ++j) {
+            orc::Matcher::next_max_loc(m, px, py, tw, th, v, overlap);
+            if (v < thr) break;
+            push(v, px, py);
+        }
+    }
+    return n;
+}
+
 // top-layer candidates in reference push order: (x, y, score, angle) per entry
 int orc_top_candidates(void* h, double* out, int cap) {
     auto* m = (orc::Matcher*)h;
