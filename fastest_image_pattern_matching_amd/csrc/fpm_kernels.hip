@@ -2023,12 +2023,11 @@ __global__ __launch_bounds__(256) void k_roi_tables(RoiArgs a) {
 // wave-private LDS with dword loads; every lane produces 4 rows x 4 pixels by gathering the bilinear taps from LDS and
 // stores them as dwords.  Interior tiles take a branch-free path; others follow remapBilinear's BORDER_CONSTANT(0)
 // rules per pixel.  No workgroup barrier.
-// The task bookkeeping is wave-uniform and stays off the VALU: each wave walks ONE contiguous run of its XCD group's
-// tile range (consecutive tiles of an ROI: neighbouring footprints), so (slot, tile row, tile column) are found by one
-// division per wave and then advanced by counting; the per-ROI data (source level, table base) is refreshed only when
-// the slot changes; footprint loads and ROI stores address a uniform base plus 32-bit lane offsets.  (Round 2's form
-// decoded every task with three integer divisions and built 64-bit addresses per lane: ~180 of the ~630 VALU
-// instructions a layer-0 tile cost, in a kernel that issue-bound.)
+// The task bookkeeping is wave-uniform and stays off the VALU: the task index is made uniform (readfirstlane of the
+// wave id), so its decode into (slot, tile row, tile column) and the per-ROI data (source level, table base) run on
+// the scalar unit; footprint loads and ROI stores address a uniform base plus 32-bit lane offsets.  (Round 2's form
+// decoded every task with integer divisions on the VALU and built 64-bit addresses per lane: ~180 of the ~630 VALU
+// instructions a layer-0 tile cost, in a kernel that is VALU-issue bound.)
 // loads / stores at a wave-uniform base + a 32-bit lane byte offset (the saddr + voffset form: no 64-bit address
 // arithmetic per lane)
 template <typename T>
@@ -2078,21 +2077,20 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
     const int tasks = roi_count(a) * per_roi;
     const int lr = lane >> 3, lg = lane & 7;   // lane -> rows lr + 8i, columns 4*lg .. 4*lg+3
     // XCD groups take contiguous task ranges (a tile's neighbours and the candidate's other angle ROIs -- nearly the
-    // same source region -- are staged through one L2); inside a group every wave takes one contiguous run
+    // same source region -- are staged through one L2), and inside a group the workgroups sweep that range together
+    // (task = lo + 4 k + wave, stride 4 nk): at any time the group works on one window of neighbouring tiles.
+    // (Measured: one contiguous run per wave instead loses that shared window, 241 -> 278 us per 43-source launch.)
     const XcdSplit xs = xcd_split(tasks);
-    const int nw = xs.nk * 4, w = xs.k * 4 + wv;
-    const int span = xs.hi - xs.lo;
-    const int t0 = xs.lo + (int)((int64_t)span * w / nw), t1 = xs.lo + (int)((int64_t)span * (w + 1) / nw);
-    if (t0 >= t1) return;
-    int slot = t0 / per_roi;
-    int rem = t0 - slot * per_roi;
-    int ty = rem / txn;
-    int tx = rem - ty * txn;
+    const int tstride = xs.nk * 4;
     int cur = -1;
     const int32_t* tb = nullptr;     // this ROI's warp tables
     const uint8_t* lvl = nullptr;    // its source level
     const uint32_t st_lane = 4u * lg + 32u * lr;   // the lane's byte offset in a 1 KB ROI tile (row lr, column 4*lg)
-    for (int task = t0; task < t1; ++task) {
+    for (int task = xs.lo + xs.k * 4 + wv; task < xs.hi; task += tstride) {
+        // wave-uniform, so on the scalar unit
+        const int slot = task / per_roi;
+        const int rem = task - slot * per_roi;
+        const int ty = rem / txn, tx = rem - ty * txn;
         if (slot != cur) {
             cur = slot;
             int id, jj;
@@ -2116,10 +2114,6 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
             Y0r[i] = ld_at<int>(tb, 4u * (2 * a.tabw + a.tabh + r));
         }
         uint8_t* tile = a.roi + (size_t)slot * a.roi_stride + ((size_t)rem << 10);   // tile-major: (ty, tx) = rem
-        // next task
-        ++rem;
-        if (++tx == txn) { tx = 0; ++ty; }
-        if (rem == per_roi) { rem = 0; ty = 0; tx = 0; ++slot; }
 
         const int bxa = __builtin_amdgcn_readfirstlane(dsc.x), by0 = __builtin_amdgcn_readfirstlane(dsc.y);
         const int dz = __builtin_amdgcn_readfirstlane(dsc.z), flags = __builtin_amdgcn_readfirstlane(dsc.w);
