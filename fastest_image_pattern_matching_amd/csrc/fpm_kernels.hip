@@ -2082,27 +2082,32 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
     // (Measured: one contiguous run per wave instead loses that shared window, 241 -> 278 us per 43-source launch.)
     const XcdSplit xs = xcd_split(tasks);
     const int tstride = xs.nk * 4;
-    int cur = -1;
-    const int32_t* tb = nullptr;     // this ROI's warp tables
-    const uint8_t* lvl = nullptr;    // its source level
     const uint32_t st_lane = 4u * lg + 32u * lr;   // the lane's byte offset in a 1 KB ROI tile (row lr, column 4*lg)
-    for (int task = xs.lo + xs.k * 4 + wv; task < xs.hi; task += tstride) {
+    int task = xs.lo + xs.k * 4 + wv;
+    if (task >= xs.hi) return;
+    // The next task's tile descriptor and candidate id are loaded one task ahead, during the current task's gathers:
+    // the footprint loads then start as soon as a task begins instead of after two dependent global round trips
+    // (candidate id / descriptor -> footprint address).  Wave-uniform values, carried in 5 VGPRs.
+    int4 nd;
+    int nid;
+    auto prefetch = [&](int t) {
+        const int s_ = t / per_roi;
+        nd = a.tdesc[(size_t)s_ * a.tdesc_stride + (t - s_ * per_roi)];
+        nid = a.live[(a.slot_base + s_) / a.n3];
+    };
+    prefetch(task);
+    for (; task < xs.hi; task += tstride) {
         // wave-uniform, so on the scalar unit
         const int slot = task / per_roi;
         const int rem = task - slot * per_roi;
         const int ty = rem / txn, tx = rem - ty * txn;
-        if (slot != cur) {
-            cur = slot;
-            int id, jj;
-            roi_slot(a, slot, id, jj);
-            id = __builtin_amdgcn_readfirstlane(id);   // uniform: the division below runs on the SALU
-            lvl = a.level + (size_t)(id / a.per_source) * a.level_stride;
-            tb = a.tab + (size_t)slot * 2 * (a.tabw + a.tabh);
-        }
+        const int32_t* tb = a.tab + (size_t)slot * 2 * (a.tabw + a.tabh);   // this ROI's warp tables
         const int cx0 = tx * ROI_T, cx1 = min(cx0 + ROI_T, RW) - 1;
         const int ry0 = ty * ROI_T, ry1 = min(ry0 + ROI_T, RH) - 1;
         const int c0 = cx0 + 4 * lg;
-        const int4 dsc = a.tdesc[(size_t)slot * a.tdesc_stride + rem];
+        const int4 dsc = nd;
+        const int id = __builtin_amdgcn_readfirstlane(nid);
+        const uint8_t* lvl = a.level + (size_t)(id / a.per_source) * a.level_stride;   // its source level
         const int cc = min(c0, cx1 & ~3);   // tables are read in bounds even for idle lanes
         const int4 A = ld_at<int4>(tb, 4u * cc);
         const int4 B = ld_at<int4>(tb, 4u * (a.tabw + cc));
@@ -2125,6 +2130,7 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
             if constexpr (FB == 0) stage_footprint_dma(FT, wpr, fth, lvl + (size_t)by0 * a.P + bxa, a.P, lane);
             else stage_footprint32<FB>(FT, ftw, wpr, fth, lvl + (size_t)by0 * a.P + bxa, a.P, lane);
         }
+        if (task + tstride < xs.hi) prefetch(task + tstride);
         wave_sync();
         if (c0 > cx1) continue;
         // tile-major ROI scratch: tile (ty, tx) is a contiguous 32 x 32 block, so one store instruction of the wave
@@ -2177,6 +2183,9 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) lds_taps(off[u], ftw, v[u]);
+                // keep the 16 reads together ahead of the arithmetic (the scheduler otherwise interleaves them with
+                // waits when it has registers to save: measured 241 -> 280 us per launch)
+                __builtin_amdgcn_sched_barrier(0);
                 uint32_t pk = 0;
 #pragma unroll
                 for (int u = 0; u < 4; ++u) pk |= (uint32_t)bilerp24(v[u], fxv[u], fyv[u]) << (8 * u);
@@ -3361,7 +3370,7 @@ void launch_roi_tables(const RoiArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_roi_tables, dim3(grid), dim3(256), lds, st, a);
 }
 
-constexpr int kWarpFootBatch = 2;   // footprint rows in flight per lane (measured: see DESIGN.md)
+constexpr int kWarpFootBatch = 4;   // footprint rows in flight per lane (round 3: 4 measured best, 108.6 vs 113.8 us at 2)
 void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0 || a.equal1) return;
     const long tiles = (long)a.slot_cap * ((a.th + 6 + ROI_T - 1) / ROI_T) * ((a.tw + 6 + ROI_T - 1) / ROI_T);
