@@ -131,9 +131,6 @@ __device__ __forceinline__ XcdSplit xcd_split(int n) {
     return s;
 }
 
-#ifndef FPM_FT_PITCH_FORCE
-#define FPM_FT_PITCH_FORCE 0
-#endif
 
 constexpr int PD_OW = 128, PD_OH = 32;
 constexpr int PD_IW = 2 * PD_OW + 32, PD_IH = 2 * PD_OH + 4;   // 288 x 68 bytes
@@ -1712,6 +1709,10 @@ void launch_top_fused(const WarpJob* wjobs, const NccJob* njobs, const NmsArgs& 
 constexpr int ROI_RC = kMmaRows;     // template rows per correlation chunk
 constexpr int ROI_T = 32;            // warp tile: 32 x 32 ROI pixels per wave task
 constexpr int ROI_FT = 4096;         // per-wave LDS footprint buffer (bytes) >= worst-case rotated tile bbox
+// k_roi_warp's footprint row pitch in LDS: one fixed odd number of dwords (row-strided byte gathers spread over the
+// banks) and a compile-time constant, so a tap's second row is the same ds_read's immediate offset and the byte address
+// is one multiply-add with a constant; boxes up to 16 dwords wide and ROI_FT / 68 = 60 rows stage into LDS
+constexpr int kFtPitch = 68;
 
 int roi_pick_rc(int /*tw*/, int th) { return th < ROI_RC ? th : ROI_RC; }
 
@@ -1815,6 +1816,12 @@ __device__ __forceinline__ void lds_taps(uint32_t off, int ftw, int v[4]) {
     fpm_lds_u8* p = (fpm_lds_u8*)(size_t)off;
     fpm_lds_u8* q = (fpm_lds_u8*)(size_t)(off + ftw);
     v[0] = p[0]; v[1] = p[1]; v[2] = q[0]; v[3] = q[1];
+}
+// with a compile-time pitch: all four are immediate offsets of one address
+template <int PITCH>
+__device__ __forceinline__ void lds_taps_c(uint32_t off, int v[4]) {
+    fpm_lds_u8* p = (fpm_lds_u8*)(size_t)off;
+    v[0] = p[0]; v[1] = p[1]; v[2] = p[PITCH]; v[3] = p[PITCH + 1];
 }
 // (32*h0 + fy*(h1 - h0) + 512) >> 10 with h = 32*va + fx*(vb - va), on the 24-bit multiplier only
 __device__ __forceinline__ int bilerp24(const int v[4], int fx, int fy) {
@@ -2005,15 +2012,11 @@ __global__ __launch_bounds__(256) void k_roi_tables(RoiArgs a) {
             bx1 = min(bx1 + 2, W - 1); by1 = min(by1 + 2, H - 1);
             const bool any = bx0 <= bx1 && by0 <= by1;
             const int bxa = bx0 & ~3;
-            int ftw = any ? ((bx1 - bxa + 4) & ~3) : 0;
-            if (((ftw >> 2) & 1) == 0) ftw += 4;    // odd dword pitch: spread gather banks
-#if FPM_FT_PITCH_FORCE > 0   // profiling builds only (scripts/roi_microbench.hip): a fixed pitch in dwords
-            if (any && ftw <= 4 * FPM_FT_PITCH_FORCE) ftw = 4 * FPM_FT_PITCH_FORCE;
-#endif
+            const int wpr = any ? (bx1 - bxa + 4) >> 2 : 0;   // dwords per footprint row
             const int fth = any ? by1 - by0 + 1 : 0;
-            const bool in_lds = (ftw >> 2) <= 16 && ftw * fth <= ROI_FT;
+            const bool in_lds = wpr <= 16 && kFtPitch * fth <= ROI_FT;
             a.tdesc[(size_t)slot * a.tdesc_stride + i] =
-                make_int4(bxa, by0, ftw | (fth << 16),
+                make_int4(bxa, by0, wpr | (fth << 16),
                           (any ? kTileAny : 0) | (in_lds ? kTileLds : 0) | (interior ? kTileInterior : 0));
         }
     }
@@ -2065,8 +2068,8 @@ __device__ __forceinline__ void stage_footprint32(uint8_t* FT, int ftw, int wpr,
 
 // FB: footprint rows in flight per lane (0 = LDS-DMA).  ABL (profiling ablations, product 0): 1 = no footprint
 // staging, 2 = no gathers (stores zeros), 3 = tables + descriptor only, 4 = dot-product interior taps (ft_tap_interior)
-template <int FB, int ABL = 0>
-__global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
+template <int FB, int ABL = 0, int WPE = 8>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_warp(RoiArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t ft_all[4 * ROI_FT + 16];   // + slack for ft_tap_interior
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2122,9 +2125,9 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
 
         const int bxa = __builtin_amdgcn_readfirstlane(dsc.x), by0 = __builtin_amdgcn_readfirstlane(dsc.y);
         const int dz = __builtin_amdgcn_readfirstlane(dsc.z), flags = __builtin_amdgcn_readfirstlane(dsc.w);
-        const int ftw = dz & 0xffff, fth = dz >> 16;
+        const int wpr = dz & 0xffff, fth = dz >> 16;
+        constexpr int ftw = kFtPitch;
         const bool in_lds = (flags & kTileLds) != 0;
-        const int wpr = ftw >> 2;
         wave_sync();   // previous task's gathers are done with FT
         if (ABL != 1 && ABL != 3 && (flags & kTileAny) && in_lds) {
             if constexpr (FB == 0) stage_footprint_dma(FT, wpr, fth, lvl + (size_t)by0 * a.P + bxa, a.P, lane);
@@ -2182,7 +2185,7 @@ __global__ __launch_bounds__(256) void k_roi_warp(RoiArgs a) {
                     off[u] = (uint32_t)mad24(syv >> kAbBits, ftw, sxv >> kAbBits);
                 }
 #pragma unroll
-                for (int u = 0; u < 4; ++u) lds_taps(off[u], ftw, v[u]);
+                for (int u = 0; u < 4; ++u) lds_taps_c<kFtPitch>(off[u], v[u]);
                 // keep the 16 reads together ahead of the arithmetic (the scheduler otherwise interleaves them with
                 // waits when it has registers to save: measured 241 -> 280 us per launch)
                 __builtin_amdgcn_sched_barrier(0);
