@@ -2068,7 +2068,7 @@ __device__ __forceinline__ void stage_footprint32(uint8_t* FT, int ftw, int wpr,
 
 // FB: footprint rows in flight per lane (0 = LDS-DMA).  ABL (profiling ablations, product 0): 1 = no footprint
 // staging, 2 = no gathers (stores zeros), 3 = tables + descriptor only, 4 = dot-product interior taps (ft_tap_interior)
-template <int FB, int ABL = 0, int WPE = 8>
+template <int FB, int ABL = 0, int WPE = 7>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_warp(RoiArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t ft_all[4 * ROI_FT + 16];   // + slack for ft_tap_interior
     const int lane = threadIdx.x & 63;
@@ -3373,7 +3373,9 @@ void launch_roi_tables(const RoiArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_roi_tables, dim3(grid), dim3(256), lds, st, a);
 }
 
-constexpr int kWarpFootBatch = 4;   // footprint rows in flight per lane (round 3: 4 measured best, 108.6 vs 113.8 us at 2)
+// footprint rows in flight per lane, and 7 waves per SIMD (66 VGPRs): Src7 layer-0 microbenchmark, 8 sources, round 3:
+// batch 2 / 7 waves 100.8 us, batch 4 / 7 waves 102.0, batch 4 / 8 waves (a 12-byte spill) 106.3, batch 2 / 8 waves 106.7
+constexpr int kWarpFootBatch = 2;
 void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0 || a.equal1) return;
     const long tiles = (long)a.slot_cap * ((a.th + 6 + ROI_T - 1) / ROI_T) * ((a.tw + 6 + ROI_T - 1) / ROI_T);
