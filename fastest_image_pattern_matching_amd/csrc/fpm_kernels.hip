@@ -1960,8 +1960,9 @@ __device__ __forceinline__ void stage_block4(uint8_t* dst, int dp, const uint8_t
 // ---- K6a: per-ROI fixed-point warp tables (getRotatedROI -> warpAffine's adelta/bdelta/X0/Y0) and, from them,
 // one descriptor per 32x32 ROI tile: the tile's source footprint box (corner samples +-1 px: the fixed-point map
 // is two roundings of a linear map, so every pixel's tap lies within the corners' range +-1) and flags
-// (bit0: footprint non-empty, bit1: fits the per-wave LDS buffer, bit2: every tap inside the image).
-constexpr int kTileAny = 1, kTileLds = 2, kTileInterior = 4;
+// (bit0: footprint non-empty, bit1: fits the per-wave LDS buffer, bit2: every tap inside the image) with the ROI's
+// source index above them (bits 8 and up: k_roi_warp then needs neither the candidate id nor a division per task).
+constexpr int kTileAny = 1, kTileLds = 2, kTileInterior = 4, kTileSrcShift = 8;
 int roi_tiles_for(int tw, int th) { return ((tw + 6 + ROI_T - 1) / ROI_T) * ((th + 6 + ROI_T - 1) / ROI_T); }
 
 __global__ __launch_bounds__(256) void k_roi_tables(RoiArgs a) {
@@ -1978,6 +1979,7 @@ __global__ __launch_bounds__(256) void k_roi_tables(RoiArgs a) {
         roi_slot(a, slot, id, jj);
         const CandState st = a.state[id];
         const AngleNode nd = a.nodes[st.node * a.n3 + jj];
+        const int src_bits = (id / a.per_source) << kTileSrcShift;
         double M[6];
         roi_matrix(a.W, a.H, f2(st.lt.x * 2, st.lt.y * 2), nd.c, nd.s, M);
         int32_t* t = a.tab + (size_t)slot * 2 * (a.tabw + a.tabh);
@@ -2017,7 +2019,7 @@ __global__ __launch_bounds__(256) void k_roi_tables(RoiArgs a) {
             const bool in_lds = wpr <= 16 && kFtPitch * fth <= ROI_FT;
             a.tdesc[(size_t)slot * a.tdesc_stride + i] =
                 make_int4(bxa, by0, wpr | (fth << 16),
-                          (any ? kTileAny : 0) | (in_lds ? kTileLds : 0) | (interior ? kTileInterior : 0));
+                          (any ? kTileAny : 0) | (in_lds ? kTileLds : 0) | (interior ? kTileInterior : 0) | src_bits);
         }
     }
 }
@@ -2042,32 +2044,36 @@ __device__ __forceinline__ void st_at(void* base, uint32_t byte_off, T v) {
     *(T*)((char*)base + (size_t)byte_off) = v;
 }
 
-// the footprint box of a tile: rows from lane >> 4 in steps of 4, dword column lane & 15 (< wpr), B rows in flight;
-// gsrc is the wave-uniform box origin in the source level (pitch gpitch)
-template <int B>
-__device__ __forceinline__ void stage_footprint32(uint8_t* FT, int ftw, int wpr, int fth, const uint8_t* gsrc,
-                                                  int gpitch, int lane) {
+// the footprint box of a tile: dword column lane & 15 (< wpr), rows (lane >> 4) + 4k for k < ceil(fth / 4), B rows in
+// flight; gsrc is the wave-uniform box origin in the source level (pitch gpitch).  Every condition is wave-uniform
+// (the row count per lane is ceil(fth / 4) for all lanes; a lane group whose last row lies past the box re-stages
+// row fth - 1, the same bytes to the same place), so the loop is straight-line code with scalar branches only.
+template <int B, int PITCH>
+__device__ __forceinline__ void stage_footprint32(uint8_t* FT, int wpr, int fth, const uint8_t* gsrc, int gpitch,
+                                                  int lane) {
     const int c = lane & 15;
     if (c >= wpr) return;
     // columns past the box read the row's pitch slack or the next row (the level images carry one spare row): those
     // bytes land in footprint columns no tap reads (the box already holds the +2 tap margin)
-    uint32_t go = 4u * c + (uint32_t)(lane >> 4) * (uint32_t)gpitch;
-    uint32_t lo = 4u * c + (uint32_t)(lane >> 4) * (uint32_t)ftw;
-    const uint32_t gstep = 4u * gpitch, lstep = 4u * ftw;
-    for (int r0 = lane >> 4; r0 < fth; r0 += 4 * B) {
+    const int rl = lane >> 4, rlast = fth - 1, n = (fth + 3) >> 2;
+    fpm_lds_u8* ft = (fpm_lds_u8*)(size_t)(lds_offset_of(FT) + 4u * c);
+    for (int k0 = 0; k0 < n; k0 += B) {
         uint32_t v[B];
+        int r[B];
 #pragma unroll
-        for (int i = 0; i < B; ++i) v[i] = r0 + 4 * i < fth ? ld_at<uint32_t>(gsrc, go + i * gstep) : 0u;
+        for (int i = 0; i < B; ++i) {
+            r[i] = min(rl + 4 * (k0 + i), rlast);
+            if (k0 + i < n) v[i] = ld_at<uint32_t>(gsrc, (uint32_t)mad24(r[i], gpitch, 4 * c));
+        }
 #pragma unroll
         for (int i = 0; i < B; ++i)
-            if (r0 + 4 * i < fth) *(uint32_t*)(FT + lo + i * lstep) = v[i];
-        go += B * gstep;
-        lo += B * lstep;
+            if (k0 + i < n) *(__attribute__((address_space(3))) uint32_t*)(ft + mad24(r[i], PITCH, 0)) = v[i];
     }
 }
 
 // FB: footprint rows in flight per lane (0 = LDS-DMA).  ABL (profiling ablations, product 0): 1 = no footprint
-// staging, 2 = no gathers (stores zeros), 3 = tables + descriptor only, 4 = dot-product interior taps (ft_tap_interior)
+// staging, 2 = no gathers (stores zeros), 3 = tables + descriptor only, 4 = dot-product interior taps (ft_tap_interior),
+// 5 = no ROI stores (interior rows computed, a never-true store kept), 6 = neither staging nor stores
 template <int FB, int ABL = 0, int WPE = 7>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_warp(RoiArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t ft_all[4 * ROI_FT + 16];   // + slack for ft_tap_interior
@@ -2088,15 +2094,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const uint32_t st_lane = 4u * lg + 32u * lr;   // the lane's byte offset in a 1 KB ROI tile (row lr, column 4*lg)
     int task = xs.lo + xs.k * 4 + wv;
     if (task >= xs.hi) return;
-    // The next task's tile descriptor and candidate id are loaded one task ahead, during the current task's gathers:
-    // the footprint loads then start as soon as a task begins instead of after two dependent global round trips
-    // (candidate id / descriptor -> footprint address).  Wave-uniform values, carried in 5 VGPRs.
+    // The next task's tile descriptor (footprint box, flags, source index) is loaded one task ahead, during the current
+    // task's gathers: the footprint loads then start as soon as a task begins instead of after a dependent global round
+    // trip.  Wave-uniform values, carried in 4 VGPRs.
     int4 nd;
-    int nid;
     auto prefetch = [&](int t) {
         const int s_ = t / per_roi;
         nd = a.tdesc[(size_t)s_ * a.tdesc_stride + (t - s_ * per_roi)];
-        nid = a.live[(a.slot_base + s_) / a.n3];
     };
     prefetch(task);
     for (; task < xs.hi; task += tstride) {
@@ -2109,8 +2113,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const int ry0 = ty * ROI_T, ry1 = min(ry0 + ROI_T, RH) - 1;
         const int c0 = cx0 + 4 * lg;
         const int4 dsc = nd;
-        const int id = __builtin_amdgcn_readfirstlane(nid);
-        const uint8_t* lvl = a.level + (size_t)(id / a.per_source) * a.level_stride;   // its source level
         const int cc = min(c0, cx1 & ~3);   // tables are read in bounds even for idle lanes
         const int4 A = ld_at<int4>(tb, 4u * cc);
         const int4 B = ld_at<int4>(tb, 4u * (a.tabw + cc));
@@ -2126,12 +2128,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const int bxa = __builtin_amdgcn_readfirstlane(dsc.x), by0 = __builtin_amdgcn_readfirstlane(dsc.y);
         const int dz = __builtin_amdgcn_readfirstlane(dsc.z), flags = __builtin_amdgcn_readfirstlane(dsc.w);
         const int wpr = dz & 0xffff, fth = dz >> 16;
+        const uint8_t* lvl = a.level + (size_t)(flags >> kTileSrcShift) * a.level_stride;   // its source level
         constexpr int ftw = kFtPitch;
         const bool in_lds = (flags & kTileLds) != 0;
         wave_sync();   // previous task's gathers are done with FT
-        if (ABL != 1 && ABL != 3 && (flags & kTileAny) && in_lds) {
+        if (ABL != 1 && ABL != 3 && ABL != 6 && (flags & kTileAny) && in_lds) {
             if constexpr (FB == 0) stage_footprint_dma(FT, wpr, fth, lvl + (size_t)by0 * a.P + bxa, a.P, lane);
-            else stage_footprint32<FB>(FT, ftw, wpr, fth, lvl + (size_t)by0 * a.P + bxa, a.P, lane);
+            else stage_footprint32<FB, kFtPitch>(FT, wpr, fth, lvl + (size_t)by0 * a.P + bxa, a.P, lane);
         }
         if (task + tstride < xs.hi) prefetch(task + tstride);
         wave_sync();
@@ -2192,7 +2195,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 uint32_t pk = 0;
 #pragma unroll
                 for (int u = 0; u < 4; ++u) pk |= (uint32_t)bilerp24(v[u], fxv[u], fyv[u]) << (8 * u);
-                if (ry0 + lr + 8 * i <= ry1) st_at<uint32_t>(tile, st_lane + 256u * i, pk & colmask);
+                if (ABL == 5 || ABL == 6) {
+                    if ((pk & colmask) == 0x9e3779b9u && (lane ^ bxa) == 977) st_at<uint32_t>(tile, st_lane, pk);
+                } else if (ry0 + lr + 8 * i <= ry1) {
+                    st_at<uint32_t>(tile, st_lane + 256u * i, pk & colmask);
+                }
             }
             continue;
         }
@@ -3373,16 +3380,19 @@ void launch_roi_tables(const RoiArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_roi_tables, dim3(grid), dim3(256), lds, st, a);
 }
 
-// footprint rows in flight per lane, and 7 waves per SIMD (66 VGPRs): Src7 layer-0 microbenchmark, 8 sources, round 3:
-// batch 2 / 7 waves 100.8 us, batch 4 / 7 waves 102.0, batch 4 / 8 waves (a 12-byte spill) 106.3, batch 2 / 8 waves 106.7
-constexpr int kWarpFootBatch = 2;
+// footprint rows in flight per lane and waves per SIMD: each staging round trip is one memory latency per wave, so
+// more rows in flight pay until the registers cost occupancy.  Src7 layer-0 microbenchmark at the bench's 43 sources
+// per pass (1419 ROIs, 579 K tiles): round 3 before the uniform staging loop, batch 2 509 us, 4 486, 8 479, 16 557-580
+// (5-6 waves); with it (61 VGPRs at batch 8), batch 8 at 7 waves 458, batch 4 / 8 / 12 at 8 waves 448 / 450 / 446
+// (scripts/gpu_kpass_mb.sh, profiles/r03_i)
+constexpr int kWarpFootBatch = 12, kWarpWaves = 8;
 void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0 || a.equal1) return;
     const long tiles = (long)a.slot_cap * ((a.th + 6 + ROI_T - 1) / ROI_T) * ((a.tw + 6 + ROI_T - 1) / ROI_T);
     if (tiles > INT_MAX) return;   // the engine bounds slot_cap far below this
     const long want = (tiles + 3) / 4;
     const int grid = (int)(want < 16384 ? want : 16384);
-    hipLaunchKernelGGL(k_roi_warp<kWarpFootBatch>, dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((k_roi_warp<kWarpFootBatch, 0, kWarpWaves>), dim3(grid), dim3(256), 0, st, a);
 }
 
 constexpr size_t kLdsPerCu = 160 * 1024;   // MI355X (gfx950) LDS per CU

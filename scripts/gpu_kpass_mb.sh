@@ -10,7 +10,7 @@ if [ -n "$2" ]; then
   tail -2 $OUT/pytest_gpu_$TAG.log
   [ $rc -ne 0 ] && exit $rc
 fi
-MB_WARP_ONLY=1 timeout -k 10 120 ./build/roi_mb 20 > $OUT/mb_$TAG.txt 2>&1 || exit $?
+MB_NSRC=${MB_NSRC:-43} MB_WARP_ONLY=1 timeout -k 10 120 ./build/roi_mb 20 > $OUT/mb_$TAG.txt 2>&1 || exit $?
 cat $OUT/mb_$TAG.txt
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o run --output-format csv -- python3 $ROOT/bench.py --kernel-pass-only --steps 50 > $OUT/kpass_$TAG.json 2> $OUT/kpass_$TAG.log || exit $?
 cd $ROOT

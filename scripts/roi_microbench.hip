@@ -110,20 +110,21 @@ int main(int argc, char** argv) {
         const long tiles = (long)a.slot_cap * ((TH + 6 + 31) / 32) * ((TW + 6 + 31) / 32);
         const int grid = (int)std::min<long>((tiles + 3) / 4, 16384);
         timeit([&] { hipLaunchKernelGGL(k_roi_warp<0>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot LDS-DMA");
-        timeit([&] { hipLaunchKernelGGL(k_roi_warp<1>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 1");
         timeit([&] { hipLaunchKernelGGL(k_roi_warp<2>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 2");
         timeit([&] { hipLaunchKernelGGL(k_roi_warp<4>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 4");
         timeit([&] { hipLaunchKernelGGL(k_roi_warp<8>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 8");
-        for (int rep = 0; rep < 2; ++rep) {
-            timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 0, 7>), dim3(grid), dim3(256), 0, 0, a); }, "warp b2 7 waves");
-            timeit([&] { hipLaunchKernelGGL((k_roi_warp<4, 0, 7>), dim3(grid), dim3(256), 0, 0, a); }, "warp b4 7 waves");
-            timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 0, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp b2 8 waves");
+        timeit([&] { hipLaunchKernelGGL(k_roi_warp<12>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 12");
+        if (!getenv("MB_SHORT")) {
             timeit([&] { hipLaunchKernelGGL((k_roi_warp<4, 0, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp b4 8 waves");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp<8, 0, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp b8 8 waves");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 0, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp b12 8 waves");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp<8, 5>), dim3(grid), dim3(256), 0, 0, a); }, "warp no stores");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp<8, 6>), dim3(grid), dim3(256), 0, 0, a); }, "warp gathers only");
         }
-        timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 1>), dim3(grid), dim3(256), 0, 0, a); }, "warp no staging");
-        timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 2>), dim3(grid), dim3(256), 0, 0, a); }, "warp no gathers");
-        timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 4>), dim3(grid), dim3(256), 0, 0, a); }, "warp dot4 taps");
-        timeit([&] { hipLaunchKernelGGL((k_roi_warp<2, 3>), dim3(grid), dim3(256), 0, 0, a); }, "warp tables only");
+        timeit([&] { hipLaunchKernelGGL((k_roi_warp<8, 1>), dim3(grid), dim3(256), 0, 0, a); }, "warp no staging");
+        timeit([&] { hipLaunchKernelGGL((k_roi_warp<8, 2>), dim3(grid), dim3(256), 0, 0, a); }, "warp no gathers");
+        timeit([&] { hipLaunchKernelGGL((k_roi_warp<8, 4>), dim3(grid), dim3(256), 0, 0, a); }, "warp dot4 taps");
+        timeit([&] { hipLaunchKernelGGL((k_roi_warp<8, 3>), dim3(grid), dim3(256), 0, 0, a); }, "warp tables only");
         printf("tiles %ld\n", tiles);
     }
     if (envi("MB_WARP_ONLY", 0)) return 0;
