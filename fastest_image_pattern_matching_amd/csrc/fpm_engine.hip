@@ -470,7 +470,7 @@ int build_plan(fpm_ctx* ctx) {
         }
         P.roi_pitch = roi_pitch_for(max_w);
         P.tabw = P.roi_pitch;
-        P.tabh = round_up((int)max_rows + 6, 4);
+        P.tabh = roi_tab_rows((int)max_rows);
         P.roi_stride = 0;
         for (int l = 0; l < L; ++l)
             P.roi_stride = std::max(P.roi_stride, roi_tiles_bytes(ctx->tmpl[l].w, ctx->tmpl[l].h));
@@ -731,7 +731,7 @@ int enqueue_search(fpm_ctx* ctx) {
         ra.state = P.d_state.as<CandState>();
         ra.nodes = P.d_nodes.as<AngleNode>() + P.node_off[d];
         // per-level scratch geometry (the buffers are sized for the largest level)
-        ra.tab = P.d_tab.as<int32_t>(); ra.tabw = roi_pitch_for(tl.w); ra.tabh = round_up(tl.h + 6, 4);
+        ra.tab = P.d_tab.as<int32_t>(); ra.tabw = roi_pitch_for(tl.w); ra.tabh = roi_tab_rows(tl.h);
         ra.tdesc = P.d_tdesc.as<int4>(); ra.tdesc_stride = P.tdesc_stride;
         ra.roi = P.d_roi.as<uint8_t>(); ra.roi_pitch = roi_pitch_for(tl.w); ra.roi_stride = P.roi_stride;
         ra.rowsum = P.d_rowsum.as<uint32_t>();

@@ -202,6 +202,7 @@ void launch_cand_step(const RoiArgs& a, int max_items, hipStream_t st);
 void launch_pack(const PackArgs& a, hipStream_t st);
 int roi_pick_rc(int tw, int th);
 int roi_pitch_for(int tw);
+int roi_tab_rows(int th);   // rows of a ROI's X0 / Y0 tables: th + 6 rounded up to a 32-row tile
 size_t roi_tiles_bytes(int tw, int th);
 int roi_tiles_for(int tw, int th);   // 32x32 warp tiles of a (tw+6) x (th+6) ROI
 size_t roi_corr_lds(int roi_pitch, int tw, int rc, bool global_a);

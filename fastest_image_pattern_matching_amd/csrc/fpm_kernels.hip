@@ -1725,6 +1725,10 @@ __host__ __device__ inline int roi_pitch_calc(int tw) {
     return q * 16;
 }
 int roi_pitch_for(int tw) { return roi_pitch_calc(tw); }
+int roi_tab_rows(int th) { return (th + 6 + ROI_T - 1) / ROI_T * ROI_T; }
+// Position of ROI row y in a ROI's X0 / Y0 tables: inside each 32-row tile block, rows y, y + 8, y + 16, y + 24 are
+// adjacent (k_roi_warp's lane of rows lr + 8i reads its four row origins as one 16-byte load)
+__host__ __device__ inline int roi_tab_row_pos(int y) { return (y & ~31) | ((y & 7) << 2) | ((y >> 3) & 3); }
 size_t roi_tiles_bytes(int tw, int th) {   // tile-major ROI scratch of one (tw+6) x (th+6) ROI
     return (size_t)((tw + 6 + ROI_T - 1) / ROI_T) * ((th + 6 + ROI_T - 1) / ROI_T) * ROI_T * ROI_T;
 }
@@ -1817,16 +1821,56 @@ __device__ __forceinline__ void lds_taps(uint32_t off, int ftw, int v[4]) {
     fpm_lds_u8* q = (fpm_lds_u8*)(size_t)(off + ftw);
     v[0] = p[0]; v[1] = p[1]; v[2] = q[0]; v[3] = q[1];
 }
-// with a compile-time pitch: all four are immediate offsets of one address
-template <int PITCH>
-__device__ __forceinline__ void lds_taps_c(uint32_t off, int v[4]) {
-    fpm_lds_u8* p = (fpm_lds_u8*)(size_t)off;
-    v[0] = p[0]; v[1] = p[1]; v[2] = p[PITCH]; v[3] = p[PITCH + 1];
-}
 // (32*h0 + fy*(h1 - h0) + 512) >> 10 with h = 32*va + fx*(vb - va), on the 24-bit multiplier only
 __device__ __forceinline__ int bilerp24(const int v[4], int fx, int fy) {
     const int h0 = mad24(fx, v[1] - v[0], v[0] << 5), h1 = mad24(fx, v[3] - v[2], v[2] << 5);
     return mad24(fy, h1 - h0, (h0 << 5) + 512) >> 10;
+}
+// The same integers for the four pixels of one output row, packed into a dword (pixel u in byte u), in 7 VALU per
+// pixel + 3 per row instead of 12 per pixel (k_roi_warp's row: 64 VALU instead of 77): the two tap rows' horizontal passes run as one pair of 16-bit lanes (h = 32 va + fx (vb - va)
+// <= 8160; lane arithmetic mod 2^16, exact since the true value fits), fx taken from the low half of its register by
+// op_sel (no splat), the vertical pass as one u16 dot product with the weights (64 (32 - fy), 64 fy) plus 64 * 512:
+// 64 * (32 h0 + fy (h1 - h0) + 512) < 2^24, so the result byte is bits 16..23 and two byte permutes + one bitwise op
+// pack the row.  Taps must be zero-extended bytes (lds_taps16).
+typedef unsigned short fpm_u16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t bilerp_row4(const int v[4][4], const int fx[4], const int fy[4]) {
+    uint32_t r[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const uint32_t a02 = __builtin_amdgcn_perm((uint32_t)v[u][2], (uint32_t)v[u][0], 0x0c040c00u);   // (v0, v2)
+        const uint32_t a13 = __builtin_amdgcn_perm((uint32_t)v[u][3], (uint32_t)v[u][1], 0x0c040c00u);   // (v1, v3)
+        const fpm_u16x2v d = __builtin_bit_cast(fpm_u16x2v, a13) - __builtin_bit_cast(fpm_u16x2v, a02);
+        const fpm_u16x2v b = __builtin_bit_cast(fpm_u16x2v, a02) << (fpm_u16x2v)5;
+        uint32_t h;
+        asm("v_pk_mad_u16 %0, %1, %2, %3 op_sel_hi:[0,1,1]"
+            : "=v"(h) : "v"(fx[u]), "v"(__builtin_bit_cast(uint32_t, d)), "v"(__builtin_bit_cast(uint32_t, b)));
+        const uint32_t wy = (uint32_t)mad24(fy[u], 64 * 0x10000 - 64, 64 * 32);   // (64 (32 - fy), 64 fy)
+        r[u] = __builtin_amdgcn_udot2(__builtin_bit_cast(fpm_u16x2v, h), __builtin_bit_cast(fpm_u16x2v, wy), 64u * 512u,
+                                      false);
+    }
+    return __builtin_amdgcn_perm(r[1], r[0], 0x0c0c0602u) | __builtin_amdgcn_perm(r[3], r[2], 0x06020c0cu);
+}
+// The 16 taps of one output row (4 pixels x 2 rows x 2 columns) at a compile-time pitch, all issued before any use:
+// explicit ds_read_u8 (zero-extending; the compiler's own form re-masks every result with 0xff when it feeds 16-bit
+// lanes) and one lgkmcnt(0) that the results depend on.
+template <int PITCH>
+__device__ __forceinline__ void lds_taps16(const uint32_t off[4], int v[4][4]) {
+#define FPM_TAPS(U)                                                                                                     \
+    asm volatile("ds_read_u8 %0, %4\n\tds_read_u8 %1, %4 offset:1\n\tds_read_u8 %2, %4 offset:%5\n\t"                \
+                 "ds_read_u8 %3, %4 offset:%6"                                                                          \
+                 : "=&v"(v[U][0]), "=&v"(v[U][1]), "=&v"(v[U][2]), "=&v"(v[U][3])                                       \
+                 : "v"(off[U]), "i"(PITCH), "i"(PITCH + 1))
+    FPM_TAPS(0);
+    FPM_TAPS(1);
+    FPM_TAPS(2);
+    FPM_TAPS(3);
+#undef FPM_TAPS
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(v[0][0]), "+v"(v[0][1]), "+v"(v[0][2]), "+v"(v[0][3]), "+v"(v[1][0]), "+v"(v[1][1]),
+                   "+v"(v[1][2]), "+v"(v[1][3]), "+v"(v[2][0]), "+v"(v[2][1]), "+v"(v[2][2]), "+v"(v[2][3]),
+                   "+v"(v[3][0]), "+v"(v[3][1]), "+v"(v[3][2]), "+v"(v[3][3])
+                 :
+                 : "memory");
 }
 
 // One bilinear ROI pixel from a staged footprint, BORDER_CONSTANT(0) rules of remapBilinear (general path).
@@ -1990,9 +2034,12 @@ __global__ __launch_bounds__(256) void k_roi_tables(RoiArgs a) {
             lad[x] = ad; lbd[x] = bd;
         }
         for (int y = threadIdx.x; y < a.tabh; y += 256) {
-            const int x0 = rint_i((M[1] * y + M[2]) * kAbScale) + kRoundDelta;
-            const int y0 = rint_i((M[4] * y + M[5]) * kAbScale) + kRoundDelta;
-            t[2 * a.tabw + y] = x0; t[2 * a.tabw + a.tabh + y] = y0;
+            // rows past the ROI (the last tile block's padding) repeat its last row: k_roi_warp reads them unclamped
+            const int yc = min(y, RH - 1);
+            const int x0 = rint_i((M[1] * yc + M[2]) * kAbScale) + kRoundDelta;
+            const int y0 = rint_i((M[4] * yc + M[5]) * kAbScale) + kRoundDelta;
+            const int q = roi_tab_row_pos(y);
+            t[2 * a.tabw + q] = x0; t[2 * a.tabw + a.tabh + q] = y0;
             lx0[y] = x0; ly0[y] = y0;
         }
         __syncthreads();
@@ -2113,24 +2160,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const int ry0 = ty * ROI_T, ry1 = min(ry0 + ROI_T, RH) - 1;
         const int c0 = cx0 + 4 * lg;
         const int4 dsc = nd;
+        const int flags = __builtin_amdgcn_readfirstlane(dsc.w);
+        const bool in_lds = (flags & kTileLds) != 0;
         const int cc = min(c0, cx1 & ~3);   // tables are read in bounds even for idle lanes
         const int4 A = ld_at<int4>(tb, 4u * cc);
         const int4 B = ld_at<int4>(tb, 4u * (a.tabw + cc));
-        int X0r[4], Y0r[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t r = min(ry0 + lr + 8 * i, ry1);
-            X0r[i] = ld_at<int>(tb, 4u * (2 * a.tabw + r));
-            Y0r[i] = ld_at<int>(tb, 4u * (2 * a.tabw + a.tabh + r));
-        }
+        const int adv[4] = {A.x, A.y, A.z, A.w}, bdv[4] = {B.x, B.y, B.z, B.w};
+        // the lane's rows ry0 + lr + 8i: one 16-byte load each for X0 and Y0 (roi_tab_row_pos; rows past the ROI hold
+        // its last row)
+        const int4 X4 = ld_at<int4>(tb, 4u * (2 * a.tabw + ry0 + 4 * lr));
+        const int4 Y4 = ld_at<int4>(tb, 4u * (2 * a.tabw + a.tabh + ry0 + 4 * lr));
+        const int X0r[4] = {X4.x, X4.y, X4.z, X4.w}, Y0r[4] = {Y4.x, Y4.y, Y4.z, Y4.w};
         uint8_t* tile = a.roi + (size_t)slot * a.roi_stride + ((size_t)rem << 10);   // tile-major: (ty, tx) = rem
 
         const int bxa = __builtin_amdgcn_readfirstlane(dsc.x), by0 = __builtin_amdgcn_readfirstlane(dsc.y);
-        const int dz = __builtin_amdgcn_readfirstlane(dsc.z), flags = __builtin_amdgcn_readfirstlane(dsc.w);
+        const int dz = __builtin_amdgcn_readfirstlane(dsc.z);
         const int wpr = dz & 0xffff, fth = dz >> 16;
         const uint8_t* lvl = a.level + (size_t)(flags >> kTileSrcShift) * a.level_stride;   // its source level
         constexpr int ftw = kFtPitch;
-        const bool in_lds = (flags & kTileLds) != 0;
         wave_sync();   // previous task's gathers are done with FT
         if (ABL != 1 && ABL != 3 && ABL != 6 && (flags & kTileAny) && in_lds) {
             if constexpr (FB == 0) stage_footprint_dma(FT, wpr, fth, lvl + (size_t)by0 * a.P + bxa, a.P, lane);
@@ -2144,10 +2191,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         if (ABL == 3) continue;
         if (ABL == 2) {
             for (int i = 0; i < 4; ++i)
-                if (ry0 + lr + 8 * i <= ry1) st_at<uint32_t>(tile, st_lane + 256u * i, (uint32_t)(X0r[i] ^ Y0r[i] ^ A.x ^ B.w));
+                if (ry0 + lr + 8 * i <= ry1) st_at<uint32_t>(tile, st_lane + 256u * i, (uint32_t)(X0r[i] ^ Y0r[i] ^ adv[0] ^ bdv[3]));
             continue;
         }
-        const int adv[4] = {A.x, A.y, A.z, A.w}, bdv[4] = {B.x, B.y, B.z, B.w};
         if ((flags & kTileInterior) && in_lds && ABL == 4) {
             const int obase = by0 * ftw + bxa;
             const int nvalid = RW - c0;
@@ -2187,14 +2233,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                     fyv[u] = __builtin_amdgcn_ubfe(syv, kAbBits - kInterBits, kInterBits);
                     off[u] = (uint32_t)mad24(syv >> kAbBits, ftw, sxv >> kAbBits);
                 }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) lds_taps_c<kFtPitch>(off[u], v[u]);
-                // keep the 16 reads together ahead of the arithmetic (the scheduler otherwise interleaves them with
-                // waits when it has registers to save: measured 241 -> 280 us per launch)
-                __builtin_amdgcn_sched_barrier(0);
-                uint32_t pk = 0;
-#pragma unroll
-                for (int u = 0; u < 4; ++u) pk |= (uint32_t)bilerp24(v[u], fxv[u], fyv[u]) << (8 * u);
+                // the 16 reads together ahead of the arithmetic (measured: the compiler's scheduling otherwise
+                // interleaves them with waits, 241 -> 280 us per launch)
+                lds_taps16<kFtPitch>(off, v);
+                const uint32_t pk = bilerp_row4(v, fxv, fyv);
                 if (ABL == 5 || ABL == 6) {
                     if ((pk & colmask) == 0x9e3779b9u && (lane ^ bxa) == 977) st_at<uint32_t>(tile, st_lane, pk);
                 } else if (ry0 + lr + 8 * i <= ry1) {

@@ -76,7 +76,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&a.wsum, ws_n * 4));
     CK(hipMalloc(&a.wsq, ws_n * 8));
     CK(hipMalloc(&a.rec, sizeof(RoiRecord) * C * n3));
-    a.tabw = roi_pitch_for(TW); a.tabh = ((TH + 6) + 3) & ~3;
+    a.tabw = roi_pitch_for(TW); a.tabh = roi_tab_rows(TH);
     a.roi_pitch = roi_pitch_for(TW); a.roi_stride = roi_tiles_bytes(TW, TH);
     CK(hipMalloc(&a.tab, (size_t)C * n3 * 2 * (a.tabw + a.tabh) * 4));
     a.tdesc_stride = roi_tiles_for(TW, TH);

@@ -89,7 +89,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&a.rec, sizeof(RoiRecord) * C * n3));
         printf("rois %d rc %d chunks %d corr lds %zu / %zu\n", C * n3, a.rc, a.nchunk, roi_corr_lds(roi_pitch_for(TW), TW, a.rc, false), roi_corr_lds(roi_pitch_for(TW), TW, a.rc, true));
     // ---- product kernels (tables -> warp -> corr -> eval) --------------------------------------------------
-    a.tabw = roi_pitch_for(TW); a.tabh = ((TH + 6) + 3) & ~3;
+    a.tabw = roi_pitch_for(TW); a.tabh = roi_tab_rows(TH);
     a.roi_pitch = roi_pitch_for(TW); a.roi_stride = roi_tiles_bytes(TW, TH);
     CK(hipMalloc(&a.tab, (size_t)C * n3 * 2 * (a.tabw + a.tabh) * 4));
     a.tdesc_stride = roi_tiles_for(TW, TH);
@@ -110,21 +110,19 @@ int main(int argc, char** argv) {
         const long tiles = (long)a.slot_cap * ((TH + 6 + 31) / 32) * ((TW + 6 + 31) / 32);
         const int grid = (int)std::min<long>((tiles + 3) / 4, 16384);
         timeit([&] { hipLaunchKernelGGL(k_roi_warp<0>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot LDS-DMA");
-        timeit([&] { hipLaunchKernelGGL(k_roi_warp<2>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 2");
-        timeit([&] { hipLaunchKernelGGL(k_roi_warp<4>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 4");
-        timeit([&] { hipLaunchKernelGGL(k_roi_warp<8>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 8");
-        timeit([&] { hipLaunchKernelGGL(k_roi_warp<12>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot batch 12");
+        timeit([&] { hipLaunchKernelGGL(k_roi_warp<12>, dim3(grid), dim3(256), 0, 0, a); }, "warp b12 7 waves (first)");
         if (!getenv("MB_SHORT")) {
-            timeit([&] { hipLaunchKernelGGL((k_roi_warp<4, 0, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp b4 8 waves");
-            timeit([&] { hipLaunchKernelGGL((k_roi_warp<8, 0, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp b8 8 waves");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 0, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp b12 8 waves");
-            timeit([&] { hipLaunchKernelGGL((k_roi_warp<8, 5>), dim3(grid), dim3(256), 0, 0, a); }, "warp no stores");
-            timeit([&] { hipLaunchKernelGGL((k_roi_warp<8, 6>), dim3(grid), dim3(256), 0, 0, a); }, "warp gathers only");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 0, 7>), dim3(grid), dim3(256), 0, 0, a); }, "warp b12 7 waves");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp<8, 0, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp b8 8 waves");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp<16, 0, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp b16 8 waves");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 5, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp no stores");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 6, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp gathers only");
         }
-        timeit([&] { hipLaunchKernelGGL((k_roi_warp<8, 1>), dim3(grid), dim3(256), 0, 0, a); }, "warp no staging");
-        timeit([&] { hipLaunchKernelGGL((k_roi_warp<8, 2>), dim3(grid), dim3(256), 0, 0, a); }, "warp no gathers");
-        timeit([&] { hipLaunchKernelGGL((k_roi_warp<8, 4>), dim3(grid), dim3(256), 0, 0, a); }, "warp dot4 taps");
-        timeit([&] { hipLaunchKernelGGL((k_roi_warp<8, 3>), dim3(grid), dim3(256), 0, 0, a); }, "warp tables only");
+        timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 1, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp no staging");
+        timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 2, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp no gathers");
+        timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 4, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp dot4 taps");
+        timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 3, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp tables only");
         printf("tiles %ld\n", tiles);
     }
     if (envi("MB_WARP_ONLY", 0)) return 0;

@@ -36,6 +36,11 @@ __global__ __launch_bounds__(256) void k(unsigned* out, unsigned long long* cyc,
         if (OP == 9) BODY8("v_add3_u32");
         if (OP == 10) BODY8("v_mad_i32_i24");
         if (OP == 11) BODY8_2("v_ashrrev_i32");
+        if (OP == 12) BODY8("v_pk_mad_u16");
+        if (OP == 13) BODY8("v_dot2_u32_u16");
+        if (OP == 14) BODY8_2("v_pk_sub_i16");
+        if (OP == 15) BODY8("v_lshl_add_u32");
+        if (OP == 16) BODY8_2("v_sub_u32");
     }
     const unsigned long long t1 = __builtin_readcyclecounter();
     out[blockIdx.x * 256 + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
@@ -45,7 +50,8 @@ __global__ __launch_bounds__(256) void k(unsigned* out, unsigned long long* cyc,
 int main() {
     const char* names[] = {"v_add_u32", "v_mul_u32_u24", "v_mad_u32_u24", "v_mul_lo_u32", "v_bfe_u32",
                            "v_alignbyte_b32", "v_dot4_u32_u8", "v_perm_b32", "v_lshl_or_b32", "v_add3_u32",
-                           "v_mad_i32_i24", "v_ashrrev_i32"};
+                           "v_mad_i32_i24", "v_ashrrev_i32", "v_pk_mad_u16", "v_dot2_u32_u16",
+                           "v_pk_sub_i16", "v_lshl_add_u32", "v_sub_u32"};
     const int blocks = 2048, iters = 2048;
     unsigned* d;
     unsigned long long* dc;
@@ -67,7 +73,12 @@ int main() {
                 case 8: hipLaunchKernelGGL(k<8>, dim3(blocks), dim3(256), 0, 0, d, dc, 7u, iters); break;
                 case 9: hipLaunchKernelGGL(k<9>, dim3(blocks), dim3(256), 0, 0, d, dc, 7u, iters); break;
                 case 10: hipLaunchKernelGGL(k<10>, dim3(blocks), dim3(256), 0, 0, d, dc, 7u, iters); break;
-                default: hipLaunchKernelGGL(k<11>, dim3(blocks), dim3(256), 0, 0, d, dc, 7u, iters); break;
+                case 11: hipLaunchKernelGGL(k<11>, dim3(blocks), dim3(256), 0, 0, d, dc, 7u, iters); break;
+                case 12: hipLaunchKernelGGL(k<12>, dim3(blocks), dim3(256), 0, 0, d, dc, 7u, iters); break;
+                case 13: hipLaunchKernelGGL(k<13>, dim3(blocks), dim3(256), 0, 0, d, dc, 7u, iters); break;
+                case 14: hipLaunchKernelGGL(k<14>, dim3(blocks), dim3(256), 0, 0, d, dc, 7u, iters); break;
+                case 15: hipLaunchKernelGGL(k<15>, dim3(blocks), dim3(256), 0, 0, d, dc, 7u, iters); break;
+                default: hipLaunchKernelGGL(k<16>, dim3(blocks), dim3(256), 0, 0, d, dc, 7u, iters); break;
             }
         };
         launch();
@@ -84,7 +95,7 @@ int main() {
     const double simds = prop.multiProcessorCount * 4.0;
     const double instr = (double)blocks * 4 * iters * 8;   // wave-instructions
     double base = 0;
-    for (int op = 0; op < 12; ++op) {
+    for (int op = 0; op < 17; ++op) {
         const double ms = run(op);
         // cycles per wave-instruction per SIMD at an assumed 2.4 GHz (relative numbers are what matter)
         const double cpi = ms * 1e-3 * 2.4e9 / (instr / simds);

@@ -173,7 +173,7 @@ int main(int argc, char** argv) {
     a.tw = TW; a.th = TH;
     a.n3 = n3; a.per_source = ncand; a.slot_base = 0; a.slot_cap = C * n3;
     a.live = d_live; a.live_count = d_cnt; a.state = d_st; a.nodes = d_nodes;
-    a.tabw = roi_pitch_for(TW); a.tabh = ((TH + 6) + 3) & ~3;
+    a.tabw = roi_pitch_for(TW); a.tabh = roi_tab_rows(TH);
     a.roi_pitch = roi_pitch_for(TW); a.roi_stride = roi_tiles_bytes(TW, TH);
     CK(hipMalloc(&a.tab, (size_t)C * n3 * 2 * (a.tabw + a.tabh) * 4));
     a.tdesc_stride = roi_tiles_for(TW, TH);
