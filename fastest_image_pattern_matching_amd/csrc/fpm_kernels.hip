@@ -2120,7 +2120,9 @@ __device__ __forceinline__ void stage_footprint32(uint8_t* FT, int wpr, int fth,
 
 // FB: footprint rows in flight per lane (0 = LDS-DMA).  ABL (profiling ablations, product 0): 1 = no footprint
 // staging, 2 = no gathers (stores zeros), 3 = tables + descriptor only, 4 = dot-product interior taps (ft_tap_interior),
-// 5 = no ROI stores (interior rows computed, a never-true store kept), 6 = neither staging nor stores
+// 5 = no ROI stores (interior rows computed, a never-true store kept), 6 = neither staging nor stores, 7 = as 6 with
+// synthetic taps (no LDS reads), 8 = as 6 with the taps XOR-folded (no bilinear arithmetic), 9 = as 6 with two tap
+// reads per pixel (the other two taps copied: LDS instruction count halved, arithmetic unchanged)
 template <int FB, int ABL = 0, int WPE = 7>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_warp(RoiArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t ft_all[4 * ROI_FT + 16];   // + slack for ft_tap_interior
@@ -2179,7 +2181,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const uint8_t* lvl = a.level + (size_t)(flags >> kTileSrcShift) * a.level_stride;   // its source level
         constexpr int ftw = kFtPitch;
         wave_sync();   // previous task's gathers are done with FT
-        if (ABL != 1 && ABL != 3 && ABL != 6 && (flags & kTileAny) && in_lds) {
+        if (ABL != 1 && ABL != 3 && ABL < 6 && (flags & kTileAny) && in_lds) {
             if constexpr (FB == 0) stage_footprint_dma(FT, wpr, fth, lvl + (size_t)by0 * a.P + bxa, a.P, lane);
             else stage_footprint32<FB, kFtPitch>(FT, wpr, fth, lvl + (size_t)by0 * a.P + bxa, a.P, lane);
         }
@@ -2235,9 +2237,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 }
                 // the 16 reads together ahead of the arithmetic (measured: the compiler's scheduling otherwise
                 // interleaves them with waits, 241 -> 280 us per launch)
-                lds_taps16<kFtPitch>(off, v);
-                const uint32_t pk = bilerp_row4(v, fxv, fyv);
-                if (ABL == 5 || ABL == 6) {
+                if constexpr (ABL == 7) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        for (int k = 0; k < 4; ++k) v[u][k] = (off[u] >> (2 * k)) & 0xff;
+                } else if constexpr (ABL == 9) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        asm volatile("ds_read_u8 %0, %2\n\tds_read_u8 %1, %2 offset:%3" : "=&v"(v[u][0]), "=&v"(v[u][2]) : "v"(off[u]), "i"(kFtPitch));
+                    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0][0]), "+v"(v[0][2]), "+v"(v[1][0]), "+v"(v[1][2]), "+v"(v[2][0]), "+v"(v[2][2]), "+v"(v[3][0]), "+v"(v[3][2]) :: "memory");
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) { v[u][1] = v[u][0]; v[u][3] = v[u][2]; }
+                } else {
+                    lds_taps16<kFtPitch>(off, v);
+                }
+                uint32_t pk;
+                if constexpr (ABL == 8) {
+                    pk = 0;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) pk ^= (uint32_t)(v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3]) << u;
+                } else {
+                    pk = bilerp_row4(v, fxv, fyv);
+                }
+                if (ABL >= 5) {
                     if ((pk & colmask) == 0x9e3779b9u && (lane ^ bxa) == 977) st_at<uint32_t>(tile, st_lane, pk);
                 } else if (ry0 + lr + 8 * i <= ry1) {
                     st_at<uint32_t>(tile, st_lane + 256u * i, pk & colmask);

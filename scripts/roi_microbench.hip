@@ -115,9 +115,11 @@ int main(int argc, char** argv) {
             timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 0, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp b12 8 waves");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 0, 7>), dim3(grid), dim3(256), 0, 0, a); }, "warp b12 7 waves");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp<8, 0, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp b8 8 waves");
-            timeit([&] { hipLaunchKernelGGL((k_roi_warp<16, 0, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp b16 8 waves");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 5, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp no stores");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 6, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp gathers only");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 7, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp gathers, no LDS");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 8, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp gathers, no math");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 9, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp gathers, 2 reads/px");
         }
         timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 1, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp no staging");
         timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 2, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp no gathers");
