@@ -16,6 +16,8 @@
 #include <cfloat>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -151,6 +153,9 @@ struct fpm_ctx {
     uint64_t plan_gen = ~0ull;
     // op scratch
     DevBuf d_op_a, d_op_b, d_op_job;
+    // filterWithRotatedRect on the device (overlap_filter_device): rectangles + counters; staging and mapped outputs
+    DevBuf d_ov;
+    PinBuf h_ov_in, h_ov_out;
     // last search stats
     std::vector<int64_t> stats;
     int64_t alg_bytes[3] = {0, 0, 0};   // SURVEY.md §8(d) algorithmic bytes of the last search: B_pyr, B_top, B_ref
@@ -832,12 +837,18 @@ void collect_candidates(fpm_ctx* ctx, int s, const std::vector<int>& pos, std::v
     const CandState* state = (const CandState*)(h + P.h_state);
     const RoiRecord* rec = (const RoiRecord*)(h + P.h_rec);
     const TmplLevel& t0 = ctx->tmpl[0];
-    std::vector<HostMatch> nm(P.n3);   // one candidate's n3 angle results, reused
     const double astep = std::atan(2.0 / std::max(t0.w, t0.h)) * kR2D;   // layer 0's angle step (:283)
     const SrcLevel& lv = ctx->src[0];
     const F2 sc = f2((lv.w - 1) / 2.0f, (lv.h - 1) / 2.0f);
-    for (int a = 0; a < P.nang; ++a) {
+    // each angle's candidates go to their place in push order (angle-major): the angles run on the host pool when
+    // there are many candidates
+    std::vector<int> first(P.nang + 1, 0);
+    for (int a = 0; a < P.nang; ++a) first[a + 1] = first[a] + counts[s * P.nang + a];
+    out.resize(first[P.nang]);
+    auto angle = [&](int a) {
         const int job = s * P.nang + a;
+        HostMatch nm[3];   // one candidate's n3 (1 or 3) angle results
+        int o = first[a];
         for (int r = 0; r < counts[job]; ++r) {
             const int id = job * P.cap + r;
             const Peak& pk = peaks[id];
@@ -851,11 +862,11 @@ void collect_candidates(fpm_ctx* ctx, int s, const std::vector<int>& pos, std::v
                 const double rad = -P.angles[a] * kD2R;
                 const F2 lt = rotate_pt(f2(pt.x, pt.y), P.center, std::cos(rad), std::sin(rad));
                 c.x = lt.x; c.y = lt.y; c.score = pk.score; c.angle = P.angles[a]; c.kept = 1;
-                out.push_back(c);
+                out[o++] = c;
                 continue;
             }
             const int li = pos[id];
-            if (li < 0) { out.push_back(c); continue; }   // broke out at a layer > 0 (:331-332)
+            if (li < 0) { out[o++] = c; continue; }   // broke out at a layer > 0 (:331-332)
             const CandState& cs = state[li];
             // layer 0 (:282-358) from the device's ROI records
             const int d = L - 1;
@@ -873,7 +884,7 @@ void collect_candidates(fpm_ctx* ctx, int s, const std::vector<int>& pos, std::v
                 nm[j] = m;
                 if (nm[j].score > big) { imax = j; big = nm[j].score; }
             }
-            if (nm[imax].score < P.layer_score[0]) { out.push_back(c); continue; }
+            if (nm[imax].score < P.layer_score[0]) { out[o++] = c; continue; }
             if (ctx->run_prm.subpixel && !nm[imax].on_border && imax != 0 && imax != 2) {
                 double nx = 0, ny = 0, na = 0;
                 subpix_estimation(nm, &nx, &ny, &na, astep, imax);
@@ -888,8 +899,13 @@ void collect_candidates(fpm_ctx* ctx, int s, const std::vector<int>& pos, std::v
             const double nrad = -nang * kD2R;
             p = rotate_pt(p, sc, std::cos(nrad), std::sin(nrad));
             c.x = p.x; c.y = p.y; c.score = nm[imax].score; c.angle = nang; c.kept = 1;
-            out.push_back(c);
+            out[o++] = c;
         }
+    };
+    if (first[P.nang] < 1024) {
+        for (int a = 0; a < P.nang; ++a) angle(a);
+    } else {
+        host_parallel(P.nang, angle);
     }
 }
 
@@ -898,7 +914,7 @@ void collect_candidates(fpm_ctx* ctx, int s, const std::vector<int>& pos, std::v
 // filterWithScore is the unique descending order, whatever the push order and the first std::sort did with equal
 // top scores.  LSD radix sort on order-preserving 64-bit keys; false (nothing decided) on a tie or a NaN, and the
 // caller replays both std::sorts.
-static bool select_distinct_scores(const fpm_params& prm, const fpm_candidate* cand, int n, std::vector<HostMatch>& all) {
+static bool select_distinct_scores(const fpm_params& prm, const fpm_candidate* cand, int n, std::vector<int>& src) {
     struct SK { uint64_t k; int32_t i; };
     std::vector<SK> a, b;
     a.reserve(n);
@@ -926,20 +942,105 @@ static bool select_distinct_scores(const fpm_params& prm, const fpm_candidate* c
     }
     for (size_t t = 1; t < m; ++t)
         if (cand[a[t].i].score == cand[a[t - 1].i].score) return false;   // equal scores (+0 == -0 included)
-    all.clear();
-    all.reserve(m);
-    for (const SK& e : a) {
-        const fpm_candidate& c = cand[e.i];
-        HostMatch h{};
-        h.ptx = c.x; h.pty = c.y; h.score = c.score; h.angle = c.angle;
-        all.push_back(h);
+    src.resize(m);
+    for (size_t t = 0; t < m; ++t) src[t] = a[t].i;
+    return true;
+}
+
+// filterWithRotatedRect (:1133-1194) with its pair tests on the device: k_overlap_pairs decides every pair i < j
+// whose boxes overlap (the exact test of fpm_rrect.h, bit-identical to the host's), and the host replays the
+// reference's loop on those decisions -- for i in order, skipped once deleted, each listed j not yet deleted
+// deletes the lower-scored of the two (j, as v is sorted by descending score) -- evaluating itself only the pairs
+// whose point order needs acos.  The same deletions as filter_with_rotated_rect.  Returns false (nothing done, the
+// caller runs the host filter) without a context, for short lists, or when a rectangle has more overlapping
+// partners than the kernel keeps.
+constexpr int kOverlapDeviceMin = 1024;   // FPM_OVERLAP_DEVICE_MIN overrides (tests force small lists through it)
+static bool overlap_filter_device(fpm_ctx* ctx, std::vector<HostMatch>& v, double max_overlap) {
+    const int n = (int)v.size();
+    int min_n = kOverlapDeviceMin;
+    if (const char* e = getenv("FPM_OVERLAP_DEVICE_MIN")) min_n = std::max(1, atoi(e));
+    if (!ctx || n < min_n) return false;
+    const int cap = 48 * n;
+    const size_t boff = (sizeof(OvRect) * (size_t)n + 15) / 16 * 16;
+    const size_t rbytes = boff + sizeof(float4) * (size_t)n;   // rects, then boxes
+    if (ctx->h_ov_in.ensure(rbytes) != hipSuccess || ctx->d_ov.ensure(rbytes + 64) != hipSuccess ||
+        ctx->h_ov_out.ensure(sizeof(int32_t) * ((size_t)cap + 2 * (size_t)n + 16)) != hipSuccess)
+        return false;
+    OvRect* rin = ctx->h_ov_in.as<OvRect>();
+    float4* bin = ctx->h_ov_in.as<float4>(boff);
+    static const bool tail_times = [] { const char* e = getenv("FPM_TAIL_TIMES"); return e && *e == '1'; }();
+    using clk = std::chrono::steady_clock;
+    const clk::time_point q0 = clk::now();
+    auto geom = [&](int i0, int i1) {   // corners and boxes exactly as filter_with_rotated_rect computes them
+        for (int i = i0; i < i1; ++i) {
+            OvRect& o = rin[i];
+            rrect_corners(v[i].rect, o.c);
+            float x0 = o.c[0].x, x1 = o.c[0].x, y0 = o.c[0].y, y1 = o.c[0].y;
+            for (int k = 1; k < 4; ++k) {
+                x0 = std::min(x0, o.c[k].x); x1 = std::max(x1, o.c[k].x);
+                y0 = std::min(y0, o.c[k].y); y1 = std::max(y1, o.c[k].y);
+            }
+            o.w = v[i].rect.w; o.h = v[i].rect.h;
+            bin[i] = make_float4(x0 - 1.f, y0 - 1.f, x1 + 1.f, y1 + 1.f);
+        }
+    };
+    host_parallel((n + 511) / 512, [&](int t) { geom(t * 512, std::min(n, t * 512 + 512)); });
+    const clk::time_point q1 = clk::now();
+    int32_t* hout = ctx->h_ov_out.as<int32_t>();   // [meta 16][offcnt 2n][lists cap]
+    int32_t* dout = nullptr;
+    if (hipHostGetDevicePointer((void**)&dout, ctx->h_ov_out.p, 0) != hipSuccess) return false;
+    OvRect* drects = ctx->d_ov.as<OvRect>();
+    int32_t* dmeta = (int32_t*)((char*)ctx->d_ov.p + rbytes);
+    if (hipMemcpyAsync(drects, rin, rbytes, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+        hipMemsetAsync(dmeta, 0, 2 * sizeof(int32_t), ctx->stream) != hipSuccess)
+        return false;
+    launch_overlap_pairs(drects, ctx->d_ov.as<float4>(boff), n, max_overlap, dout + 16 + 2 * n, cap, dout + 16, dmeta,
+                         ctx->stream);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(hout, dmeta, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess)
+        return false;
+    const clk::time_point q2 = clk::now();
+    if (hout[1] != 0) return false;   // a rectangle with too many partners, or the list overflowed
+    // the outputs, written by the device into mapped host memory, read once into ordinary memory
+    std::vector<int32_t> local((size_t)2 * n + hout[0]);
+    std::memcpy(local.data(), hout + 16, sizeof(int32_t) * local.size());
+    const clk::time_point q3 = clk::now();
+    const int32_t* offcnt = local.data();
+    const int32_t* lists = local.data() + 2 * n;
+    std::vector<char> del(n, 0);
+    int host_pairs = 0;
+    // v is sorted by descending score, so "the lower-scored of the two" is j; a NaN score breaks that order, and then
+    // the scores are compared as the reference does
+    bool monotone = true;
+    for (int i = 0; i + 1 < n && monotone; ++i) monotone = v[i].score >= v[i + 1].score;
+    for (int i = 0; i < n; ++i) {
+        if (del[i]) continue;
+        const int32_t* L = lists + offcnt[2 * i];
+        for (int k = 0; k < offcnt[2 * i + 1]; ++k) {
+            const int32_t e = L[k];
+            const int j = e >= 0 ? e : ~e;
+            if (del[j]) continue;
+            if (e < 0 && (++host_pairs, !rrect_pair_drops(v[i].rect, v[j].rect, max_overlap))) continue;
+            if (monotone || v[i].score >= v[j].score) del[j] = 1;
+            else del[i] = 1;
+        }
+    }
+    size_t w = 0;
+    for (int i = 0; i < n; ++i)
+        if (!del[i]) v[w++] = v[i];
+    v.resize(w);
+    if (tail_times) {
+        auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        fprintf(stderr, "overlap-dev n=%d geom %.3f device %.3f read %.3f replay %.3f ms, %d pair entries, %d decided on the host\n",
+                n, ms(q0, q1), ms(q1, q2), ms(q2, q3), ms(q3, clk::now()), hout[0], host_pairs);
     }
     return true;
 }
 
 // Returns false when `cand` is not in push order (angle_index ascending, peak_rank 0, 1, ... within an angle).
 bool merge_candidates(const fpm_params& prm, int t0w, int t0h, const fpm_candidate* cand, int n,
-                      std::vector<fpm_result>& out) {
+                      std::vector<fpm_result>& out, fpm_ctx* dev_ctx) {
     out.clear();
     for (int i = 0; i < n; ++i) {
         const bool first = i == 0 || cand[i].angle_index != cand[i - 1].angle_index;
@@ -947,44 +1048,68 @@ bool merge_candidates(const fpm_params& prm, int t0w, int t0h, const fpm_candida
                   : cand[i].peak_rank != cand[i - 1].peak_rank + 1)
             return false;
     }
+    // FPM_TAIL_TIMES=1: per-stage wall clocks of this tail on stderr (profiling aid)
+    static const bool tail_times = [] { const char* e = getenv("FPM_TAIL_TIMES"); return e && *e == '1'; }();
+    using clk = std::chrono::steady_clock;
+    const clk::time_point t0 = clk::now();
+    clk::time_point t1 = t0;
     std::vector<HostMatch> all;
-    if (!select_distinct_scores(prm, cand, n, all)) {
+    // vecAllResult entry from a candidate record, with its rotated rectangle (:380-390)
+    auto fill = [&](HostMatch& m, const fpm_candidate& c) {
+        m = HostMatch{};
+        m.ptx = c.x; m.pty = c.y; m.score = c.score; m.angle = c.angle;
+        const double rad = -m.angle * kD2R;
+        const float cs = (float)std::cos(rad), sn = (float)std::sin(rad);
+        const F2 lt = f2((float)m.ptx, (float)m.pty);
+        const F2 rt = f2(lt.x + t0w * cs, lt.y - t0w * sn);
+        const F2 rb = f2(rt.x + t0h * sn, rt.y + t0h * cs);
+        m.rect = rrect_from3(lt, rt, rb);
+        m.del = false;
+    };
+    std::vector<int> src;   // candidate index of each vecAllResult entry after filterWithScore
+    if (select_distinct_scores(prm, cand, n, src)) {
+        t1 = clk::now();
+    } else {
         // std::sort(vecMatchParameter, compareScoreBig2Small) (:214) over the push-order sequence.  The permutation
         // std::sort produces depends only on the sequence of comparison results, so sorting light (score, index)
         // keys with the same comparator reproduces the reference's order of equal scores exactly.
         struct Key { double score; int i; };
+        auto by_score = [](const Key& l, const Key& r) { return l.score > r.score; };
         std::vector<Key> order(n);
         for (int i = 0; i < n; ++i) order[i] = {cand[i].top_score, i};
-        std::sort(order.begin(), order.end(), [](const Key& l, const Key& r) { return l.score > r.score; });
-        all.clear();
-        all.reserve(n);
-        for (const Key& k : order) {   // vecAllResult in sorted-candidate order (:262-358)
-            const fpm_candidate& c = cand[k.i];
-            if (!c.kept) continue;
-            HostMatch m{};
-            m.ptx = c.x; m.pty = c.y; m.score = c.score; m.angle = c.angle;
-            all.push_back(m);
-        }
-        filter_with_score(all, prm.score);
+        std::sort(order.begin(), order.end(), by_score);
+        // vecAllResult in sorted-candidate order (:262-358) is the kept candidates' sequence; filterWithScore's
+        // std::sort (:373-378) sees exactly their scores in that order, so it runs on (score, candidate) keys too
+        std::vector<Key> ks;
+        ks.reserve(n);
+        for (const Key& k : order)
+            if (cand[k.i].kept) ks.push_back({cand[k.i].score, k.i});
+        t1 = clk::now();
+        std::sort(ks.begin(), ks.end(), by_score);
+        size_t m = 0;   // the sorted list ends at the first score below the threshold (filter_with_score)
+        while (m < ks.size() && !(ks[m].score < prm.score)) ++m;
+        src.resize(m);
+        for (size_t t = 0; t < m; ++t) src[t] = ks[t].i;
     }
-    // rotated rectangles (:380-390), per candidate
-    auto rects = [&](int i0, int i1) {
-        for (int i = i0; i < i1; ++i) {
-            HostMatch& m = all[i];
-            const double rad = -m.angle * kD2R;
-            const float c = (float)std::cos(rad), sn = (float)std::sin(rad);
-            const F2 lt = f2((float)m.ptx, (float)m.pty);
-            const F2 rt = f2(lt.x + t0w * c, lt.y - t0w * sn);
-            const F2 rb = f2(rt.x + t0h * sn, rt.y + t0h * c);
-            m.rect = rrect_from3(lt, rt, rb);
-            m.del = false;
-        }
-    };
-    const int na = (int)all.size();
-    if (na <= 512) rects(0, na);
-    else host_parallel((na + 511) / 512, [&](int t) { rects(t * 512, std::min(na, t * 512 + 512)); });
-    filter_with_rotated_rect(all, prm.max_overlap);
+    const clk::time_point t2 = clk::now();
+    const int na = (int)src.size();
+    all.resize(na);
+    if (na <= 512) {
+        for (int i = 0; i < na; ++i) fill(all[i], cand[src[i]]);
+    } else {
+        host_parallel((na + 255) / 256, [&](int t) {
+            for (int i = t * 256; i < std::min(na, t * 256 + 256); ++i) fill(all[i], cand[src[i]]);
+        });
+    }
+    const clk::time_point t3 = clk::now();
+    if (!overlap_filter_device(dev_ctx, all, prm.max_overlap)) filter_with_rotated_rect(all, prm.max_overlap);
+    const clk::time_point t4 = clk::now();
     std::sort(all.begin(), all.end(), score_big2small);
+    if (tail_times) {
+        auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        fprintf(stderr, "tail n=%d sort1+collect %.3f score %.3f rects %.3f overlap %.3f final %.3f ms -> %zu\n", n,
+                ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4), ms(t4, clk::now()), all.size());
+    }
     if (prm.semantics == FPM_SEMANTICS_MFC) {   // MatchToolDlg.cpp:1080-1116
         for (const HostMatch& m : all) {
             const double rad = -m.angle * kD2R;
@@ -1070,6 +1195,12 @@ int complete_staged(fpm_ctx* ctx, std::vector<std::vector<fpm_result>>& results,
     if (!ctx->pending) { ctx->err = "no search in flight"; return FPM_E_INVALID_ARG; }
     ctx->pending = false;
     const auto c0 = ctx->t_call0;
+    {   // a large host tail follows (thousands of top-layer candidates per source): wake the host pool now, so its
+        // workers are spinning, not asleep, when the tail's parallel regions start after the device wait
+        const Plan& P = ctx->plan;
+        if ((size_t)P.nang * P.cap >= 2048)
+            host_pool_warm((int)std::min(10000.0, 1000.0 * std::max(1.0, (double)ctx->last_device_ms) + 1000.0));
+    }
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     const auto c1 = std::chrono::steady_clock::now();
     {
@@ -1092,7 +1223,7 @@ int complete_staged(fpm_ctx* ctx, std::vector<std::vector<fpm_result>>& results,
         collect_candidates(ctx, s, pos, ctx->cands[s]);
         if (merge)
             merge_candidates(ctx->run_prm, ctx->tmpl[0].w, ctx->tmpl[0].h, ctx->cands[s].data(), (int)ctx->cands[s].size(),
-                         results[s]);
+                             results[s], ctx);
     }
     // stats: [angles, top candidates, live entering layer L-1 .. 0] (totals over the batch)
     const char* h = P.h_out.as<char>();
@@ -1214,6 +1345,7 @@ int fpm_destroy(fpm_ctx* ctx) {
     ctx->plan.release();
     ctx->d_tmpl.release(); ctx->d_tmpl8.release(); ctx->d_tsum.release(); ctx->d_src.release();
     ctx->d_op_a.release(); ctx->d_op_b.release(); ctx->d_op_job.release();
+    ctx->d_ov.release(); ctx->h_ov_in.release(); ctx->h_ov_out.release();
     for (auto& k : ctx->kp)
         for (auto& e : k.ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
     (void)hipStreamDestroy(ctx->stream);
@@ -1452,8 +1584,9 @@ int fpm_merge_candidates(const fpm_params* p, int32_t tmpl_w, int32_t tmpl_h, co
                          fpm_result* out, int32_t cap, int32_t* n_results) {
     if (!p || !n_results || tmpl_w <= 0 || tmpl_h <= 0 || n < 0 || (n > 0 && !cand)) return FPM_E_INVALID_ARG;
     *n_results = 0;
+    if (n >= 2048) host_pool_warm(2000);   // a large tail: the pool's workers awake for its parallel regions
     std::vector<fpm_result> res;
-    if (!merge_candidates(*p, tmpl_w, tmpl_h, cand, n, res)) return FPM_E_INVALID_ARG;
+    if (!merge_candidates(*p, tmpl_w, tmpl_h, cand, n, res, nullptr)) return FPM_E_INVALID_ARG;
     *n_results = (int32_t)res.size();
     for (int i = 0; i < (int)res.size() && i < cap && out; ++i) out[i] = res[i];
     return (int)res.size() > cap ? FPM_E_CAPACITY : FPM_OK;

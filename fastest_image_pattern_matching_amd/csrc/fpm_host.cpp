@@ -4,6 +4,7 @@
 // set and order are identical (TemplateMatcher.cpp:373-395, 984-1194) and the OpenCV geometry primitives
 // they call (OpenCV 4.5.x semantics).  Compile with -ffp-contract=off.
 #include "fpm_host.h"
+#include "fpm_rrect.h"
 
 #include <algorithm>
 #include <atomic>
@@ -11,6 +12,7 @@
 #include <cmath>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <functional>
 #include <mutex>
@@ -25,7 +27,7 @@ bool score_big2small(const HostMatch& a, const HostMatch& b) { return a.score > 
 
 // worker threads for the overlap filter's independent components: FPM_HOST_THREADS if set (>= 1), else the
 // hardware concurrency capped at 8
-static int host_threads() {
+int host_thread_count() {
     static const int n = [] {
         if (const char* e = std::getenv("FPM_HOST_THREADS")) {
             const int v = std::atoi(e);
@@ -59,15 +61,25 @@ struct Pool {
     const std::function<void(int)>* fn = nullptr;   // guarded by m; null between regions
     int ntasks = 0;
     std::atomic<int> next{0}, done{0}, active{0};
+    std::atomic<int64_t> spin_until{0};   // steady_clock ns: idle workers spin instead of sleeping until then
 
+    static int64_t now_ns() {
+        return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+            .count();
+    }
     void worker() {
         uint64_t seen = 0;
         for (;;) {
-            const auto t0 = std::chrono::steady_clock::now();
+            auto t0 = std::chrono::steady_clock::now();
             while (gen.load(std::memory_order_acquire) == seen) {
-                if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(300)) {
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(300) &&
+                    now_ns() >= spin_until.load(std::memory_order_relaxed)) {
                     std::unique_lock<std::mutex> lk(m);
-                    cv.wait(lk, [&] { return gen.load(std::memory_order_acquire) != seen; });
+                    cv.wait(lk, [&] {
+                        return gen.load(std::memory_order_acquire) != seen ||
+                               now_ns() < spin_until.load(std::memory_order_relaxed);
+                    });
+                    t0 = std::chrono::steady_clock::now();
                 } else {
                     cpu_relax();
                 }
@@ -103,8 +115,17 @@ Pool* pool_instance(int workers) {
 }
 }  // namespace
 
+void host_pool_warm(int us) {
+    const int nthreads = host_thread_count();
+    if (nthreads <= 1 || us <= 0) return;
+    Pool* p = pool_instance(nthreads - 1);
+    p->spin_until.store(Pool::now_ns() + (int64_t)us * 1000, std::memory_order_relaxed);
+    std::lock_guard<std::mutex> lk(p->m);
+    p->cv.notify_all();
+}
+
 void host_parallel(int ntasks, const std::function<void(int)>& fn) {
-    const int nthreads = host_threads();
+    const int nthreads = host_thread_count();
     if (ntasks <= 1 || nthreads <= 1) {
         for (int t = 0; t < ntasks; ++t) fn(t);
         return;
@@ -124,8 +145,12 @@ void host_parallel(int ntasks, const std::function<void(int)>& fn) {
         p->gen.fetch_add(1, std::memory_order_acq_rel);
     }
     p->cv.notify_all();
+    static const bool trace = [] { const char* e = std::getenv("FPM_POOL_TRACE"); return e && *e == '1'; }();
+    const auto r0 = std::chrono::steady_clock::now();
+    int mine = 0;
     for (int t = p->next.fetch_add(1); t < ntasks; t = p->next.fetch_add(1)) {
         fn(t);
+        ++mine;
         p->done.fetch_add(1, std::memory_order_acq_rel);
     }
     while (p->done.load(std::memory_order_acquire) < ntasks) cpu_relax();
@@ -134,6 +159,9 @@ void host_parallel(int ntasks, const std::function<void(int)>& fn) {
         p->fn = nullptr;   // workers that wake from here on skip this region
     }
     while (p->active.load(std::memory_order_acquire) > 0) cpu_relax();
+    if (trace)
+        fprintf(stderr, "pool region: %d tasks, %d by the caller, %.1f us\n", ntasks, mine,
+                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - r0).count());
 }
 
 static inline double len2(float x, float y) { return std::sqrt((double)x * x + (double)y * y); }
@@ -152,7 +180,7 @@ RRect rrect_from3(F2 p1, F2 p2, F2 p3) {
     return r;
 }
 
-static void rrect_corners(const RRect& r, F2 pt[4]) {
+void rrect_corners(const RRect& r, F2 pt[4]) {
     const double rad = r.angle * kPi / 180.;
     const float b = (float)std::cos(rad) * 0.5f;
     const float a = (float)std::sin(rad) * 0.5f;
@@ -162,96 +190,9 @@ static void rrect_corners(const RRect& r, F2 pt[4]) {
     pt[3] = f2(2 * r.c.x - pt[1].x, 2 * r.c.y - pt[1].y);
 }
 
-// returns 0 = INTERSECT_NONE, 1 = INTERSECT_PARTIAL, 2 = INTERSECT_FULL
-// on precomputed corners (rrect_corners of ra / rb), into a fixed array: at most 16 edge crossings + 8 corners
-// before the near-duplicate pass, at most 8 after it (cv::rotatedRectangleIntersection, OpenCV 4.5.x)
+// cv::rotatedRectangleIntersection on precomputed corners (fpm_rrect.h, shared with the device pair kernel)
 static int rrect_isect(const RRect& ra, const RRect& rb, const F2* A, const F2* B, F2* pts, int* np) {
-    int n = 0;
-    F2 eA[4], eB[4];
-    float eps = 1e-6f * std::max(ra.w * ra.h, rb.w * rb.h);
-    bool coincident = true;
-    for (int i = 0; i < 4 && coincident; ++i)
-        coincident = !(std::fabs(A[i].x - B[i].x) > eps || std::fabs(A[i].y - B[i].y) > eps);
-    if (coincident) {
-        for (int i = 0; i < 4; ++i) pts[i] = A[i];
-        *np = 4;
-        return 2;
-    }
-    for (int i = 0; i < 4; ++i) {
-        const int k = (i + 1) & 3;
-        eA[i] = f2(A[k].x - A[i].x, A[k].y - A[i].y);
-        eB[i] = f2(B[k].x - B[i].x, B[k].y - B[i].y);
-    }
-    for (int i = 0; i < 4; ++i) {
-        eps = std::min(eps, std::sqrt(eA[i].x * eA[i].x + eA[i].y * eA[i].y));
-        eps = std::min(eps, std::sqrt(eB[i].x * eB[i].x + eB[i].y * eB[i].y));
-    }
-    eps = std::max(1e-16f, eps);
-    int kind = 2;
-    // edge-edge crossings
-    for (int i = 0; i < 4; ++i) {
-        for (int j = 0; j < 4; ++j) {
-            const float dx = B[j].x - A[i].x, dy = B[j].y - A[i].y;
-            const float det = eB[j].x * eA[i].y - eA[i].x * eB[j].y;
-            if (std::fabs(det) < 1e-12) continue;
-            const float ta = (eB[j].x * dy - eB[j].y * dx) / det;
-            const float tb = (eA[i].x * dy - eA[i].y * dx) / det;
-            if (!std::isfinite(ta) || !std::isfinite(tb)) continue;
-            if (ta >= 0.0f && ta <= 1.0f && tb >= 0.0f && tb <= 1.0f)
-                pts[n++] = f2(A[i].x + eA[i].x * ta, A[i].y + eA[i].y * ta);
-        }
-    }
-    if (n > 0) kind = 1;
-    // corners of one rectangle inside the other (sign test against the 4 edge lines)
-    auto inside = [](const F2& p, const F2* Q, const F2* eQ) {
-        int pos = 0, neg = 0;
-        for (int j = 0; j < 4; ++j) {
-            const float a = -eQ[j].y, b = eQ[j].x;
-            const float c = -(a * Q[j].x + b * Q[j].y);
-            const float s = a * p.x + b * p.y + c;
-            if (s >= 0) ++pos; else ++neg;
-        }
-        return pos == 4 || neg == 4;
-    };
-    for (int i = 0; i < 4; ++i)
-        if (inside(A[i], B, eB)) pts[n++] = A[i];
-    for (int i = 0; i < 4; ++i)
-        if (inside(B[i], A, eA)) pts[n++] = B[i];
-    if (n == 0) { *np = 0; return 0; }
-    // drop near-duplicates (swap-with-last), remembering pairwise distances for the > 8 pass
-    const int stride = n;
-    float dist[24 * 24];
-    int slot[24];
-    for (int i = 0; i < n * n; ++i) dist[i] = 0.f;
-    for (int i = 0; i < n; ++i) {
-        slot[i] = i;
-        const F2 p = pts[i];
-        int j = i + 1;
-        while (j < n) {
-            const float ddx = pts[j].x - p.x, ddy = pts[j].y - p.y;
-            const float d2 = ddx * ddx + ddy * ddy;
-            if (d2 <= eps) {
-                if (j < n - 1) pts[j] = pts[n - 1];
-                --n;
-                continue;
-            }
-            dist[(size_t)i * stride + j] = d2;
-            ++j;
-        }
-    }
-    while (n > 8) {
-        int bj = 1;
-        float bd = dist[1];
-        for (int i = 0; i < n - 1; ++i) {
-            const float* row = dist + (size_t)stride * slot[i];
-            for (int j = i + 1; j < n; ++j)
-                if (row[slot[j]] < bd) { bd = row[slot[j]]; bj = j; }
-        }
-        if (bj < n - 1) { pts[bj] = pts[n - 1]; slot[bj] = slot[n - 1]; }
-        --n;
-    }
-    *np = n;
-    return kind;
+    return rrect_isect_pts(ra.w, ra.h, rb.w, rb.h, A, B, pts, np);
 }
 
 int rrect_intersection(const RRect& ra, const RRect& rb, std::vector<F2>& pts) {
@@ -339,18 +280,25 @@ void sort_pt_with_center_keyed(std::vector<F2>& pts) {
     if (!pts.empty()) sort_pts_keyed(pts.data(), (int)pts.size());
 }
 
-static double contour_area_a(const F2* pts, int n) {
-    if (n == 0) return 0.;
-    double acc = 0;
-    F2 prev = pts[n - 1];
-    for (int i = 0; i < n; ++i) {
-        acc += (double)prev.x * pts[i].y - (double)prev.y * pts[i].x;
-        prev = pts[i];
-    }
-    return std::fabs(acc * 0.5);
-}
+static double contour_area_a(const F2* pts, int n) { return contour_area_pts(pts, n); }
 
 double contour_area(const std::vector<F2>& pts) { return contour_area_a(pts.data(), (int)pts.size()); }
+
+// filterWithRotatedRect's decision for one pair (pair_del below, without the score rule): does a's overlap with b
+// exceed max_overlap (ratio to a's area)
+bool rrect_pair_drops(const RRect& ra, const RRect& rb, double max_overlap) {
+    F2 A[4], B[4], p[24];
+    rrect_corners(ra, A);
+    rrect_corners(rb, B);
+    int np = 0;
+    const int kind = rrect_isect(ra, rb, A, B, p, &np);
+    if (kind == 0) return false;
+    if (kind == 2) return true;
+    if (np < 3) return false;
+    sort_pts_center(p, np);
+    return contour_area_a(p, np) / (ra.w * ra.h) > max_overlap;
+}
+
 
 void filter_with_score(std::vector<HostMatch>& v, double score) {
     // std::sort's permutation depends only on the comparison results, so sorting light (score, index) keys with
@@ -370,6 +318,11 @@ void filter_with_score(std::vector<HostMatch>& v, double score) {
 void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
     if (v.empty()) return;
     const int n = (int)v.size();
+    // FPM_TAIL_TIMES=1: phase clocks on stderr (profiling aid)
+    static const bool tail_times = [] { const char* e = std::getenv("FPM_TAIL_TIMES"); return e && *e == '1'; }();
+    using clk = std::chrono::steady_clock;
+    const clk::time_point q0 = clk::now();
+    clk::time_point q1 = q0, q2 = q0, q3 = q0;
     // corner bounding boxes: pairs whose boxes are > 1 px apart cannot have an edge crossing or a contained corner,
     // so rrect_intersection would return INTERSECT_NONE; skipping them keeps the reference's O(n^2) loop order
     // and deletions exactly while avoiding the exact test for far-apart detections
@@ -389,6 +342,7 @@ void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
     };
     if (n <= 512) geom(0, n);
     else host_parallel((n + 511) / 512, [&](int t) { geom(t * 512, std::min(n, t * 512 + 512)); });
+    q1 = clk::now();
     // the reference's inner-loop body for (i, j), boxes overlapping: the index it deletes, or -1
     auto pair_del = [&](int i, int j) {
         F2 pts[24];
@@ -484,6 +438,7 @@ void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
         std::vector<int> local(n);
         for (int c = 0; c < ncomp; ++c)
             for (int k = comp_off[c]; k < comp_off[c + 1]; ++k) local[members[k]] = k - comp_off[c];
+        q2 = clk::now();
         auto run_comp = [&](int c, std::vector<int>& nb, std::vector<char>& del) {
             const int m0 = comp_off[c], m1 = comp_off[c + 1];
             del.assign(m1 - m0, 0);
@@ -520,6 +475,12 @@ void filter_with_rotated_rect(std::vector<HostMatch>& v, double max_overlap) {
                 run_comp(c, nb, del);
             });
         }
+        q3 = clk::now();
+        if (tail_times)
+            fprintf(stderr, "overlap n=%d comps=%d geom %.3f grid+comps %.3f tests %.3f ms\n", n, ncomp,
+                    std::chrono::duration<double, std::milli>(q1 - q0).count(),
+                    std::chrono::duration<double, std::milli>(q2 - q1).count(),
+                    std::chrono::duration<double, std::milli>(q3 - q2).count());
     }
     v.erase(std::remove_if(v.begin(), v.end(), [](const HostMatch& m) { return m.del; }), v.end());
 }
@@ -553,7 +514,7 @@ static bool invert_lu(std::vector<double> a, int n, std::vector<double>& inv) {
     return true;
 }
 
-void subpix_estimation(const std::vector<HostMatch>& v, double* dx, double* dy, double* dangle, double angle_step,
+void subpix_estimation(const HostMatch* v, double* dx, double* dy, double* dangle, double angle_step,
                        int imax) {
     double A[27][10], S[27];
     const double x0 = v[imax].ptx, y0 = v[imax].pty, t0 = v[imax].angle;

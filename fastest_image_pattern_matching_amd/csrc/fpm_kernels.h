@@ -200,6 +200,21 @@ size_t roi_small_lds(int tw, int th);
 void launch_roi_small(const RoiArgs& a, hipStream_t st);
 void launch_cand_step(const RoiArgs& a, int max_items, hipStream_t st);
 void launch_pack(const PackArgs& a, hipStream_t st);
+
+// ---- filterWithRotatedRect's pair decisions on the device (TemplateMatcher.cpp:1133-1194) ----
+// One result's rotated rectangle: its corners (rrect corners, host-computed from the cv::RotatedRect) and size; its
+// corner box widened by 1 px (the host's prefilter: boxes farther apart cannot intersect) in a separate float4 array
+// (x0, y0, x1, y1), which the all-pairs sweep reads.
+struct OvRect { F2 c[4]; float w, h; };
+constexpr int kOverlapMaxCand = 512;   // overlapping partners of one rectangle decided on the device
+// For every pair i < j of the n rectangles (sorted as the filter sees them) whose boxes overlap, the exact
+// rotatedRectangleIntersection + sortPtWithCenter + area test (fpm_rrect.h); the j of every pair whose overlap
+// exceeds max_overlap are written, ascending, to lists[off[i] .. off[i] + cnt[i]) (offcnt[2i], offcnt[2i+1]), as ~j
+// when the point order depends on acos (the host decides that pair).  meta[0] = entries written (atomic allocator,
+// zeroed by the caller), meta[1] bit 0 = more than kOverlapMaxCand overlapping partners, bit 1 = list full.
+// lists / offcnt may be mapped host memory (plain stores only); meta must be device memory.
+void launch_overlap_pairs(const OvRect* r, const float4* box, int n, double max_overlap, int32_t* lists, int list_cap,
+                          int32_t* offcnt, int32_t* meta, hipStream_t st);
 int roi_pick_rc(int tw, int th);
 int roi_pitch_for(int tw);
 int roi_tab_rows(int th);   // rows of a ROI's X0 / Y0 tables: th + 6 rounded up to a 32-row tile

@@ -23,6 +23,7 @@
 #include <utility>
 
 #include "fpm_kernels.h"
+#include "fpm_rrect.h"
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) is per device: remember, per (device, kernel), the largest dynamic
 // LDS already allowed, under a mutex (contexts on several devices / host threads launch concurrently)
@@ -3581,6 +3582,94 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
 
 void launch_pack(const PackArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_pack, dim3(16), dim3(256), 0, st, a);
+}
+
+// ---- filterWithRotatedRect pair decisions (launch_overlap_pairs).  One wave per rectangle i: the lanes sweep j > i in
+// chunks of 64 with the box prefilter and compact the overlapping partners into the wave's LDS list (ballot + prefix,
+// ascending j), then run the exact pair test on them 64 at a time; one atomic per wave reserves the output range.
+__global__ __launch_bounds__(256) void k_overlap_pairs(const OvRect* __restrict__ r, const float4* __restrict__ box,
+                                                       int n, double max_overlap, int32_t* lists, int list_cap,
+                                                       int32_t* offcnt, int32_t* meta) {
+    __shared__ int32_t cand[4][kOverlapMaxCand];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int i = blockIdx.x * 4 + wv; i < n; i += gridDim.x * 4) {
+        const OvRect ri = r[i];
+        const float4 bi = box[i];
+        int nc = 0;   // wave-uniform
+        bool over = false;
+        for (int j0 = i + 1; j0 < n; j0 += 64) {
+            const int j = j0 + lane;
+            bool ov = false;
+            if (j < n) {
+                const float4 bj = box[j];
+                ov = !(bj.x > bi.z || bj.z < bi.x || bj.y > bi.w || bj.w < bi.y);
+            }
+            const uint64_t m = __ballot(ov);
+            const int c = __popcll(m);
+            if (nc + c > kOverlapMaxCand) { over = true; break; }
+            if (ov) cand[wv][nc + __popcll(m & below)] = j;
+            nc += c;
+        }
+        if (over) {
+            if (lane == 0) atomicOr(&meta[1], 1);
+            if (lane == 0) { offcnt[2 * i] = 0; offcnt[2 * i + 1] = 0; }
+            continue;
+        }
+        __builtin_amdgcn_wave_barrier();
+        // exact tests: lane k of round t decides partner cand[64 t + k]; verdicts replace the entries (j: drop, ~j:
+        // undecided, INT_MIN: no drop)
+        for (int k0 = 0; k0 < nc; k0 += 64) {
+            const int k = k0 + lane;
+            if (k < nc) {
+                const int j = cand[wv][k];
+                const OvRect rj = r[j];
+                F2 pts[24];
+                int np = 0;
+                const int kind = rrect_isect_pts(ri.w, ri.h, rj.w, rj.h, ri.c, rj.c, pts, &np);
+                int verdict = INT_MIN;
+                if (kind == 2) {
+                    verdict = j;
+                } else if (kind == 1 && np >= 3) {
+                    if (!sort_pts_fast(pts, np)) verdict = ~j;
+                    else if (contour_area_pts(pts, np) / (ri.w * ri.h) > max_overlap) verdict = j;
+                }
+                cand[wv][k] = verdict;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        // compact the drops / undecided pairs (ascending j) into the output
+        int nd = 0;
+        for (int k0 = 0; k0 < nc; k0 += 64) {
+            const int k = k0 + lane;
+            const bool keep = k < nc && cand[wv][k] != INT_MIN;
+            nd += __popcll(__ballot(keep));
+        }
+        int base = 0;
+        if (lane == 0 && nd > 0) base = atomicAdd(&meta[0], nd);
+        base = __shfl(base, 0, 64);
+        if (base + nd > list_cap) {
+            if (lane == 0) { atomicOr(&meta[1], 2); offcnt[2 * i] = 0; offcnt[2 * i + 1] = 0; }
+            continue;
+        }
+        int w = 0;
+        for (int k0 = 0; k0 < nc; k0 += 64) {
+            const int k = k0 + lane;
+            const bool keep = k < nc && cand[wv][k] != INT_MIN;
+            const uint64_t m = __ballot(keep);
+            if (keep) lists[base + w + __popcll(m & below)] = cand[wv][k];
+            w += __popcll(m);
+        }
+        if (lane == 0) { offcnt[2 * i] = base; offcnt[2 * i + 1] = nd; }
+    }
+}
+
+void launch_overlap_pairs(const OvRect* r, const float4* box, int n, double max_overlap, int32_t* lists, int list_cap,
+                          int32_t* offcnt, int32_t* meta, hipStream_t st) {
+    if (n <= 0) return;
+    const int grid = std::min((n + 3) / 4, 65535);
+    hipLaunchKernelGGL(k_overlap_pairs, dim3(grid), dim3(256), 0, st, r, box, n, max_overlap, lists, list_cap, offcnt,
+                       meta);
 }
 
 }  // namespace fpm

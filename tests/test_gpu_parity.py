@@ -275,14 +275,29 @@ def test_blockmax_fallback_paths(hip, templates, prm):
     assert_same_results(gpu, orc, f"blockmax_{prm}")
 
 
-def test_config2_src10_rotation_sweep(hip, templates):
-    """configs[2] stress (+-180 deg, 47 top angles, TargetNum 100) on the 1824x1824 top-left quarter."""
+@pytest.mark.parametrize("overlap_on_device", [False, True])
+def test_config2_src10_rotation_sweep(hip, templates, monkeypatch, overlap_on_device):
+    """configs[2] stress (+-180 deg, 47 top angles, TargetNum 100) on the 1824x1824 top-left quarter; with the
+    overlap filter's pair tests forced onto the device (FPM_OVERLAP_DEVICE_MIN=1) and on the host."""
+    monkeypatch.setenv("FPM_OVERLAP_DEVICE_MIN", "1" if overlap_on_device else "1000000000")
     s, t = synth.src10_scene(templates["Dst10"])
     crop = np.ascontiguousarray(s[:1824, :1824])
     gpu, orc, ostats, gstats = _run_both(hip, crop, t, max_pos=100, score=0.7, tolerance_angle=180.0)
     assert gstats == ostats
     assert_same_results(gpu, orc, "src10_180")
     assert len(orc) >= 30
+
+
+def test_config2_src10_full_rotation_sweep(hip, templates):
+    """configs[2] stress at full size (3648x3648, +-180 deg, TargetNum 100: ~4900 top candidates, whose overlap
+    filter runs its pair tests on the device by default) equal to the oracle."""
+    s, t = synth.src10_scene(templates["Dst10"])
+    gpu, orc, ostats, gstats = _run_both(hip, np.ascontiguousarray(s), t, max_pos=100, score=0.7,
+                                         tolerance_angle=180.0)
+    assert gstats == ostats
+    assert gstats[1] >= 1024
+    assert_same_results(gpu, orc, "src10_180_full")
+    assert len(orc) >= 100
 
 
 def test_config3_batch_4096(hip):
