@@ -205,13 +205,18 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(d_live3, live3.data(), 4 * C3, hipMemcpyHostToDevice));
         CK(hipMemcpy(d_cnt3, &C3, 4, hipMemcpyHostToDevice));
         b.state = d_st3; b.live = d_live3; b.live_count = d_cnt3;
-        b.slot_cap = 7872;   // the product's plan capacity for this batch (most WGs find no ROI)
+        // records of this section's C3 x n3 ROIs (k_roi_small writes rec[id * n3 + j]; the layer-0 section's buffer
+        // holds C x n3 only -- sharing it overran that allocation, which faulted the GPU at MB_NSRC=43)
+        RoiRecord* d_rec3;
+        CK(hipMalloc(&d_rec3, sizeof(RoiRecord) * (size_t)C3 * n3));
+        b.rec = d_rec3;
+        b.slot_cap = std::max(7872, C3 * n3);   // the product's plan capacity for the 8-source batch (most WGs idle)
         const size_t lds = roi_small_lds(TW3, TH3);
         printf("small L3: rois %d lds %zu\n", C3 * n3, lds);
         timeit([&] { launch_roi_small(b, 0); }, "small prod");
-        timeit([&] { hipLaunchKernelGGL(k_roi_small<1>, dim3(7872), dim3(256), lds, 0, b); }, "small sample only");
-        timeit([&] { hipLaunchKernelGGL(k_roi_small<2>, dim3(7872), dim3(256), lds, 0, b); }, "small +sums");
-        timeit([&] { hipLaunchKernelGGL(k_roi_small<3>, dim3(7872), dim3(256), lds, 0, b); }, "small +bands nofold");
+        timeit([&] { hipLaunchKernelGGL(k_roi_small<1>, dim3(b.slot_cap), dim3(256), lds, 0, b); }, "small sample only");
+        timeit([&] { hipLaunchKernelGGL(k_roi_small<2>, dim3(b.slot_cap), dim3(256), lds, 0, b); }, "small +sums");
+        timeit([&] { hipLaunchKernelGGL(k_roi_small<3>, dim3(b.slot_cap), dim3(256), lds, 0, b); }, "small +bands nofold");
         timeit([&] { hipLaunchKernelGGL(k_roi_small<0>, dim3(C3 * n3), dim3(256), lds, 0, b); }, "small exact grid");
         timeit([&] { hipLaunchKernelGGL(k_roi_small<5>, dim3(C3 * n3), dim3(256), lds, 0, b); }, "small byte-gather taps");
         {   // per-phase s_memtime stamps of the first 64 workgroups
