@@ -251,20 +251,23 @@ __global__ __launch_bounds__(256) void k_pyr_down(const uint8_t* __restrict__ sr
 // filtered and stored, so every workgroup keeps its loads in flight for its whole life instead of one burst per
 // tile (the one-tile form above reaches 3.2-4.2 TB/s: its workgroups wait for their single burst).  Same integer
 // arithmetic as k_pyr_down, exact.
-constexpr int PS_NL = (PD_IH * (PD_IW / 16) + 255) / 256;   // 16-byte loads per thread for a 68-row window: 5
 typedef unsigned short fpm_u16x2 __attribute__((ext_vector_type(2)));
 
+// OH: output rows per chunk (window 2 OH + 4 input rows; 16-byte loads per thread for it: 5 at OH 32, 3 at OH 16)
+template <int OH>
 __global__ __launch_bounds__(256) void k_pyr_down_s(const uint8_t* __restrict__ src0, int sw, int sh, int sp,
                                                     size_t s_img, uint8_t* __restrict__ dst0, int dw, int dh,
                                                     int dp, size_t d_img, int nimg, int32_t* zero, int nzero) {
-    __shared__ __attribute__((aligned(16))) uint8_t tin[PD_IH][PD_IW];
+    constexpr int IH = 2 * OH + 4;
+    constexpr int PS_NL = (IH * (PD_IW / 16) + 255) / 256;
+    __shared__ __attribute__((aligned(16))) uint8_t tin[IH][PD_IW];
     if (blockIdx.x == 0)
         for (int i = threadIdx.x; i < nzero; i += 256) zero[i] = 0;
-    __shared__ __attribute__((aligned(16))) uint16_t hs[PD_IH][PD_OW];
+    __shared__ __attribute__((aligned(16))) uint16_t hs[IH][PD_OW];
     // work units = (image, strip, chunk) in row-major order; workgroup w takes the contiguous range
     // [U*w/G, U*(w+1)/G) (equal shares: no tail round of a few workgroups), split where it crosses a strip; XCD
     // groups take contiguous ranges of workgroups (neighbouring strips share the halo columns' lines)
-    const int gx = (dw + PD_OW - 1) / PD_OW, chunks = (dh + PD_OH - 1) / PD_OH;
+    const int gx = (dw + PD_OW - 1) / PD_OW, chunks = (dh + OH - 1) / OH;
     const long U = (long)gx * chunks * nimg;
     const int w = xcd_remap(blockIdx.x, gridDim.x);
     long u = U * w / gridDim.x;
@@ -279,7 +282,7 @@ __global__ __launch_bounds__(256) void k_pyr_down_s(const uint8_t* __restrict__ 
         const uint8_t* src = src0 + (size_t)bz * s_img;
         uint8_t* dst = dst0 + (size_t)bz * d_img;
         const int ox0 = bx * PD_OW;
-        const int oy_begin = c0 * PD_OH, oy_end = min(dh, (c0 + run) * PD_OH);
+        const int oy_begin = c0 * OH, oy_end = min(dh, (c0 + run) * OH);
         __syncthreads();   // the previous run is done with tin / hs
         const int ix0 = 2 * ox0 - 16;     // tin column 0 <-> source column ix0 (16-byte aligned)
         constexpr int Q = PD_IW / 16;     // 18 uint4 per row
@@ -311,10 +314,10 @@ __global__ __launch_bounds__(256) void k_pyr_down_s(const uint8_t* __restrict__ 
         // columns outside [0, sw) that an output of this strip reads (at most 2 on each side): reflect-101
         const int xlo = 2 * ox0 - 2, xhi = min(2 * (ox0 + PD_OW - 1) + 2, 2 * (dw - 1) + 2);
         const bool edge = xlo < 0 || xhi >= sw;   // uniform per workgroup
-        issue(2 * oy_begin - 2, PD_IH);
-        for (int oyc = oy_begin; oyc < oy_end; oyc += PD_OH) {
+        issue(2 * oy_begin - 2, IH);
+        for (int oyc = oy_begin; oyc < oy_end; oyc += OH) {
             const bool first = oyc == oy_begin;
-            const int roff = first ? 0 : 4, nrows = first ? PD_IH : 2 * PD_OH;
+            const int roff = first ? 0 : 4, nrows = first ? IH : 2 * OH;
             const int iy = 2 * oyc - 2 + roff;
             commit(roff, nrows);
             if (edge) {
@@ -328,7 +331,7 @@ __global__ __launch_bounds__(256) void k_pyr_down_s(const uint8_t* __restrict__ 
             }
             __syncthreads();
             // the next chunk's 64 new input rows (its window rows 4..67) are in flight while this chunk is filtered
-            if (oyc + PD_OH < oy_end) issue(2 * oyc + 2 * PD_OH + 2, 2 * PD_OH);
+            if (oyc + OH < oy_end) issue(2 * oyc + 2 * OH + 2, 2 * OH);
             // horizontal [1 4 6 4 1] of the new window rows: 4 consecutive outputs per item (as k_pyr_down; the 5th tap
             // enters the v_dot4 as its accumulator)
             const int nh = nrows * (PD_OW / 4);
@@ -350,7 +353,7 @@ __global__ __launch_bounds__(256) void k_pyr_down_s(const uint8_t* __restrict__ 
             // a horizontal sum is <= 16 * 255, so 128 + sum_t k_t * h_t <= 65408 fits 16 bits, and (v >> 8) is the
             // half's high byte, gathered by one v_perm
 #pragma unroll
-            for (int k = 0; k < PD_OH * (PD_OW / 4) / 256; ++k) {
+            for (int k = 0; k < OH * (PD_OW / 4) / 256; ++k) {
                 const int i = tid + 256 * k;
                 const int orow = i / (PD_OW / 4), g = i - orow * (PD_OW / 4);
                 const int oy = oyc + orow, ox = ox0 + 4 * g;
@@ -373,8 +376,8 @@ __global__ __launch_bounds__(256) void k_pyr_down_s(const uint8_t* __restrict__ 
                 }
             }
             __syncthreads();
-            // carry: window rows 64..67 (input rows 2 * (oyc + PD_OH) - 2 .. + 1) are the next window's rows 0..3
-            ((uint32_t*)hs[tid >> 6])[tid & 63] = ((uint32_t*)hs[2 * PD_OH + (tid >> 6)])[tid & 63];
+            // carry: window rows 2 OH .. 2 OH + 3 (input rows 2 * (oyc + OH) - 2 .. + 1) are the next window's rows 0..3
+            ((uint32_t*)hs[tid >> 6])[tid & 63] = ((uint32_t*)hs[2 * OH + (tid >> 6)])[tid & 63];
             __syncthreads();
         }
     }
@@ -384,17 +387,26 @@ static const int kPyrWGs = [] {   // FPM_PYR_WGS: profiling override
     const char* e = getenv("FPM_PYR_WGS");
     return e && atoi(e) > 0 ? atoi(e) : 4096;
 }();
+static const int kPyrOH = [] {   // FPM_PYR_OH (16 or 32): profiling override of the chunk height
+    const char* e = getenv("FPM_PYR_OH");
+    return e && atoi(e) == 16 ? 16 : 32;
+}();
 void launch_pyr_down(const uint8_t* src, int sw, int sh, int sp, size_t s_img, uint8_t* dst, int dw, int dh,
                      int dp, size_t d_img, int nimg, hipStream_t st, int seg_chunks, int32_t* zero, int nzero) {
     // equal shares of the (image, strip, chunk) units over kPyrWGs workgroups (4 rounds of 4 per CU; measured
     // 2048 / 4096 / 8192: 37.1 / 35.7 / 36.0 µs per launch averaged over the Src7 levels), or
     // seg_chunks units each
     if (dw <= 0 || dh <= 0 || nimg <= 0) return;
-    const int gx = (dw + PD_OW - 1) / PD_OW, chunks = (dh + PD_OH - 1) / PD_OH;
+    const int oh = kPyrOH;
+    const int gx = (dw + PD_OW - 1) / PD_OW, chunks = (dh + oh - 1) / oh;
     const long units = (long)gx * chunks * nimg;
     const long g = seg_chunks > 0 ? (units + seg_chunks - 1) / seg_chunks : std::min(units, (long)kPyrWGs);
-    hipLaunchKernelGGL(k_pyr_down_s, dim3((unsigned)g), dim3(256), 0, st, src, sw, sh, sp, s_img, dst, dw, dh, dp,
-                       d_img, nimg, zero, nzero);
+    if (oh == 16)
+        hipLaunchKernelGGL(k_pyr_down_s<16>, dim3((unsigned)g), dim3(256), 0, st, src, sw, sh, sp, s_img, dst, dw, dh,
+                           dp, d_img, nimg, zero, nzero);
+    else
+        hipLaunchKernelGGL(k_pyr_down_s<32>, dim3((unsigned)g), dim3(256), 0, st, src, sw, sh, sp, s_img, dst, dw, dh,
+                           dp, d_img, nimg, zero, nzero);
 }
 
 // ============================================================================================== K2
@@ -2307,6 +2319,147 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
+// ---- K6b over a candidate's three angle ROIs at once (n3 == 3): the three ROIs of one candidate sample nearly the
+// same source region (their angles differ by the layer's angle step, a fraction of a degree), so a task is one tile
+// position of all three: their footprint boxes' union is staged into LDS once (when it fits the wave's buffer) and
+// the three tiles are sampled from it one after the other -- the same taps, addressed from the union's origin, so
+// the same bytes as k_roi_warp.  A union that does not fit falls back to staging each ROI's own box.
+template <int FB, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_warp3(RoiArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t ft_all[4 * ROI_FT + 16];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t* FT = ft_all + wv * ROI_FT;
+    const int RW = a.tw + 6, RH = a.th + 6, W = a.W, H = a.H;
+    const int txn = (RW + ROI_T - 1) / ROI_T, tyn = (RH + ROI_T - 1) / ROI_T;
+    const int per_roi = txn * tyn;
+    const int tasks = roi_count(a) / 3 * per_roi;
+    const int lr = lane >> 3, lg = lane & 7;
+    const XcdSplit xs = xcd_split(tasks);
+    const int tstride = xs.nk * 4;
+    const uint32_t st_lane = 4u * lg + 32u * lr;
+    constexpr int ftw = kFtPitch;
+    for (int task = xs.lo + xs.k * 4 + wv; task < xs.hi; task += tstride) {
+        const int cand = task / per_roi;
+        const int rem = task - cand * per_roi;
+        const int ty = rem / txn, tx = rem - ty * txn;
+        const int cx0 = tx * ROI_T, cx1 = min(cx0 + ROI_T, RW) - 1;
+        const int ry0 = ty * ROI_T, ry1 = min(ry0 + ROI_T, RH) - 1;
+        const int c0 = cx0 + 4 * lg;
+        int bx[3], by[3], wp[3], fh[3], fl[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int4 d = a.tdesc[(size_t)(3 * cand + j) * a.tdesc_stride + rem];
+            bx[j] = __builtin_amdgcn_readfirstlane(d.x);
+            by[j] = __builtin_amdgcn_readfirstlane(d.y);
+            const int dz = __builtin_amdgcn_readfirstlane(d.z);
+            wp[j] = dz & 0xffff;
+            fh[j] = dz >> 16;
+            fl[j] = __builtin_amdgcn_readfirstlane(d.w);
+        }
+        const uint8_t* lvl = a.level + (size_t)(fl[0] >> kTileSrcShift) * a.level_stride;   // one candidate, one source
+        // union of the boxes that stage into LDS
+        int ux0 = INT_MAX, uy0 = INT_MAX, ux1 = INT_MIN, uy1 = INT_MIN;
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            if ((fl[j] & kTileAny) && (fl[j] & kTileLds)) {
+                ux0 = min(ux0, bx[j]); uy0 = min(uy0, by[j]);
+                ux1 = max(ux1, bx[j] + 4 * wp[j]); uy1 = max(uy1, by[j] + fh[j]);
+            }
+        const bool any_lds = ux0 != INT_MAX;
+        const int uwpr = any_lds ? (ux1 - ux0) >> 2 : 0, ufth = any_lds ? uy1 - uy0 : 0;
+        const bool uni = any_lds && uwpr <= 16 && kFtPitch * ufth <= ROI_FT;
+        if (uni) {
+            wave_sync();   // previous task's gathers are done with FT
+            stage_footprint32<FB, kFtPitch>(FT, uwpr, ufth, lvl + (size_t)uy0 * a.P + ux0, a.P, lane);
+            wave_sync();
+        }
+#pragma unroll 1
+        for (int j = 0; j < 3; ++j) {
+            const int slot = 3 * cand + j;
+            const int flags = fl[j];
+            const bool in_lds = (flags & kTileLds) != 0;
+            int bxa = bx[j], by0 = by[j];
+            if (uni) {
+                bxa = ux0; by0 = uy0;
+            } else {
+                wave_sync();
+                if ((flags & kTileAny) && in_lds)
+                    stage_footprint32<FB, kFtPitch>(FT, wp[j], fh[j], lvl + (size_t)by0 * a.P + bxa, a.P, lane);
+                wave_sync();
+            }
+            const int32_t* tb = a.tab + (size_t)slot * 2 * (a.tabw + a.tabh);
+            const int cc = min(c0, cx1 & ~3);
+            const int4 A = ld_at<int4>(tb, 4u * cc);
+            const int4 B = ld_at<int4>(tb, 4u * (a.tabw + cc));
+            const int adv[4] = {A.x, A.y, A.z, A.w}, bdv[4] = {B.x, B.y, B.z, B.w};
+            const int4 X4 = ld_at<int4>(tb, 4u * (2 * a.tabw + ry0 + 4 * lr));
+            const int4 Y4 = ld_at<int4>(tb, 4u * (2 * a.tabw + a.tabh + ry0 + 4 * lr));
+            const int X0r[4] = {X4.x, X4.y, X4.z, X4.w}, Y0r[4] = {Y4.x, Y4.y, Y4.z, Y4.w};
+            uint8_t* tile = a.roi + (size_t)slot * a.roi_stride + ((size_t)rem << 10);
+            if (c0 > cx1) continue;
+            if ((flags & kTileInterior) && in_lds) {
+                const int nvalid = RW - c0;
+                const uint32_t colmask = nvalid >= 4 ? 0xffffffffu : (1u << (8 * nvalid)) - 1u;
+                const int xo = ((int)lds_offset_of(FT) - bxa) << kAbBits, yo = -(by0 << kAbBits);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int x0r = X0r[i] + xo, y0r = Y0r[i] + yo;
+                    uint32_t off[4];
+                    int fxv[4], fyv[4], v[4][4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int sxv = x0r + adv[u], syv = y0r + bdv[u];
+                        fxv[u] = __builtin_amdgcn_ubfe(sxv, kAbBits - kInterBits, kInterBits);
+                        fyv[u] = __builtin_amdgcn_ubfe(syv, kAbBits - kInterBits, kInterBits);
+                        off[u] = (uint32_t)mad24(syv >> kAbBits, ftw, sxv >> kAbBits);
+                    }
+                    lds_taps16<kFtPitch>(off, v);
+                    const uint32_t pk = bilerp_row4(v, fxv, fyv);
+                    if (ry0 + lr + 8 * i <= ry1) st_at<uint32_t>(tile, st_lane + 256u * i, pk & colmask);
+                }
+                continue;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (ry0 + lr + 8 * i > ry1) break;
+                uint32_t pk = 0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int X = (X0r[i] + adv[u]) >> (kAbBits - kInterBits);
+                    const int Y = (Y0r[i] + bdv[u]) >> (kAbBits - kInterBits);
+                    int v;
+                    if (in_lds) {
+                        const int sx = sat_s16(X >> kInterBits), sy = sat_s16(Y >> kInterBits);
+                        const int fx = X & (kInterTab - 1), fy = Y & (kInterTab - 1);
+                        const uint8_t* p = FT + (sy - by0) * ftw + (sx - bxa);
+                        int v0, v1, v2, v3;
+                        if ((unsigned)sx < (unsigned)(W - 1) && (unsigned)sy < (unsigned)(H - 1)) {
+                            v0 = p[0]; v1 = p[1]; v2 = p[ftw]; v3 = p[ftw + 1];
+                        } else if (sx >= W || sx + 1 < 0 || sy >= H || sy + 1 < 0) {
+                            v0 = v1 = v2 = v3 = 0;
+                        } else {
+                            const bool x0 = sx >= 0 && sx < W, x1 = sx + 1 >= 0 && sx + 1 < W;
+                            const bool y0 = sy >= 0 && sy < H, y1 = sy + 1 >= 0 && sy + 1 < H;
+                            v0 = x0 && y0 ? p[0] : 0;
+                            v1 = x1 && y0 ? p[1] : 0;
+                            v2 = x0 && y1 ? p[ftw] : 0;
+                            v3 = x1 && y1 ? p[ftw + 1] : 0;
+                        }
+                        const int h0 = 32 * v0 + fx * (v1 - v0), h1 = 32 * v2 + fx * (v3 - v2);
+                        v = (32 * h0 + fy * (h1 - h0) + 512) >> 10;
+                    } else {
+                        v = roi_tap(lvl, W, H, a.P, X, Y);
+                    }
+                    if (c0 + u >= RW) v = 0;
+                    pk |= (uint32_t)v << (8 * u);
+                }
+                st_at<uint32_t>(tile, st_lane + 256u * i, pk);
+            }
+        }
+    }
+}
+
 // ---- K7: per-row exact correlation on the matrix cores.  For one ROI, the 49 per-row dot products
 // R[t][dy][dx] = sum_c T[t][c] * I[t+dy][c+dx] (IM_Conv_SIMD's int32 row results, TemplateMatcher.cpp:487-512)
 // are, for each shift dx, a banded GEMM  D_dx[t][s] = sum_c T[t][c] * I[s][c+dx]  kept where 0 <= s - t < 7:
@@ -3457,6 +3610,19 @@ void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
     if (tiles > INT_MAX) return;   // the engine bounds slot_cap far below this
     const long want = (tiles + 3) / 4;
     const int grid = (int)(want < 16384 ? want : 16384);
+    // a candidate's three angle ROIs from one staged union footprint (k_roi_warp3; Src7 kernel pass at 43 sources:
+    // layer 0 395 -> 329 us, layer 1 114 -> 99, bench 28.07k -> 29.62k searches/s, profiles/r03_r); FPM_WARP3=0 keeps
+    // one ROI per task (measurement)
+    static const int warp3 = [] {
+        const char* e = getenv("FPM_WARP3");
+        return e ? atoi(e) : 1;
+    }();
+    if (warp3 && a.n3 == 3 && a.slot_base % 3 == 0 && a.slot_cap % 3 == 0) {
+        const long want3 = (tiles / 3 + 3) / 4;
+        hipLaunchKernelGGL((k_roi_warp3<kWarpFootBatch, kWarpWaves>), dim3((int)(want3 < 16384 ? want3 : 16384)),
+                           dim3(256), 0, st, a);
+        return;
+    }
     hipLaunchKernelGGL((k_roi_warp<kWarpFootBatch, 0, kWarpWaves>), dim3(grid), dim3(256), 0, st, a);
 }
 
