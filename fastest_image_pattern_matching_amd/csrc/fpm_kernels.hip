@@ -2323,8 +2323,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // same source region (their angles differ by the layer's angle step, a fraction of a degree), so a task is one tile
 // position of all three: their footprint boxes' union is staged into LDS once (when it fits the wave's buffer) and
 // the three tiles are sampled from it one after the other -- the same taps, addressed from the union's origin, so
-// the same bytes as k_roi_warp.  A union that does not fit falls back to staging each ROI's own box.
-template <int FB, int WPE>
+// the same bytes as k_roi_warp.  A union that does not fit falls back to staging each ROI's own box.  PF 1: the
+// next task's descriptors loaded during the current one (wave-uniform, in SGPRs; measured 412 vs 404 us per Src7
+// layer-0 microbenchmark launch at 43 sources without, profiles/r03_r)
+template <int FB, int WPE, int PF = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_warp3(RoiArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t ft_all[4 * ROI_FT + 16];
     const int lane = threadIdx.x & 63;
@@ -2339,17 +2341,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const int tstride = xs.nk * 4;
     const uint32_t st_lane = 4u * lg + 32u * lr;
     constexpr int ftw = kFtPitch;
-    for (int task = xs.lo + xs.k * 4 + wv; task < xs.hi; task += tstride) {
+    // the next task's three tile descriptors are loaded (wave-uniform) while the current task runs
+    int task = xs.lo + xs.k * 4 + wv;
+    int4 nd[3];
+    auto prefetch = [&](int t) {
+        const int c_ = t / per_roi, r_ = t - c_ * per_roi;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int4 d = a.tdesc[(size_t)(3 * c_ + j) * a.tdesc_stride + r_];
+            nd[j] = make_int4(__builtin_amdgcn_readfirstlane(d.x), __builtin_amdgcn_readfirstlane(d.y),
+                              __builtin_amdgcn_readfirstlane(d.z), __builtin_amdgcn_readfirstlane(d.w));
+        }
+    };
+    if (PF && task < xs.hi) prefetch(task);
+    for (; task < xs.hi; task += tstride) {
+        if (!PF) prefetch(task);
         const int cand = task / per_roi;
         const int rem = task - cand * per_roi;
         const int ty = rem / txn, tx = rem - ty * txn;
         const int cx0 = tx * ROI_T, cx1 = min(cx0 + ROI_T, RW) - 1;
         const int ry0 = ty * ROI_T, ry1 = min(ry0 + ROI_T, RH) - 1;
         const int c0 = cx0 + 4 * lg;
+        int4 cd[3] = {nd[0], nd[1], nd[2]};
+        if (PF && task + tstride < xs.hi) prefetch(task + tstride);
         int bx[3], by[3], wp[3], fh[3], fl[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            const int4 d = a.tdesc[(size_t)(3 * cand + j) * a.tdesc_stride + rem];
+            const int4 d = cd[j];
             bx[j] = __builtin_amdgcn_readfirstlane(d.x);
             by[j] = __builtin_amdgcn_readfirstlane(d.y);
             const int dz = __builtin_amdgcn_readfirstlane(d.z);
