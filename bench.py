@@ -64,18 +64,24 @@ def pmc_traffic(kernel):
 
     if not os.path.exists(TRAFFIC_CSV):
         return None
-    fetch, write = {}, {}
+    fetch, write = {}, {}   # kernel name -> (mean bytes per dispatch, dispatches)
     with open(TRAFFIC_CSV) as fh:
         for row in csv.DictReader(fh):
             if row["counter"].startswith("FETCH_BYTES"):
-                fetch[row["kernel"]] = float(row["mean_per_dispatch"])
+                fetch[row["kernel"]] = (float(row["mean_per_dispatch"]), int(row["dispatches"]))
             elif row["counter"].startswith("WRITE_BYTES"):
-                write[row["kernel"]] = float(row["mean_per_dispatch"])
+                write[row["kernel"]] = (float(row["mean_per_dispatch"]), int(row["dispatches"]))
+    # every instantiation of the kernel (one per pyramid layer for the templated ROI kernels), weighted by its
+    # dispatches: the mean per launch over the same launches the algorithmic bytes are averaged over
+    total, launches = 0.0, 0
     for sym in L.KERNEL_SYMBOLS.get(kernel, []):
-        for name in fetch:
+        for name, (f, n) in fetch.items():
             if (name.startswith(f"fpm::{sym}(") or name.startswith(f"void fpm::{sym}<")) and name in write:
-                return int(fetch[name] + write[name])
-    return None
+                total += (f + write[name][0]) * n
+                launches += n
+        if launches:
+            break
+    return int(total / launches) if launches else None
 
 
 def make_sources(templ, n, seed0):

@@ -29,7 +29,7 @@ KERNEL_NAMES = ["pyr_down", "top_warp", "top_ncc", "top_nms", "cand_init", "roi_
                 "roi_eval", "roi_small", "cand_step"]
 KERNEL_SYMBOLS = {"pyr_down": ["k_pyr_down_s", "k_pyr_down"], "top_warp": ["k_warp"], "top_ncc": ["k_ncc_tile", "k_ncc_map"],
                   "top_nms": ["k_nms"], "cand_init": ["k_cand_init"], "roi_tables": ["k_roi_tables"],
-                  "roi_warp": ["k_roi_warp"], "roi_corr": ["k_roi_corr"], "roi_eval": ["k_roi_eval"],
+                  "roi_warp": ["k_roi_warp3", "k_roi_warp"], "roi_corr": ["k_roi_corr"], "roi_eval": ["k_roi_eval"],
                   "roi_small": ["k_roi_small"], "cand_step": ["k_cand_step"]}
 
 
