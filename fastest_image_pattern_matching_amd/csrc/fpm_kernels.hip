@@ -1865,7 +1865,9 @@ __device__ __forceinline__ uint32_t bilerp_row4(const int v[4][4], const int fx[
 }
 // The 16 taps of one output row (4 pixels x 2 rows x 2 columns) at a compile-time pitch, all issued before any use:
 // explicit ds_read_u8 (zero-extending; the compiler's own form re-masks every result with 0xff when it feeds 16-bit
-// lanes) and one lgkmcnt(0) that the results depend on.
+// lanes) and one lgkmcnt(0) that the results depend on.  Half as many reads as ds_read_u16 pairs (each tap row's two
+// columns, at byte-aligned addresses) give the same bytes but ran 4.2x slower (k_roi_warp3 layer-0 microbenchmark
+// 1689 vs 399 us, round 3): the LDS serves unaligned halfwords, slowly.
 template <int PITCH>
 __device__ __forceinline__ void lds_taps16(const uint32_t off[4], int v[4][4]) {
 #define FPM_TAPS(U)                                                                                                     \
@@ -2325,8 +2327,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // the three tiles are sampled from it one after the other -- the same taps, addressed from the union's origin, so
 // the same bytes as k_roi_warp.  A union that does not fit falls back to staging each ROI's own box.  PF 1: the
 // next task's descriptors loaded during the current one (wave-uniform, in SGPRs; measured 412 vs 404 us per Src7
-// layer-0 microbenchmark launch at 43 sources without, profiles/r03_r)
-template <int FB, int WPE, int PF = 0>
+// layer-0 microbenchmark launch at 43 sources without, profiles/r03_r).  TH0 1: the first ROI's table loads issued
+// before the union staging
+template <int FB, int WPE, int PF = 0, int TH0 = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_warp3(RoiArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t ft_all[4 * ROI_FT + 16];
     const int lane = threadIdx.x & 63;
@@ -2387,6 +2390,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const bool any_lds = ux0 != INT_MAX;
         const int uwpr = any_lds ? (ux1 - ux0) >> 2 : 0, ufth = any_lds ? uy1 - uy0 : 0;
         const bool uni = any_lds && uwpr <= 16 && kFtPitch * ufth <= ROI_FT;
+        // the lane's warp-table entries of one ROI (columns c0 .. c0 + 3, rows ry0 + lr + 8i); the first ROI's are
+        // requested before the staging, whose round trip they then share
+        const int cc = min(c0, cx1 & ~3);
+        int4 tA, tB, tX, tY;
+        auto load_tabs = [&](int slot_) {
+            const int32_t* tb = a.tab + (size_t)slot_ * 2 * (a.tabw + a.tabh);
+            tA = ld_at<int4>(tb, 4u * cc);
+            tB = ld_at<int4>(tb, 4u * (a.tabw + cc));
+            tX = ld_at<int4>(tb, 4u * (2 * a.tabw + ry0 + 4 * lr));
+            tY = ld_at<int4>(tb, 4u * (2 * a.tabw + a.tabh + ry0 + 4 * lr));
+        };
+        if (TH0) load_tabs(3 * cand);
         if (uni) {
             wave_sync();   // previous task's gathers are done with FT
             stage_footprint32<FB, kFtPitch>(FT, uwpr, ufth, lvl + (size_t)uy0 * a.P + ux0, a.P, lane);
@@ -2406,14 +2421,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                     stage_footprint32<FB, kFtPitch>(FT, wp[j], fh[j], lvl + (size_t)by0 * a.P + bxa, a.P, lane);
                 wave_sync();
             }
-            const int32_t* tb = a.tab + (size_t)slot * 2 * (a.tabw + a.tabh);
-            const int cc = min(c0, cx1 & ~3);
-            const int4 A = ld_at<int4>(tb, 4u * cc);
-            const int4 B = ld_at<int4>(tb, 4u * (a.tabw + cc));
-            const int adv[4] = {A.x, A.y, A.z, A.w}, bdv[4] = {B.x, B.y, B.z, B.w};
-            const int4 X4 = ld_at<int4>(tb, 4u * (2 * a.tabw + ry0 + 4 * lr));
-            const int4 Y4 = ld_at<int4>(tb, 4u * (2 * a.tabw + a.tabh + ry0 + 4 * lr));
-            const int X0r[4] = {X4.x, X4.y, X4.z, X4.w}, Y0r[4] = {Y4.x, Y4.y, Y4.z, Y4.w};
+            if (!TH0 || j > 0) load_tabs(slot);
+            const int adv[4] = {tA.x, tA.y, tA.z, tA.w}, bdv[4] = {tB.x, tB.y, tB.z, tB.w};
+            const int X0r[4] = {tX.x, tX.y, tX.z, tX.w}, Y0r[4] = {tY.x, tY.y, tY.z, tY.w};
             uint8_t* tile = a.roi + (size_t)slot * a.roi_stride + ((size_t)rem << 10);
             if (c0 > cx1) continue;
             if ((flags & kTileInterior) && in_lds) {
@@ -3637,7 +3647,9 @@ void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
     }();
     if (warp3 && a.n3 == 3 && a.slot_base % 3 == 0 && a.slot_cap % 3 == 0) {
         const long want3 = (tiles / 3 + 3) / 4;
-        hipLaunchKernelGGL((k_roi_warp3<kWarpFootBatch, kWarpWaves>), dim3((int)(want3 < 16384 ? want3 : 16384)),
+        // 7 waves per SIMD with the first ROI's tables requested before the staging (8 would spill them): microbenchmark
+        // 405.5 / 406.3 -> 400.6 / 402.0 us (round 3)
+        hipLaunchKernelGGL((k_roi_warp3<kWarpFootBatch, 7, 0, 1>), dim3((int)(want3 < 16384 ? want3 : 16384)),
                            dim3(256), 0, st, a);
         return;
     }

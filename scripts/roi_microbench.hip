@@ -116,10 +116,10 @@ int main(int argc, char** argv) {
             timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 0, 7>), dim3(grid), dim3(256), 0, 0, a); }, "warp b12 7 waves");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp<8, 0, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp b8 8 waves");
             const int grid3 = (int)std::min<long>((tiles / 3 + 3) / 4, 16384);
-            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<12, 8, 0>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 b12 8w");
-            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<12, 8, 1>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 b12 8w desc prefetch");
-            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<12, 7, 1>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 b12 7w desc prefetch");
-            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<16, 8, 1>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 b16 8w desc prefetch");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<12, 8, 0, 0>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 b12 8w");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<12, 8, 0, 1>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 b12 8w tables early");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<12, 7, 0, 1>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 b12 7w tables early");
+
             timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 5, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp no stores");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 6, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp gathers only");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 7, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp gathers, no LDS");
