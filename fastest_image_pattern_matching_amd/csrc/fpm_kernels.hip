@@ -1757,7 +1757,7 @@ size_t roi_corr_lds(int roi_pitch, int tw, int /*rc*/, bool ga) {
     constexpr int src_rows = 2 * kMmaRows + 6;
     const int tp8 = 64 * ((tw + 63) / 64);
     return (size_t)src_rows * roi_pitch + (ga ? 0 : (size_t)2 * kMmaRows * tmpl_lds_pitch(tp8)) +
-           sizeof(uint32_t) * (2 * src_rows + 2 * 7 * src_rows) + 64;
+           sizeof(uint32_t) * (2 * src_rows + 2 * 7 * src_rows + 2 * kMmaRows) + 64;
 }
 
 // bilinear tap from global memory (fallback when a footprint does not fit the LDS buffer);
@@ -2627,6 +2627,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     uint32_t* rallq = rall + kBandSrc;                         // full-row sums of I^2
     uint32_t* wi = rallq + kBandSrc;                           // [row][dx] window sums of I
     uint32_t* wq = wi + kBandSrc * 7;                          // [row][dx] window sums of I^2
+    uint32_t* lts = wq + kBandSrc * 7;                         // the band's template-row sums (16-byte aligned)
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int nband = (th + kBandRows - 1) / kBandRows;
     const int rois = roi_count(a), items = rois * nband;
@@ -2689,6 +2690,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             }
             if (band != a_band) {
                 a_band = band;
+                if (tid < kBandRows) lts[tid] = tid < rb ? (uint32_t)a.tsum[T0 + tid] : 0u;
                 if (kMmaRows * mt < rb) {
                     const int8_t* ap = a.tmpl8 + (size_t)(T0 + kMmaRows * mt + n) * a.tp8 + 16 * g;
 #pragma unroll
@@ -2698,6 +2700,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             }
             if (PFR && item + 1 < it_hi) load_rows(item + 1);
         } else if (MODE != 3) {   // stage: wave wv stages rows wv + 4i (kStageBatch rows' loads in flight), ^ 0x80
+            if (tid < kBandRows) lts[tid] = tid < rb ? (uint32_t)a.tsum[T0 + tid] : 0u;
             // tile-major ROI scratch (k_roi_warp): row R, 16-byte chunk c lives in tile (R >> 5, c >> 1)
             const uint8_t* rsrc = a.roi + (size_t)slot * a.roi_stride;
             for (int c0 = 0; c0 < q4; c0 += 64) {
@@ -2780,11 +2783,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             uint32_t* rs_out = a.rowsum + (((size_t)th * 49 + 3) & ~(size_t)3) * slot + (size_t)T0 * 49;
             const uint32_t kFix = 16384u * (uint32_t)tw;
             const int s_ = kMmaRows * nt + n;
+            // the template-row sums of the lane's 4 output rows from LDS (staged with the band; read from global memory
+            // here, each row's load also waited for the previous row's stores: 4 memory round trips per item)
+            const uint4 ts4 = *(const uint4*)(lts + kMmaRows * mt + 4 * g);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int t = kMmaRows * mt + 4 * g + r, dy = s_ - t;
                 if (t < rb && s_ < nsrc && dy >= 0 && dy < 7) {
-                    const uint32_t ts = (uint32_t)a.tsum[T0 + t];
+                    const uint32_t ts = r == 0 ? ts4.x : r == 1 ? ts4.y : r == 2 ? ts4.z : ts4.w;
 #pragma unroll
                     for (int d = 0; d < 7; ++d)
                         rs_out[(size_t)t * 49 + dy * 7 + d] = (uint32_t)acc[d][r] + 128u * (wi[s_ * 7 + d] + ts) - kFix;
@@ -3024,6 +3030,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
                 int sr = kMmaRows * nt + n;
                 if (sr >= nsrc) sr = 0;   // column outside the band: computed, never stored
                 const uint8_t* bp = SB + (size_t)ring(T0 + sr) * SBp + 16 * g;
+                const uint4 ts4 = ld_at<uint4>(a.tsum, 4u * (T0 + kMmaRows * mt + 4 * g));   // (see k_roi_corr)
                 fpm_v4i acc[7];
                 band_mfma_regs<NK>(Areg, bp, a.nk, acc);
                 // D_dx: col = lane & 15 -> source row 16*nt + n, row = 4*(lane >> 4) + r -> template row 16*mt + 4g + r
@@ -3037,7 +3044,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
                 for (int r = 0; r < 4; ++r) {
                     const int t = tb + r, dy = s_ - t;
                     if (t < rb && s_ < nsrc && dy >= 0 && dy < 7) {
-                        const uint32_t ts = (uint32_t)a.tsum[T0 + t];
+                        const uint32_t ts = r == 0 ? ts4.x : r == 1 ? ts4.y : r == 2 ? ts4.z : ts4.w;
 #pragma unroll
                         for (int d = 0; d < 7; ++d) ob[42 * r + d] = (uint32_t)acc[d][r] + 128u * (wr[d] + ts) - kFix;
                     }
@@ -3070,7 +3077,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 // candidates.  Used where the ROI, the template and one band of row sums fit the LDS budget (upper layers), so a
 // layer costs two launches instead of four and no scratch leaves the CU.
 struct SmallLayout {
-    int sbp, tbp, rh, u, tab, sum, rs, sc, total;
+    int sbp, tbp, rh, u, tab, sum, rs, sc, ts, total;
 };
 __host__ __device__ inline SmallLayout small_layout(int tw, int th) {
     SmallLayout L;
@@ -3084,11 +3091,12 @@ __host__ __device__ inline SmallLayout small_layout(int tw, int th) {
     L.sum = L.tab + 4 * (2 * L.sbp + 2 * ((L.rh + 3) & ~3));
     L.rs = L.sum + 4 * (2 * L.rh + 2 * 7 * L.rh) + 8 * 49 * 2;
     L.sc = L.rs + 4 * kBandRows * 49;
-    L.total = L.sc + 4 * 64;
+    L.ts = L.sc + 4 * 64;
+    L.total = L.ts + 4 * th16;
     return L;
 }
 constexpr int kSmallLdsMax = 72 * 1024;
-bool roi_small_fits(int tw, int th) { return small_layout(tw, th).total <= kSmallLdsMax; }
+bool roi_small_fits(int tw, int th) { return th <= 256 && small_layout(tw, th).total <= kSmallLdsMax; }
 size_t roi_small_lds(int tw, int th) { return (size_t)small_layout(tw, th).total; }
 
 // MODE (profiling ablations in scripts/roi_microbench.hip; the product uses 0): 1 = tables + sampling only,
@@ -3114,6 +3122,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     uint64_t* tot = (uint64_t*)(((uintptr_t)(wq + RH * 7) + 7) & ~(uintptr_t)7);   // [2][49] window totals
     uint32_t* rs = (uint32_t*)(smem + LY.rs);            // kBandRows x 49 row sums of the current band
     float* sc = (float*)(smem + LY.sc);
+    uint32_t* lts = (uint32_t*)(smem + LY.ts);            // template-row sums, 16-row padded
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int rois = roi_count(a);
     const int q4 = SBp >> 4, nwr = (RW + 3) >> 2;
@@ -3312,6 +3321,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         {   // all template rows (padded to 16) of the i8 slab
             const int trows = (th + kMmaRows - 1) / kMmaRows * kMmaRows;
             stage_block16(TB, TBp, (const uint8_t*)a.tmpl8, a.tp8, trows, a.tp8 >> 4, tid, 256);
+            // and the template-row sums (trows <= 256) for the band epilogues (3 waves per SIMD: 82.9 -> 81.0 us per
+            // Src7 layer-3 launch; the 4-wave form reads them from global memory there, as its registers spill more)
+            if (WPE < 4 && tid < trows) lts[tid] = (uint32_t)a.tsum[tid];
         }
         __syncthreads();
         STAMP(3);
@@ -3369,7 +3381,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 for (int r = 0; r < 4; ++r) {
                     const int t = kMmaRows * mt + 4 * g + r, dy = s_ - t;
                     if (t < rb && s_ < nsrc && dy >= 0 && dy < 7) {
-                        const uint32_t ts = (uint32_t)a.tsum[T0 + t];
+                        const uint32_t ts = WPE < 4 ? lts[T0 + t] : (uint32_t)a.tsum[T0 + t];
 #pragma unroll
                         for (int d = 0; d < 7; ++d)
                             rs[t * 49 + dy * 7 + d] = (uint32_t)acc[d][r] + 128u * (wi[(T0 + s_) * 7 + d] + ts) - kFix;
