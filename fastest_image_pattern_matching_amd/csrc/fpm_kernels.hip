@@ -2611,12 +2611,13 @@ __device__ __forceinline__ void band_mfma_regs(const fpm_v4i* A, const uint8_t* 
 }
 
 // MODE (profiling ablations in scripts/roi_microbench.hip; the product uses 0): 2 = no MFMA loop, 3 = no staging
+// (slot-major form only), 4 = no window-edge phase, 5 = no row-result stores, 6 = no window partials, 7 = no row sums
 // GA: A operand read from the global i8 slab (no template rows in LDS); WPE: register cap (waves per SIMD);
 // NK > 0: register-A form (A fragments of nk <= NK k-steps held per wave, band-major item runs; needs GA)
 // PFR (register-A form): prefetch the next item's rows (false: load this item's rows at its start, fewer VGPRs)
 template <int MODE, bool GA, int WPE, int NK = 0, bool PFR = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_corr(RoiArgs a) {
-    static_assert(NK == 0 || (GA && MODE == 0), "the register-A form stages no template rows");
+    static_assert(NK == 0 || (GA && MODE != 3), "the register-A form stages no template rows");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tw = a.tw, th = a.th, RW = tw + 6;
     const int SBp = a.roi_pitch;
@@ -2728,7 +2729,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             }
         }
         __syncthreads();
-        if (tid < 4 * nsrc) {   // exact full-row sums of I and I^2: thread (row, quarter of the row's words)
+        if (MODE != 7 && tid < 4 * nsrc) {   // exact full-row sums of I and I^2: thread (row, quarter of the row's words)
             const int r = tid >> 2, qq = tid & 3;
             const int per = (nwr + 3) >> 2, k0 = qq * per, k1 = min(nwr, k0 + per);
             const uint32_t* row = (const uint32_t*)(SB + (size_t)r * SBp);
@@ -2757,7 +2758,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             stage_block16(TB, TBp, (const uint8_t*)a.tmpl8 + (size_t)T0 * a.tp8, a.tp8, trows, a.tp8 >> 4, tid, 256);
         }
         __syncthreads();
-        for (int i = tid; i < nsrc * 7; i += 256) {   // window [dx, dx + tw): full row minus <= 6 edge pixels
+        for (int i = tid; MODE != 4 && i < nsrc * 7; i += 256) {   // window [dx, dx + tw): full row minus <= 6 edge pixels
             const int r = i / 7, dx = i - r * 7;
             const uint8_t* sbr = SB + (size_t)r * SBp;
             uint32_t q1 = rall[r], q2 = rallq[r];
@@ -2791,13 +2792,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 const int t = kMmaRows * mt + 4 * g + r, dy = s_ - t;
                 if (t < rb && s_ < nsrc && dy >= 0 && dy < 7) {
                     const uint32_t ts = r == 0 ? ts4.x : r == 1 ? ts4.y : r == 2 ? ts4.z : ts4.w;
+                    if (MODE == 5) {   // ablation: keep the MFMA results live, store nothing
+                        uint32_t x = ts;
+#pragma unroll
+                        for (int d = 0; d < 7; ++d) x += (uint32_t)acc[d][r];
+                        if (x == 0x9e3779b9u && a.W < 0) rs_out[t] = x;
+                        continue;
+                    }
 #pragma unroll
                     for (int d = 0; d < 7; ++d)
                         rs_out[(size_t)t * 49 + dy * 7 + d] = (uint32_t)acc[d][r] + 128u * (wi[s_ * 7 + d] + ts) - kFix;
                 }
             }
         }
-        if (tid < 2 * 49) {   // per-16-row-chunk partials of the window sums
+        if (MODE != 6 && tid < 2 * 49) {   // per-16-row-chunk partials of the window sums
             const int h = tid / 49, k = tid - h * 49;
             const int chunk = (T0 >> 4) + h;
             const int tlo = kMmaRows * h, thi = min(tlo + kMmaRows, rb);

@@ -106,7 +106,7 @@ int main(int argc, char** argv) {
     };
     timeit([&] { launch_roi_tables(a, 0); }, "prod tables");
     timeit([&] { launch_roi_warp(a, 0); }, "prod warp");
-    {
+    if (!envi("MB_CORR", 0)) {   // MB_CORR=1: the correlation section only (the ROIs from the product warp above)
         const long tiles = (long)a.slot_cap * ((TH + 6 + 31) / 32) * ((TW + 6 + 31) / 32);
         const int grid = (int)std::min<long>((tiles + 3) / 4, 16384);
         timeit([&] { hipLaunchKernelGGL(k_roi_warp<0>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot LDS-DMA");
@@ -134,6 +134,18 @@ int main(int argc, char** argv) {
     }
     if (envi("MB_WARP_ONLY", 0)) return 0;
     timeit([&] { launch_roi_corr(a, 0); }, "prod corr");
+    if (TW > 512 && TW <= 768) {   // register-A form (12 k-steps, the Src7 layer-0 product) and its phase ablations
+        const size_t lds = roi_corr_lds(a.roi_pitch, a.tw, a.rc, true);
+        const long items = (long)a.slot_cap * ((TH + 31) / 32);
+        const int grid = (int)std::min<long>(items, 768);
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA full");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<2, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA no mfma+epi");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<4, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA no edges");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<5, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA no stores");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<6, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA no partials");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<7, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA no rowsums");
+        if (envi("MB_CORR_ONLY", 0)) { launch_roi_corr(a, 0); }
+    }
     timeit([&] { launch_roi_eval(a, 0); }, "prod eval");
     {
         const size_t lds0 = roi_corr_lds(a.roi_pitch, a.tw, a.rc, false), lds1 = roi_corr_lds(a.roi_pitch, a.tw, a.rc, true);
@@ -181,6 +193,7 @@ int main(int argc, char** argv) {
         }
         printf("corr host check: %s (%d mismatches)\n", bad ? "FAIL" : "OK", bad);
     }
+    if (envi("MB_CORR", 0)) return 0;
     {   // small-template single-kernel refinement at Src7 layer-3 geometry: 96x66 template, 503x380 level,
         // 224 candidates x 3 angles (8 sources x 28), grid sized like the product (slot_cap WGs, most idle)
         const int TW3 = 96, TH3 = 66, W3 = 503, H3 = 380, nc3 = 28, C3 = nsrc * nc3;
