@@ -2615,7 +2615,10 @@ __device__ __forceinline__ void band_mfma_regs(const fpm_v4i* A, const uint8_t* 
 // GA: A operand read from the global i8 slab (no template rows in LDS); WPE: register cap (waves per SIMD);
 // NK > 0: register-A form (A fragments of nk <= NK k-steps held per wave, band-major item runs; needs GA)
 // PFR (register-A form): prefetch the next item's rows (false: load this item's rows at its start, fewer VGPRs)
-template <int MODE, bool GA, int WPE, int NK = 0, bool PFR = true>
+// RS: 1 = row statistics in one phase (a quad of lanes per row: its I / I^2 totals reduced by DPP, then the edge pixels
+// of each window subtracted by the same lanes; the window partials split over lane pairs), 0 = the earlier form (row
+// totals by LDS atomics, a separate edge phase, one thread per partial), 2 = as 1 with the partials before the GEMM
+template <int MODE, bool GA, int WPE, int NK = 0, bool PFR = true, int RS = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_corr(RoiArgs a) {
     static_assert(NK == 0 || (GA && MODE != 3), "the register-A form stages no template rows");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -2674,7 +2677,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         else { slot = item / nband; band = item - slot * nband; }
         const int T0 = band * kBandRows, rb = min(kBandRows, th - T0), nsrc = rb + 6;
         __syncthreads();   // previous item done with SB / rall / wi
-        if (tid < kBandSrc) { rall[tid] = 0; rallq[tid] = 0; }
+        if (RS == 0 && tid < kBandSrc) { rall[tid] = 0; rallq[tid] = 0; }
         if (NK > 0) {
             // this item's rows (loaded during the previous item) ^ 0x80 into LDS; this wave's A fragments when the
             // band changes (workgroup-uniform); then the next item's row loads
@@ -2729,7 +2732,64 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             }
         }
         __syncthreads();
-        if (MODE != 7 && tid < 4 * nsrc) {   // exact full-row sums of I and I^2: thread (row, quarter of the row's words)
+        if (RS >= 1 && MODE != 7 && tid < 4 * nsrc) {
+            // row r's statistics by the quad of lanes 4r .. 4r + 3 (whole quads: DPP within the quad): exact full-row
+            // sums of I and I^2 over the row's words (pixels past RW are zero), then each lane subtracts the window's
+            // edge pixels for its dx (qq and qq + 4): window [dx, dx + tw) = row minus bytes [0, dx) and [dx + tw, RW)
+            const int r = tid >> 2, qq = tid & 3;
+            const int per = (nwr + 3) >> 2, k0 = qq * per, k1 = min(nwr, k0 + per);
+            const uint32_t* row = (const uint32_t*)(SB + (size_t)r * SBp);
+            uint32_t s1 = 0, s2 = 0;
+            int k = k0;
+            for (; k + 8 <= k1; k += 8) {
+                uint32_t x[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) x[u] = row[k + u] ^ 0x80808080u;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    s1 = __builtin_amdgcn_udot4(x[u], 0x01010101u, s1, false);
+                    s2 = __builtin_amdgcn_udot4(x[u], x[u], s2, false);
+                }
+            }
+            for (; k < k1; ++k) {
+                const uint32_t x = row[k] ^ 0x80808080u;
+                s1 = __builtin_amdgcn_udot4(x, 0x01010101u, s1, false);
+                s2 = __builtin_amdgcn_udot4(x, x, s2, false);
+            }
+            // left edge bytes 0..5 (words 0, 1) and right edge bytes tw .. tw + 5 (funnel-shifted from 3 words)
+            const uint32_t l0 = row[0] ^ 0x80808080u, l1 = row[1] ^ 0x80808080u;
+            const int wr = tw >> 2;
+            const uint32_t x0 = row[wr], x1 = row[wr + 1], x2 = row[wr + 2];
+            const uint32_t e0 = __builtin_amdgcn_alignbyte(x1, x0, (uint32_t)tw) ^ 0x80808080u;
+            const uint32_t e1 = __builtin_amdgcn_alignbyte(x2, x1, (uint32_t)tw) ^ 0x80808080u;
+            s1 += (uint32_t)__builtin_amdgcn_mov_dpp((int)s1, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+            s2 += (uint32_t)__builtin_amdgcn_mov_dpp((int)s2, 0xB1, 0xF, 0xF, false);
+            s1 += (uint32_t)__builtin_amdgcn_mov_dpp((int)s1, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+            s2 += (uint32_t)__builtin_amdgcn_mov_dpp((int)s2, 0x4E, 0xF, 0xF, false);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int dx = qq + 4 * h;
+                if (dx < 7) {
+                    // left: bytes c < dx of (l0, l1); right: bytes i >= dx of (e0, e1[0..1])
+                    const uint32_t ml0 = dx >= 4 ? 0xffffffffu : (1u << (8 * dx)) - 1u;
+                    const uint32_t ml1 = dx <= 4 ? 0u : (1u << (8 * (dx - 4))) - 1u;
+                    const uint32_t mr0 = dx >= 4 ? 0u : ~((1u << (8 * dx)) - 1u);
+                    const uint32_t mr1 = dx <= 4 ? 0xffffu : dx == 5 ? 0xff00u : 0u;
+                    const uint32_t a0 = l0 & ml0, a1 = l1 & ml1, b0 = e0 & mr0, b1 = e1 & mr1;
+                    uint32_t q1 = __builtin_amdgcn_udot4(a0, 0x01010101u, 0u, false);
+                    q1 = __builtin_amdgcn_udot4(a1, 0x01010101u, q1, false);
+                    q1 = __builtin_amdgcn_udot4(b0, 0x01010101u, q1, false);
+                    q1 = __builtin_amdgcn_udot4(b1, 0x01010101u, q1, false);
+                    uint32_t q2 = __builtin_amdgcn_udot4(a0, a0, 0u, false);
+                    q2 = __builtin_amdgcn_udot4(a1, a1, q2, false);
+                    q2 = __builtin_amdgcn_udot4(b0, b0, q2, false);
+                    q2 = __builtin_amdgcn_udot4(b1, b1, q2, false);
+                    wi[r * 7 + dx] = s1 - q1;
+                    wq[r * 7 + dx] = s2 - q2;
+                }
+            }
+        }
+        if (RS == 0 && MODE != 7 && tid < 4 * nsrc) {   // exact full-row sums of I and I^2: thread (row, quarter of the row's words)
             const int r = tid >> 2, qq = tid & 3;
             const int per = (nwr + 3) >> 2, k0 = qq * per, k1 = min(nwr, k0 + per);
             const uint32_t* row = (const uint32_t*)(SB + (size_t)r * SBp);
@@ -2757,8 +2817,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             const int trows = (rb + kMmaRows - 1) / kMmaRows * kMmaRows;
             stage_block16(TB, TBp, (const uint8_t*)a.tmpl8 + (size_t)T0 * a.tp8, a.tp8, trows, a.tp8 >> 4, tid, 256);
         }
-        __syncthreads();
-        for (int i = tid; MODE != 4 && i < nsrc * 7; i += 256) {   // window [dx, dx + tw): full row minus <= 6 edge pixels
+        if (RS == 0) __syncthreads();
+        for (int i = tid; RS == 0 && MODE != 4 && i < nsrc * 7; i += 256) {   // window [dx, dx + tw): full row minus <= 6 edge pixels
             const int r = i / 7, dx = i - r * 7;
             const uint8_t* sbr = SB + (size_t)r * SBp;
             uint32_t q1 = rall[r], q2 = rallq[r];
@@ -2768,6 +2828,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             wq[i] = q2;
         }
         __syncthreads();
+        // per-16-row-chunk partials of the window sums, 8 rows per lane (lane pairs, combined by DPP within the quad;
+        // the 8 rows' LDS reads all in flight)
+        auto partials = [&]() {
+            if (MODE == 6 || tid >= 4 * 49) return;
+            const int pr = tid >> 1, half = tid & 1;
+            const int h = pr / 49, k = pr - h * 49;
+            const int chunk = (T0 >> 4) + h;
+            const int tlo = kMmaRows * h, thi = min(tlo + kMmaRows, rb);
+            const bool ok = chunk < a.nchunk && tlo < thi;   // the same for both lanes of the pair
+            const int pdy = k / 7, ddx = k - pdy * 7;
+            const int t0 = tlo + 8 * half, n8 = ok ? min(8, thi - t0) : 0;
+            uint32_t s1 = 0, x[8], y[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = (t0 + u + pdy) * 7 + ddx;
+                x[u] = u < n8 ? wi[i] : 0u;
+                y[u] = u < n8 ? wq[i] : 0u;
+            }
+            uint64_t s2 = 0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) { s1 += x[u]; s2 += y[u]; }
+            s1 += (uint32_t)__builtin_amdgcn_mov_dpp((int)s1, 0xB1, 0xF, 0xF, false);
+            const uint32_t lo = (uint32_t)s2, hi = (uint32_t)(s2 >> 32);
+            s2 += (uint64_t)(uint32_t)__builtin_amdgcn_mov_dpp((int)lo, 0xB1, 0xF, 0xF, false) |
+                  ((uint64_t)(uint32_t)__builtin_amdgcn_mov_dpp((int)hi, 0xB1, 0xF, 0xF, false) << 32);
+            if (ok && half == 0) {
+                // 32-bit index recomputed per item (opaque k): a loop-invariant 64-bit address kept across the item
+                // loop was spilled, and its reload's vmcnt(0) waited for every row-result store of the item
+                uint32_t kk = (uint32_t)k;
+                asm volatile("" : "+v"(kk));
+                const uint32_t wo = ((uint32_t)slot * (uint32_t)a.nchunk + (uint32_t)chunk) * 49u + kk;
+                a.wsum[wo] = s1;
+                a.wsq[wo] = s2;
+            }
+        };
+        if (RS == 2) partials();   // before the banded GEMM (the same wave's MFMA work follows)
         const bool active = kMmaRows * mt < rb && kMmaRows * nt < nsrc;   // wave-uniform
         if (MODE != 2 && active) {
             int sr = kMmaRows * nt + n;
@@ -2781,15 +2877,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             else
                 band_mfma(TB + (size_t)(kMmaRows * mt + n) * TBp + 16 * g, bp, a.nk, acc);
             // D_dx: col = lane & 15 -> source row 16*nt + n, row = 4*(lane >> 4) + r -> template row 16*mt + 4g + r
-            uint32_t* rs_out = a.rowsum + (((size_t)th * 49 + 3) & ~(size_t)3) * slot + (size_t)T0 * 49;
+            uint32_t* rs_out = a.rowsum + (((size_t)th * 49 + 3) & ~(size_t)3) * slot + (size_t)T0 * 49;   // uniform
             const uint32_t kFix = 16384u * (uint32_t)tw;
+            // the lane's row offsets as 32-bit values recomputed per item (opaque t0): kept across the item loop as
+            // 64-bit addresses they were spilled, and each reload's vmcnt(0) waited for the previous rows' stores
+            int t0 = kMmaRows * mt + 4 * g;
+            asm volatile("" : "+v"(t0));
             const int s_ = kMmaRows * nt + n;
             // the template-row sums of the lane's 4 output rows from LDS (staged with the band; read from global memory
             // here, each row's load also waited for the previous row's stores: 4 memory round trips per item)
-            const uint4 ts4 = *(const uint4*)(lts + kMmaRows * mt + 4 * g);
+            const uint4 ts4 = *(const uint4*)(lts + t0);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int t = kMmaRows * mt + 4 * g + r, dy = s_ - t;
+                const int t = t0 + r, dy = s_ - t;
                 if (t < rb && s_ < nsrc && dy >= 0 && dy < 7) {
                     const uint32_t ts = r == 0 ? ts4.x : r == 1 ? ts4.y : r == 2 ? ts4.z : ts4.w;
                     if (MODE == 5) {   // ablation: keep the MFMA results live, store nothing
@@ -2799,13 +2899,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                         if (x == 0x9e3779b9u && a.W < 0) rs_out[t] = x;
                         continue;
                     }
+                    const uint32_t o = (uint32_t)(t * 49 + dy * 7);
 #pragma unroll
-                    for (int d = 0; d < 7; ++d)
-                        rs_out[(size_t)t * 49 + dy * 7 + d] = (uint32_t)acc[d][r] + 128u * (wi[s_ * 7 + d] + ts) - kFix;
+                    for (int d = 0; d < 7; ++d) rs_out[o + d] = (uint32_t)acc[d][r] + 128u * (wi[s_ * 7 + d] + ts) - kFix;
                 }
             }
         }
-        if (MODE != 6 && tid < 2 * 49) {   // per-16-row-chunk partials of the window sums
+        if (RS == 1) partials();
+        if (RS == 0 && MODE != 6 && tid < 2 * 49) {   // per-16-row-chunk partials of the window sums
             const int h = tid / 49, k = tid - h * 49;
             const int chunk = (T0 >> 4) + h;
             const int tlo = kMmaRows * h, thi = min(tlo + kMmaRows, rb);

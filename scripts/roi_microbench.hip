@@ -139,6 +139,8 @@ int main(int argc, char** argv) {
         const long items = (long)a.slot_cap * ((TH + 31) / 32);
         const int grid = (int)std::min<long>(items, 768);
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA full");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 12, false, 0>), dim3(grid), dim3(256), lds, 0, a); }, "corrA RS0 full");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 12, false, 2>), dim3(grid), dim3(256), lds, 0, a); }, "corrA RS2 full");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<2, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA no mfma+epi");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<4, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA no edges");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<5, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA no stores");
