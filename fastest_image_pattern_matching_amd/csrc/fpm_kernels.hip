@@ -1757,7 +1757,7 @@ size_t roi_corr_lds(int roi_pitch, int tw, int /*rc*/, bool ga) {
     constexpr int src_rows = 2 * kMmaRows + 6;
     const int tp8 = 64 * ((tw + 63) / 64);
     return (size_t)src_rows * roi_pitch + (ga ? 0 : (size_t)2 * kMmaRows * tmpl_lds_pitch(tp8)) +
-           sizeof(uint32_t) * (2 * src_rows + 2 * 7 * src_rows + 2 * kMmaRows) + 64;
+           sizeof(uint32_t) * (2 * src_rows + 2 * 7 * src_rows + 2 * kMmaRows + 2 * kMmaRows * 49) + 64;
 }
 
 // bilinear tap from global memory (fallback when a footprint does not fit the LDS buffer);
@@ -2618,9 +2618,12 @@ __device__ __forceinline__ void band_mfma_regs(const fpm_v4i* A, const uint8_t* 
 // RS: 1 = row statistics in one phase (a quad of lanes per row: its I / I^2 totals reduced by DPP, then the edge pixels
 // of each window subtracted by the same lanes; the window partials split over lane pairs), 0 = the earlier form (row
 // totals by LDS atomics, a separate edge phase, one thread per partial), 2 = as 1 with the partials before the GEMM
-template <int MODE, bool GA, int WPE, int NK = 0, bool PFR = true, int RS = 1>
+// SE: the band's row results are written into LDS by the epilogue and copied to HBM as 16-byte runs during the next
+// item's staging (after the loads of its rows are issued, so waiting for those loads does not wait for these stores)
+template <int MODE, bool GA, int WPE, int NK = 0, bool PFR = true, int RS = 1, bool SE = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_corr(RoiArgs a) {
     static_assert(NK == 0 || (GA && MODE != 3), "the register-A form stages no template rows");
+    static_assert(!SE || NK > 0, "the staged epilogue is flushed in the register-A form's staging phase");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tw = a.tw, th = a.th, RW = tw + 6;
     const int SBp = a.roi_pitch;
@@ -2632,6 +2635,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     uint32_t* wi = rallq + kBandSrc;                           // [row][dx] window sums of I
     uint32_t* wq = wi + kBandSrc * 7;                          // [row][dx] window sums of I^2
     uint32_t* lts = wq + kBandSrc * 7;                         // the band's template-row sums (16-byte aligned)
+    uint32_t* rsb = lts + 2 * kMmaRows;                        // (SE) the band's [rb][49] row results (16-byte aligned)
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int nband = (th + kBandRows - 1) / kBandRows;
     const int rois = roi_count(a), items = rois * nband;
@@ -2671,6 +2675,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
     };
     if (NK > 0 && PFR && it_lo < it_hi) load_rows(it_lo);
+    // (SE) the previous item's row results: LDS -> its [rb][49] range of the ROI's series, 16-byte stores (the range
+    // starts 16-byte aligned: slot stride and T0 * 49 are multiples of 4 words), the < 4-word tail by single words
+    int pv_slot = -1, pv_T0 = 0, pv_rb = 0;
+    auto flush = [&]() {
+        if (!SE || pv_slot < 0) return;
+        uint32_t* dst = a.rowsum + (((size_t)th * 49 + 3) & ~(size_t)3) * pv_slot + (size_t)pv_T0 * 49;
+        const int nw = pv_rb * 49, n16 = nw >> 2;
+        for (int i = tid; i < n16; i += 256) *(uint4*)(dst + 4 * i) = *(const uint4*)(rsb + 4 * i);
+        if (tid < (nw & 3)) dst[4 * n16 + tid] = rsb[4 * n16 + tid];
+    };
     for (int item = it_lo; item < it_hi; item += it_step) {
         int slot, band;
         if (NK > 0) { band = item / rois; slot = item - band * rois; }
@@ -2683,6 +2697,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             // band changes (workgroup-uniform); then the next item's row loads
             const bool in_roi = lane < 2 * txn;
             if (!PFR) load_rows(item);
+            flush();
 #pragma unroll
             for (int i = 0; i < kStageRows; ++i) {
                 const int r = wv + 4 * i;
@@ -2900,6 +2915,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                         continue;
                     }
                     const uint32_t o = (uint32_t)(t * 49 + dy * 7);
+                    if (SE) {
+#pragma unroll
+                        for (int d = 0; d < 7; ++d) rsb[o + d] = (uint32_t)acc[d][r] + 128u * (wi[s_ * 7 + d] + ts) - kFix;
+                        continue;
+                    }
 #pragma unroll
                     for (int d = 0; d < 7; ++d) rs_out[o + d] = (uint32_t)acc[d][r] + 128u * (wi[s_ * 7 + d] + ts) - kFix;
                 }
@@ -2922,6 +2942,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 a.wsq[((size_t)slot * a.nchunk + chunk) * 49 + k] = s2;
             }
         }
+        if (SE) { pv_slot = slot; pv_T0 = T0; pv_rb = rb; }
+    }
+    if (SE && pv_slot >= 0) {   // the last item's row results
+        __syncthreads();
+        flush();
     }
 }
 
@@ -3793,11 +3818,13 @@ static void launch_corr_regs(const RoiArgs& a, long items, size_t lds, hipStream
         // launch); at 8 / 12 k-steps the larger spills lose (136.5 -> 145.2, 301.1 -> 403.2 us)
         if (NK == 4 && lds * 4 <= kLdsPerCu) {
             const int grid = (int)(items < 256 * 4 ? items : 256 * 4);
-            hipLaunchKernelGGL((k_roi_corr<0, true, 4, NK, false>), dim3(grid), dim3(256), lds, st, a);
+            hipLaunchKernelGGL((k_roi_corr<0, true, 4, NK, false, 1, true>), dim3(grid), dim3(256), lds, st, a);
             return;
         }
+        // row results staged in LDS and flushed during the next item's staging (SE; Src7 microbenchmark at 43 sources:
+        // layer 0 293.6 -> 264.4 us, layer 1 124.2 -> 115.4, bit-identical)
         const int grid = (int)(items < 256 * kCorrWaves ? items : 256 * kCorrWaves);
-        hipLaunchKernelGGL((k_roi_corr<0, true, kCorrWaves, NK, false>), dim3(grid), dim3(256), lds, st, a);
+        hipLaunchKernelGGL((k_roi_corr<0, true, kCorrWaves, NK, false, 1, true>), dim3(grid), dim3(256), lds, st, a);
     } else {
         const int grid = (int)(items < kCorrRunWGs ? items : kCorrRunWGs);
         hipLaunchKernelGGL((k_roi_corr<0, true, kCorrRunWaves, NK>), dim3(grid), dim3(256), lds, st, a);

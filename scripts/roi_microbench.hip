@@ -140,13 +140,20 @@ int main(int argc, char** argv) {
         const int grid = (int)std::min<long>(items, 768);
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA full");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 12, false, 0>), dim3(grid), dim3(256), lds, 0, a); }, "corrA RS0 full");
-        timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 12, false, 2>), dim3(grid), dim3(256), lds, 0, a); }, "corrA RS2 full");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 12, false, 1, true>), dim3(grid), dim3(256), lds, 0, a); }, "corrA SE full");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<2, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA no mfma+epi");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<4, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA no edges");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<5, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA no stores");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<6, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA no partials");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<7, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA no rowsums");
         if (envi("MB_CORR_ONLY", 0)) { launch_roi_corr(a, 0); }
+    }
+    if (TW > 256 && TW <= 512) {   // 8 k-steps (the Src7 layer-1 product): 3 vs 4 waves per SIMD
+        const size_t lds = roi_corr_lds(a.roi_pitch, a.tw, a.rc, true);
+        const long items = (long)a.slot_cap * ((TH + 31) / 32);
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 8, false>), dim3((int)std::min<long>(items, 768)), dim3(256), lds, 0, a); }, "corrA8 3 waves");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 8, false, 1, true>), dim3((int)std::min<long>(items, 768)), dim3(256), lds, 0, a); }, "corrA8 SE 3 waves");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 8, false, 0>), dim3((int)std::min<long>(items, 768)), dim3(256), lds, 0, a); }, "corrA8 RS0 3 waves");
     }
     timeit([&] { launch_roi_eval(a, 0); }, "prod eval");
     {
@@ -162,6 +169,15 @@ int main(int argc, char** argv) {
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<3, true, 3>), dim3(grid), dim3(256), lds1, 0, a); }, "corr globA w3 no stage");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<2, true, 3>), dim3(grid), dim3(256), lds1, 0, a); }, "corr globA w3 no mfma");
         launch_roi_corr(a, 0);
+        if (envi("MB_SE_CHECK", 0)) {   // the host check below then checks the LDS-staged epilogue form
+            hipMemset(a.rowsum, 0xff, (size_t)C * n3 * ((TH * 49 + 3) & ~3) * 4);
+            const long items = (long)a.slot_cap * ((TH + 31) / 32);
+            if (TW > 512 && TW <= 768)
+                hipLaunchKernelGGL((k_roi_corr<0, true, 3, 12, false, 1, true>), dim3((int)std::min<long>(items, 768)), dim3(256), lds1, 0, a);
+            else if (TW > 256 && TW <= 512)
+                hipLaunchKernelGGL((k_roi_corr<0, true, 3, 8, false, 1, true>), dim3((int)std::min<long>(items, 768)), dim3(256), lds1, 0, a);
+            printf("host check of the SE form\n");
+        }
     }
     {   // host check of k_roi_corr on a few ROI slots
         const int RW = TW + 6;
