@@ -2668,10 +2668,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const int bd = it / rois, sl = it - bd * rois;
         const int T0n = bd * kBandRows, nsn = min(kBandRows, th - T0n) + 6;
         const uint8_t* rsrc = a.roi + (size_t)sl * a.roi_stride;
+        // row indices wave-uniform (scalar), the lane's column offset recomputed per call (opaque): no per-row
+        // address registers kept across the item loop
+        const int wvu = __builtin_amdgcn_readfirstlane(wv);
+        int lcv = lc;
+        asm volatile("" : "+v"(lcv));
+        const uint32_t lane_off = ((uint32_t)(lcv >> 1) << 10) + 16u * (uint32_t)(lcv & 1);
 #pragma unroll
         for (int i = 0; i < kStageRows; ++i) {
-            const int R = T0n + min(wv + 4 * i, nsn - 1);
-            pv[i] = *(const uint4*)(rsrc + ((size_t)((R >> 5) * txn + (lc >> 1)) << 10) + (R & 31) * ROI_T + 16 * (lc & 1));
+            const int R = T0n + min(wvu + 4 * i, nsn - 1);
+            pv[i] = *(const uint4*)(rsrc + ((size_t)((R >> 5) * txn) << 10) + (R & 31) * ROI_T + lane_off);
         }
     };
     if (NK > 0 && PFR && it_lo < it_hi) load_rows(it_lo);
@@ -3816,7 +3822,9 @@ static void launch_corr_regs(const RoiArgs& a, long items, size_t lds, hipStream
         // faster than the prefetching 2-wave form (occupancy hides the staging latency better)
         // at 4 k-steps 4 waves per SIMD pay despite a 28-byte spill (Src7 layer 2: 68.2 -> 58.0 us per 43-source
         // launch); at 8 / 12 k-steps the larger spills lose (136.5 -> 145.2, 301.1 -> 403.2 us)
-        if (NK == 4 && lds * 4 <= kLdsPerCu) {
+        // ... and at 8 k-steps since the load addressing is scalar (136 VGPRs at 3 waves, 4 spilled at 4 waves: Src7
+        // layer 1 107.7 -> 99.4 us per 43-source microbenchmark launch, profiles/r03_y)
+        if ((NK == 4 || NK == 8) && lds * 4 <= kLdsPerCu) {
             const int grid = (int)(items < 256 * 4 ? items : 256 * 4);
             hipLaunchKernelGGL((k_roi_corr<0, true, 4, NK, false, 1, true>), dim3(grid), dim3(256), lds, st, a);
             return;

@@ -153,6 +153,7 @@ int main(int argc, char** argv) {
         const long items = (long)a.slot_cap * ((TH + 31) / 32);
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 8, false>), dim3((int)std::min<long>(items, 768)), dim3(256), lds, 0, a); }, "corrA8 3 waves");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 8, false, 1, true>), dim3((int)std::min<long>(items, 768)), dim3(256), lds, 0, a); }, "corrA8 SE 3 waves");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 4, 8, false, 1, true>), dim3((int)std::min<long>(items, 1024)), dim3(256), lds, 0, a); }, "corrA8 SE 4 waves");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 8, false, 0>), dim3((int)std::min<long>(items, 768)), dim3(256), lds, 0, a); }, "corrA8 RS0 3 waves");
     }
     timeit([&] { launch_roi_eval(a, 0); }, "prod eval");
@@ -175,7 +176,7 @@ int main(int argc, char** argv) {
             if (TW > 512 && TW <= 768)
                 hipLaunchKernelGGL((k_roi_corr<0, true, 3, 12, false, 1, true>), dim3((int)std::min<long>(items, 768)), dim3(256), lds1, 0, a);
             else if (TW > 256 && TW <= 512)
-                hipLaunchKernelGGL((k_roi_corr<0, true, 3, 8, false, 1, true>), dim3((int)std::min<long>(items, 768)), dim3(256), lds1, 0, a);
+                hipLaunchKernelGGL((k_roi_corr<0, true, 4, 8, false, 1, true>), dim3((int)std::min<long>(items, 1024)), dim3(256), lds1, 0, a);
             printf("host check of the SE form\n");
         }
     }
