@@ -99,6 +99,7 @@ struct Plan {
     // top-layer layout (per source)
     std::vector<size_t> canvas_off, map_off, blk_off;
     std::vector<int> canvas_pitch, map_w, map_h, nblk;
+    std::vector<int32_t> order;                // k_top_fused workgroup -> job (costliest angles first)
     size_t canvas_bytes = 0, map_floats = 0, blk_count = 0;
     int max_canvas = 0, max_map = 0, max_nblk = 0, max_cells = 0, max_nitems = 0;
     int off_skey = 0, nzero = 0;   // d_livecnt layout: strip keys' offset, words zeroed by k_warp
@@ -109,7 +110,7 @@ struct Plan {
     int tabw = 0, tabh = 0, roi_pitch = 0, tdesc_stride = 1;
     size_t roi_stride = 0;
     int slot_cap = 0;                          // ROIs per refinement round (bounded scratch)
-    size_t off_warp = 0, off_ncc = 0, off_nms = 0;
+    size_t off_warp = 0, off_ncc = 0, off_nms = 0, off_order = 0;
     PinBuf h_out;
     size_t h_counts = 0, h_peaks = 0, h_live = 0, h_live0 = 0, h_state = 0, h_rec = 0, h_total = 0;
     char* h_dev = nullptr;   // device-side address of h_out (k_pack writes it over PCIe)
@@ -447,7 +448,8 @@ int build_plan(fpm_ctx* ctx) {
     P.off_warp = 0;
     P.off_ncc = round_up(sizeof(WarpJob) * J, (size_t)256);
     P.off_nms = P.off_ncc + round_up(sizeof(NccJob) * J, (size_t)256);
-    HIP_TRY(P.d_jobs.ensure(P.off_nms + sizeof(NmsJob) * J));
+    P.off_order = P.off_nms + round_up(sizeof(NmsJob) * J, (size_t)256);
+    HIP_TRY(P.d_jobs.ensure(P.off_order + sizeof(int32_t) * J));
     HIP_TRY(P.d_nodes.ensure(sizeof(AngleNode) * std::max<size_t>(noff, 1)));
     HIP_TRY(P.d_top.ensure(sizeof(TopAngle) * P.nang));
     HIP_TRY(P.d_topn.ensure(sizeof(AngleNode) * P.nang));
@@ -544,6 +546,21 @@ int build_plan(fpm_ctx* ctx) {
     HIP_TRY(hipMemcpyAsync(P.d_jobs.as<char>(P.off_warp), wj.data(), sizeof(WarpJob) * J, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(P.d_jobs.as<char>(P.off_ncc), nj.data(), sizeof(NccJob) * J, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(P.d_jobs.as<char>(P.off_nms), mj.data(), sizeof(NmsJob) * J, hipMemcpyHostToDevice, ctx->stream));
+    {   // k_top_fused's workgroup -> job order: the angles with the largest map x template work first, every source's
+        // job of an angle together (one launch covers S x nang jobs in ~1.4 rounds of resident workgroups at Src7: the
+        // cheap jobs fill the last round); a scheduling choice only, every job writes its own outputs
+        std::vector<int> ang(P.nang);
+        for (int a = 0; a < P.nang; ++a) ang[a] = a;
+        auto cost = [&](int a) {
+            return (double)P.map_w[a] * P.map_h[a] * tt.w * tt.h + (double)P.top[a].bw * P.top[a].bh;
+        };
+        std::stable_sort(ang.begin(), ang.end(), [&](int x, int y) { return cost(x) > cost(y); });
+        P.order.resize(J);
+        for (int i = 0; i < P.nang; ++i)
+            for (int s = 0; s < S; ++s) P.order[(size_t)i * S + s] = s * P.nang + ang[i];
+        HIP_TRY(hipMemcpyAsync(P.d_jobs.as<char>(P.off_order), P.order.data(), sizeof(int32_t) * J,
+                               hipMemcpyHostToDevice, ctx->stream));
+    }
     for (int d = 0; d < L; ++d)
         HIP_TRY(hipMemcpyAsync(P.d_nodes.as<AngleNode>() + P.node_off[d], P.nodes[d].data(),
                                sizeof(AngleNode) * P.nodes[d].size(), hipMemcpyHostToDevice, ctx->stream));
@@ -675,7 +692,7 @@ int enqueue_search(fpm_ctx* ctx) {
         ProfScope ps(ctx, FPM_K_TOP_NCC, bytes * S);
         launch_top_fused(P.d_jobs.as<WarpJob>(P.off_warp), P.d_jobs.as<NccJob>(P.off_ncc), na, J, fused_lds,
                          pyr_zero ? nullptr : P.d_livecnt.as<int32_t>(), pyr_zero ? 0 : P.nzero, st,
-                         top_init ? &ca : nullptr);
+                         top_init ? &ca : nullptr, P.d_jobs.as<int32_t>(P.off_order));
         cand_fused = top_init;
     }
     // profiling bytes: each kernel's share of §8(d)'s B_top = sum_angles (W_L H_L + 4 |R_a|): the rotation reads the

@@ -186,8 +186,11 @@ size_t top_fused_lds_limit();   // 64 KB minus k_top_fused's static LDS (hipFunc
 constexpr int kTopFusedMinJobs = 256;   // fewer jobs than CUs: the three split kernels finish sooner
 // ci (cap <= kNmsInitCap): the candidate init fused as in k_nms; the live counter must be zero before the launch
 // (zero / nzero are then 0: block 0's clearing would race with the other blocks' atomics)
+// order (optional): the job each workgroup takes, costliest angles first (fewer workgroups than resident slots are
+// left for the last round)
 void launch_top_fused(const WarpJob* wjobs, const NccJob* njobs, const NmsArgs& a, int njobs_n, size_t lds,
-                      int32_t* zero, int nzero, hipStream_t st, const CandInitArgs* ci = nullptr);
+                      int32_t* zero, int nzero, hipStream_t st, const CandInitArgs* ci = nullptr,
+                      const int32_t* order = nullptr);
 void launch_roi_tables(const RoiArgs& a, hipStream_t st);
 void launch_roi_warp(const RoiArgs& a, hipStream_t st);
 void launch_roi_corr(const RoiArgs& a, hipStream_t st);

@@ -1523,7 +1523,7 @@ constexpr int kTopThreads = 256;   // k_top_fused workgroup (measured: 512 threa
 __global__ __launch_bounds__(kTopThreads) void k_top_fused(const WarpJob* __restrict__ wjobs,
                                                            const NccJob* __restrict__ njobs,
                                                            NmsArgs a, int32_t* zero, int nzero, int abl,
-                                                           CandInitArgs ci, int ci_mode) {
+                                                           CandInitArgs ci, int ci_mode, const int32_t* order) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tf_lds[];
     __shared__ float sv[kTopThreads / 64];
     __shared__ int si[kTopThreads / 64];
@@ -1532,13 +1532,14 @@ __global__ __launch_bounds__(kTopThreads) void k_top_fused(const WarpJob* __rest
     const int tid = threadIdx.x;
     if (blockIdx.x == 0)
         for (int i = tid; i < nzero; i += kTopThreads) zero[i] = 0;
-    const WarpJob& w = wjobs[blockIdx.x];
-    const NccJob& j = njobs[blockIdx.x];
+    const int job = order ? order[blockIdx.x] : (int)blockIdx.x;
+    const WarpJob& w = wjobs[job];
+    const NccJob& j = njobs[job];
     const int dw = w.dw, dh = w.dh, cpw = ((dw + 3) >> 2) + 1;   // canvas words per row (+1: the funnel reads)
     const int tw = j.tw, th = j.th, ntw = (tw + 3) >> 2, ow = j.ow, oh = j.oh, n = ow * oh;
     if (n <= 0) {   // uniform: no map for this angle (TemplateMatcher.cpp:176-178)
-        if (tid == 0) a.counts[blockIdx.x] = 0;
-        if (ci_mode) cand_init_job(ci, ci_mode, blockIdx.x, 0, spk, &sbase);
+        if (tid == 0) a.counts[job] = 0;
+        if (ci_mode) cand_init_job(ci, ci_mode, job, 0, spk, &sbase);
         return;
     }
     uint32_t* Cw = tf_lds;                        // [dh][cpw] canvas, zero past dw
@@ -1619,15 +1620,15 @@ __global__ __launch_bounds__(kTopThreads) void k_top_fused(const WarpJob* __rest
     }
     __syncthreads();
     // K5 (plain getNextMaxLoc, TemplateMatcher.cpp:197-212 / :1196-1206) on the LDS map
-    Peak* out = a.peaks + (size_t)blockIdx.x * a.cap;
+    Peak* out = a.peaks + (size_t)job * a.cap;
     const double ov = a.overlap;
     float v = -INFINITY;
     int i = INT_MAX;
     for (int k = tid; k < n; k += kTopThreads) { const float x = Mp[k]; if (x > v) { v = x; i = k; } }
     wg_argmax(v, i, sv, si);
     if ((double)v < a.thr) {
-        if (tid == 0) a.counts[blockIdx.x] = 0;
-        if (ci_mode) cand_init_job(ci, ci_mode, blockIdx.x, 0, spk, &sbase);
+        if (tid == 0) a.counts[job] = 0;
+        if (ci_mode) cand_init_job(ci, ci_mode, job, 0, spk, &sbase);
         return;
     }
     int cnt = 0;
@@ -1661,8 +1662,8 @@ __global__ __launch_bounds__(kTopThreads) void k_top_fused(const WarpJob* __rest
         }
         ++cnt;
     }
-    if (tid == 0) a.counts[blockIdx.x] = cnt;
-    if (ci_mode) cand_init_job(ci, ci_mode, blockIdx.x, cnt, spk, &sbase);
+    if (tid == 0) a.counts[job] = cnt;
+    if (ci_mode) cand_init_job(ci, ci_mode, job, cnt, spk, &sbase);
 }
 
 size_t top_fused_lds(int bw, int bh, int tw, int th) {
@@ -1690,7 +1691,7 @@ size_t top_fused_lds_limit() {
 }
 
 void launch_top_fused(const WarpJob* wjobs, const NccJob* njobs, const NmsArgs& a, int njobs_n, size_t lds,
-                      int32_t* zero, int nzero, hipStream_t st, const CandInitArgs* ci) {
+                      int32_t* zero, int nzero, hipStream_t st, const CandInitArgs* ci, const int32_t* order) {
     if (njobs_n <= 0) return;
     static const int abl = getenv("FPM_TOP_ABL") ? atoi(getenv("FPM_TOP_ABL")) : 0;   // profiling ablations only
     CandInitArgs cz{};
@@ -1703,8 +1704,9 @@ void launch_top_fused(const WarpJob* wjobs, const NccJob* njobs, const NmsArgs& 
                      mode);
         std::abort();
     }
+    static const bool use_order = !(getenv("FPM_TOP_ORDER") && atoi(getenv("FPM_TOP_ORDER")) == 0);   // A/B only
     hipLaunchKernelGGL(k_top_fused, dim3(njobs_n), dim3(kTopThreads), lds, st, wjobs, njobs, a, zero, nzero, abl,
-                       fuse ? *ci : cz, mode);
+                       fuse ? *ci : cz, mode, use_order ? order : nullptr);
 }
 
 // ============================================================================================== K6+K7+K8
