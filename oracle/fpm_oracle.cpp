@@ -15,7 +15,9 @@
 // Pinning.  The reference cannot be compiled here (OpenCV absent), so this restatement is
 // pinned by constructed known-answer tests (tests/test_oracle_kat.py) and by the committed golden vectors
 // it generated (tests/golden/).  Against real OpenCV the parity is UNPINNED; the one intentional deviation
-// is TM_CCORR, restated as the exact integer sum rounded once to f32 (Appendix A.4).
+// is TM_CCORR, restated as the exact integer sum rounded once to f32 (Appendix A.4).  A test-only second mode
+// (orc_set_ccorr_mode(h, 1)) computes TM_CCORR as OpenCV's crossCorr does, in float32 DFTs, to measure how the
+// reference's screenshots respond to that arithmetic (cross_corr_f32 below; tests/test_reference_pins.py).
 //
 // Build: oracle/Makefile (g++ -O3, -ffp-contract=off, no -ffast-math: the float/double operation order
 // below IS the contract).
@@ -472,6 +474,129 @@ struct SearchStats {
 };
 static const int kTraceCols = 19;
 
+// ---------------------------------------------------------------------------------------------------
+// cv::matchTemplate(TM_CCORR) as OpenCV's CPU crossCorr computes it: float32 DFTs (SENSITIVITY MODE).
+//
+// Every TM_CCORR call of the reference goes through OpenCV's crossCorr (imgproc/src/templmatch.cpp, 4.5.x,
+// non-IPP): for 8-bit inputs the working depth is CV_32F, the correlation map is tiled into blocks of
+// max(round(4.5 * templ), 256 - templ + 1) (clipped to the map), each block's image window and the template are
+// zero-padded to getOptimalDFTSize(block + templ - 1), and the block is Re(IDFT(DFT(img) * conj(DFT(templ))))
+// scaled by 1 / (W * H), all in float32.  Callers: the top layer always (TemplateMatcher.cpp:177 -> :514,
+// MatchToolDlg.cpp:858 -> :1304) and every refinement layer when SIMD is off (:489 / MatchToolDlg.cpp:1277, whose
+// "SIMD" checkbox is unchecked by default: MatchTool.rc:118 has no BS_CHECKED state and nothing sets it).
+//
+// OpenCV's own DFT kernels (CCS-packed real transforms, its radix order) are not reproduced: this is a plain
+// mixed-radix (2/3/5) complex DIT FFT in float32 with double-computed twiddles rounded to float, i.e. arithmetic of
+// the same precision and block structure whose rounding noise has the same magnitude, not the same bits.  It is a
+// test-only mode (orc_set_ccorr_mode) used to measure how the reference-held screenshots respond to float TM_CCORR
+// (tests/test_reference_pins.py); the parity mode (0) stays the exact integer sum rounded once (Appendix A.4).
+// ---------------------------------------------------------------------------------------------------
+static int optimal_dft_size(int n) {   // cv::getOptimalDFTSize: the smallest 2^a 3^b 5^c >= n
+    if (n <= 1) return 1;
+    for (int m = n;; ++m) {
+        int r = m;
+        for (int p : {2, 3, 5})
+            while (r % p == 0) r /= p;
+        if (r == 1) return m;
+    }
+}
+
+struct Cf { float re, im; };
+
+class Fft32 {
+public:
+    explicit Fft32(int n) : n_(n), tw_(n) {
+        for (int k = 0; k < n; ++k) {
+            double a = -2.0 * kPi * k / n;
+            tw_[k].re = (float)std::cos(a);
+            tw_[k].im = (float)std::sin(a);
+        }
+    }
+    // in-place 1-D transform of n elements spaced by `stride` (forward e^{-2 pi i jk/n}; inverse unscaled)
+    void run(Cf* x, int stride, bool inverse) {
+        buf_.resize(n_);
+        out_.resize(n_);
+        for (int i = 0; i < n_; ++i) buf_[i] = x[(size_t)i * stride];
+        rec(buf_.data(), 1, out_.data(), n_, 1, inverse);
+        for (int i = 0; i < n_; ++i) x[(size_t)i * stride] = out_[i];
+    }
+
+private:
+    int n_;
+    std::vector<Cf> tw_, buf_, out_;
+    Cf w(int k, bool inverse) const {
+        Cf t = tw_[k % n_];
+        if (inverse) t.im = -t.im;
+        return t;
+    }
+    void rec(const Cf* in, int stride, Cf* out, int n, int tstep, bool inverse) {
+        if (n == 1) { out[0] = in[0]; return; }
+        int p = n % 2 == 0 ? 2 : n % 3 == 0 ? 3 : 5;
+        int m = n / p;
+        for (int r = 0; r < p; ++r) rec(in + (size_t)r * stride, stride * p, out + (size_t)r * m, m, tstep * p, inverse);
+        Cf xr[5], y[5];
+        for (int k = 0; k < m; ++k) {
+            for (int r = 0; r < p; ++r) {
+                Cf a = out[r * m + k], t = w(r * k * tstep, inverse);
+                xr[r].re = a.re * t.re - a.im * t.im;
+                xr[r].im = a.re * t.im + a.im * t.re;
+            }
+            for (int q = 0; q < p; ++q) {
+                Cf s = xr[0];
+                for (int r = 1; r < p; ++r) {
+                    Cf t = w(((r * q) % p) * (n_ / p), inverse);
+                    s.re += xr[r].re * t.re - xr[r].im * t.im;
+                    s.im += xr[r].re * t.im + xr[r].im * t.re;
+                }
+                y[q] = s;
+            }
+            for (int q = 0; q < p; ++q) out[k + q * m] = y[q];
+        }
+    }
+};
+
+// 2-D transform of a dh x dw complex array (rows, then columns)
+static void fft2_f32(std::vector<Cf>& a, int dw, int dh, bool inverse) {
+    Fft32 fr(dw), fc(dh);
+    for (int y = 0; y < dh; ++y) fr.run(a.data() + (size_t)y * dw, 1, inverse);
+    for (int x = 0; x < dw; ++x) fc.run(a.data() + x, dw, inverse);
+}
+
+// OpenCV crossCorr (templmatch.cpp, 4.5.x) for one 8-bit image and template, anchor (0, 0), delta 0
+static void cross_corr_f32(const Mat8& img, const Mat8& t, MatF& corr) {
+    corr = MatF(img.w - t.w + 1, img.h - t.h + 1, 0.f);
+    const double blockScale = 4.5;
+    const int minBlockSize = 256;
+    int bw = (int)std::lrint(t.w * blockScale), bh = (int)std::lrint(t.h * blockScale);
+    bw = std::min(std::max(bw, minBlockSize - t.w + 1), corr.w);
+    bh = std::min(std::max(bh, minBlockSize - t.h + 1), corr.h);
+    const int dw = std::max(optimal_dft_size(bw + t.w - 1), 2), dh = optimal_dft_size(bh + t.h - 1);
+    bw = std::min(dw - t.w + 1, corr.w);
+    bh = std::min(dh - t.h + 1, corr.h);
+    std::vector<Cf> ft((size_t)dw * dh, Cf{0.f, 0.f}), fi((size_t)dw * dh);
+    for (int y = 0; y < t.h; ++y)
+        for (int x = 0; x < t.w; ++x) ft[(size_t)y * dw + x].re = (float)t.row(y)[x];
+    fft2_f32(ft, dw, dh, false);
+    const float scale = (float)(1.0 / ((double)dw * dh));
+    for (int y0 = 0; y0 < corr.h; y0 += bh)
+        for (int x0 = 0; x0 < corr.w; x0 += bw) {
+            int bsw = std::min(bw, corr.w - x0), bsh = std::min(bh, corr.h - y0);
+            int sw = bsw + t.w - 1, sh = bsh + t.h - 1;
+            std::fill(fi.begin(), fi.end(), Cf{0.f, 0.f});
+            for (int y = 0; y < sh; ++y)
+                for (int x = 0; x < sw; ++x) fi[(size_t)y * dw + x].re = (float)img.row(y0 + y)[x0 + x];
+            fft2_f32(fi, dw, dh, false);
+            for (size_t i = 0; i < fi.size(); ++i) {   // mulSpectrums(img, templ, conjB = true)
+                Cf a = fi[i], b = ft[i];
+                fi[i].re = a.re * b.re + a.im * b.im;
+                fi[i].im = a.im * b.re - a.re * b.im;
+            }
+            fft2_f32(fi, dw, dh, true);
+            for (int y = 0; y < bsh; ++y)
+                for (int x = 0; x < bsw; ++x) corr.at(y0 + y, x0 + x) = fi[(size_t)y * dw + x].re * scale;
+        }
+}
+
 class Matcher {
 public:
     fpm_params prm;
@@ -479,6 +604,7 @@ public:
     double last_seconds = 0.0;
     SearchStats stats;
     bool trace = false;
+    int ccorr_mode = 0;   // TM_CCORR arithmetic: 0 = exact integer sum rounded once (parity), 1 = f32 DFT (above)
 
     Matcher() { fpm_params_default(&prm); }
 
@@ -544,6 +670,8 @@ public:
                         acc = acc + (float)row_dot(t.row(tr), src.row(r + tr) + c, t.w);
                     res.at(r, c) = acc;
                 }
+        } else if (ccorr_mode == 1) {
+            cross_corr_f32(src, t, res);   // test-only sensitivity mode (see cross_corr_f32)
         } else {
             // cv::matchTemplate(TM_CCORR): exact integer sum rounded once to f32 (Appendix A.4)
             for (int r = 0; r < res.h; ++r)
@@ -1142,6 +1270,25 @@ int orc_candidates(void* h, fpm_candidate* out, int cap) {
     int n = (int)m->stats.cands.size();
     for (int i = 0; i < n && i < cap; ++i) out[i] = m->stats.cands[i];
     return n;
+}
+
+// TM_CCORR arithmetic of the next matches: 0 = exact (the parity contract), 1 = OpenCV crossCorr in float32 DFTs
+// (sensitivity mode for the reference-held screenshots; see orc::cross_corr_f32)
+int orc_set_ccorr_mode(void* h, int mode) {
+    if (mode != 0 && mode != 1) return FPM_E_INVALID_ARG;
+    ((orc::Matcher*)h)->ccorr_mode = mode;
+    return FPM_OK;
+}
+
+// the f32-DFT TM_CCORR map of one image and template (both u8, contiguous rows given by stride), for the KAT
+// that checks it against numpy's float32 FFT and the exact sum
+int orc_cross_corr_f32(const uint8_t* img, int w, int h, size_t is, const uint8_t* t, int tw, int th, size_t ts,
+                       float* out) {
+    if (tw > w || th > h || tw <= 0 || th <= 0) return FPM_E_INVALID_ARG;
+    orc::MatF r;
+    orc::cross_corr_f32(orc::from_strided(img, w, h, is), orc::from_strided(t, tw, th, ts), r);
+    std::memcpy(out, r.px.data(), r.px.size() * sizeof(float));
+    return FPM_OK;
 }
 
 // refinement decision trace of the next matches (diagnostic): rows of 19 doubles, see SearchStats::trace

@@ -55,6 +55,9 @@ def load(path: str = ORACLE_LIB):
                                 C.POINTER(C.c_float)]
     lib.orc_rotrect_overlap.argtypes = [C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_double),
                                         C.POINTER(C.c_int)]
+    lib.orc_set_ccorr_mode.argtypes = [C.c_void_p, C.c_int]
+    lib.orc_cross_corr_f32.argtypes = [_U8P, C.c_int, C.c_int, C.c_size_t, _U8P, C.c_int, C.c_int, C.c_size_t,
+                                       C.POINTER(C.c_float)]
     lib.fpm_params_default.argtypes = [C.POINTER(Params)]
     _libs[path] = lib
     return lib
@@ -86,6 +89,19 @@ def rotation_matrix(cx: float, cy: float, angle: float) -> np.ndarray:
     m = (C.c_double * 6)()
     load().orc_rotation_matrix(cx, cy, angle, m)
     return np.array(m[:], np.float64).reshape(2, 3)
+
+
+def cross_corr_f32(img: np.ndarray, templ: np.ndarray) -> np.ndarray:
+    """TM_CCORR map as OpenCV's crossCorr computes it (float32 DFTs, block structure): the oracle's sensitivity
+    mode, not the parity contract."""
+    img = np.ascontiguousarray(img, np.uint8)
+    templ = np.ascontiguousarray(templ, np.uint8)
+    (h, w), (th, tw) = img.shape, templ.shape
+    out = np.zeros((h - th + 1, w - tw + 1), np.float32)
+    rc = load().orc_cross_corr_f32(_u8(img), w, h, img.strides[0], _u8(templ), tw, th, templ.strides[0],
+                                   out.ctypes.data_as(C.POINTER(C.c_float)))
+    assert rc == 0
+    return out
 
 
 def rotrect_overlap(a, b):
@@ -155,6 +171,12 @@ class OracleMatcher:
         if n:
             self._lib.orc_candidates(self._h, out.ctypes.data_as(C.c_void_p), n)
         return out
+
+    def set_ccorr_mode(self, mode: int):
+        """TM_CCORR arithmetic of the next searches: 0 = exact integer sum rounded once (parity), 1 = OpenCV's
+        float32-DFT crossCorr (sensitivity mode for the reference's screenshots)."""
+        assert self._lib.orc_set_ccorr_mode(self._h, int(mode)) == 0
+        return self
 
     def set_trace(self, on: bool = True):
         self._lib.orc_set_trace(self._h, 1 if on else 0)

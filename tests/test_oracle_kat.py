@@ -178,3 +178,25 @@ def test_rotrect_overlap_cases():
     assert t == 0                                           # disjoint -> INTERSECT_NONE
     t, area, n = oracle.rotrect_overlap(sq, [(5, 0), (15, 0), (15, 10)])
     assert t == 1 and n == 4 and area == pytest.approx(50.0)
+
+
+@pytest.mark.parametrize("shape,tshape", [((70, 90), (17, 24)), ((300, 280), (40, 31)), ((12, 9), (12, 9))])
+def test_cross_corr_f32_sensitivity_mode(shape, tshape):
+    """The oracle's float32-DFT TM_CCORR (sensitivity mode, OpenCV crossCorr's block structure; the 300x280 case
+    spans several DFT blocks) against the exact integer sum: its error is of float32 DFT size -- the same order as
+    numpy's float32 FFT of the same product."""
+    rng = np.random.default_rng(sum(shape) + sum(tshape))
+    img = rng.integers(0, 256, shape, dtype=np.uint8)
+    t = rng.integers(0, 256, tshape, dtype=np.uint8)
+    got = oracle.cross_corr_f32(img, t).astype(np.float64)
+    (h, w), (th, tw) = shape, tshape
+    ex = np.zeros((h - th + 1, w - tw + 1), np.float64)
+    for y in range(th):
+        for x in range(tw):
+            ex += float(t[y, x]) * img[y:y + h - th + 1, x:x + w - tw + 1]
+    H, W = h + th, w + tw
+    A = np.fft.fft2(img.astype(np.float32), s=(H, W))
+    B = np.fft.fft2(t.astype(np.float32), s=(H, W))
+    npf = np.fft.ifft2(A * np.conj(B)).real[:h - th + 1, :w - tw + 1]
+    err, np_err = np.abs(got - ex).max(), np.abs(npf - ex).max()
+    assert err <= 8 * max(np_err, 1.0) and err / ex.max() < 1e-5

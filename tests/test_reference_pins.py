@@ -24,9 +24,14 @@ Where the oracle departs from a screenshot the departure is pinned exactly (``EX
   below.  The exact-decode full order is therefore an expected failure whose cause lies in the unpinned decoder
   (OpenCV's bundled libjpeg, MatchToolDlg.cpp:62), not in the oracle's semantics.
 * Result3 (older build): 34 of the 35 adjacent label pairs are x-ordered; two are not, by one source pixel
-  (labels 21/22 and 30/31).  Src3/Dst3 are lossless 8-bit BMPs and a Tol-0 search is integer from decode to the
-  layer-0 argmax, so no decoder or rounding freedom explains them: they are recorded as a difference of that older
-  build (which also drew different labels and sorted differently), not reproducible from the shipped code.
+  (labels 21/22 and 30/31).  Src3/Dst3 are lossless 8-bit BMPs, but the search is not integer end to end in the
+  reference: its TM_CCORR is OpenCV's float32 DFT crossCorr at the top layer always (MatchToolDlg.cpp:858 -> :1304)
+  and at every refinement layer when the tool's SIMD box is unchecked (:1277; unchecked by default, MatchTool.rc:118).
+  The oracle's sensitivity mode restates that arithmetic (orc_set_ccorr_mode 1, oracle/fpm_oracle.cpp
+  cross_corr_f32); ``test_ccorr_sensitivity`` runs all four pins in {exact, f32 DFT} x {SIMD on, off}: every mode
+  gives the same detections and the same mismatch set, so float TM_CCORR explains neither Result3's two pairs nor
+  Result6's 8/9 swap.  Result3's pairs stay unexplained by anything in the shipped code (recorded as a difference
+  of that older build, which also drew different labels and sorted differently).
 
 Parameters: pins run ``params``; ``fitted`` names the ones chosen by running the oracle (not published).  README
 Test1's published Score 0.8 gives one detection (``count_at_published``), the screenshot shows four: their oracle
@@ -49,8 +54,14 @@ with open(os.path.join(GOLDEN, "reference_pins.json")) as _fh:
 # labels the oracle does not reproduce (score order: labels whose box gets another index; x order: label k with
 # x(k) > x(k+1)), each explained in the module docstring
 EXPECTED_MISMATCH = {"test6_src6": [8, 9], "test4_src3": [21, 30], "test1_src9": [], "test5_src4": []}
-# the pinned decoder-level perturbation of Src6 (scripts/result6_sensitivity.py): salt 2, 1 % of the pixels
-RESULT6_SALT, RESULT6_FRAC = 2, 0.01
+# the pinned decoder-level perturbation of Src6 (scripts/result6_sensitivity.py): FITTED -- salt 2 at 1 % of the
+# pixels is one of the 10 of 32 salts that give the screenshot's full order at that level (6/32 at 0.3 %, 20/32 at
+# 3 %); the JSON records it as fitted together with those rates
+_PERT = PINS["test6_src6"]["perturbation"]
+RESULT6_SALT, RESULT6_FRAC = _PERT["salt"], _PERT["frac"]
+# TM_CCORR sensitivity (scripts/ccorr_sensitivity.py): labels not reproduced per (ccorr mode, use_simd); float32
+# DFT TM_CCORR changes none of them
+CCORR_MODES = [(0, 1), (0, 0), (1, 1), (1, 0)]
 
 
 def _image(name):
@@ -140,6 +151,34 @@ def test_oracle_reproduces_reference_screenshot(name):
     # the same detections (centres: f32 in the Qt class, f64 in the MFC tool)
     key = lambda r: (round(r[8], 2), round(r[9], 2))  # noqa: E731
     assert sorted(map(key, qt[:pin["count"]])) == sorted(map(key, res))
+
+
+def test_result6_perturbation_is_labelled_fitted():
+    assert _PERT["fitted"] is True and _PERT["full_order_rate"]["0.01"] == "10/32"
+
+
+@pytest.mark.parametrize("ccorr,simd", CCORR_MODES)
+@pytest.mark.parametrize("name", sorted(PINS))
+def test_ccorr_sensitivity(name, ccorr, simd, request):
+    """The reference's float TM_CCORR (OpenCV crossCorr in float32 DFTs) as the cause of the residual mismatches:
+    under every (TM_CCORR arithmetic, SIMD) combination the pins give the same count, residual bound and mismatch
+    set as the exact parity mode -- the float path explains none of them -- and the same poses
+    with scores within 1e-5 of it."""
+    if (name, ccorr, simd) == ("test6_src6", 1, 0) and request.config.getoption("-m") == "not gpu and not slow":
+        pytest.skip("34 s on one core: runs in the full CPU suite")
+    pin = PINS[name]
+    s, t = _load(pin)
+    o = oracle.OracleMatcher().set(semantics=1, **dict(pin["params"], use_simd=simd)).set_ccorr_mode(ccorr)
+    assert o.learnPattern(t)
+    res = o.match(s)
+    assert len(res) == pin["count"]
+    assert cross_residual(pin, s.shape, res) < 1.5
+    assert label_mismatches(pin, s.shape, res) == EXPECTED_MISMATCH[name]
+    # against the parity mode: the same poses (centres, angles) and scores within north_star's 1e-5
+    base = _search(s, t, semantics=1, **pin["params"])
+    for r in res:
+        b = min(base, key=lambda q: (q[8] - r[8]) ** 2 + (q[9] - r[9]) ** 2)
+        assert (b[8], b[9], b[10]) == (r[8], r[9], r[10]) and abs(b[11] - r[11]) < 1e-5
 
 
 def test_test1_at_published_score():
