@@ -767,27 +767,12 @@ int enqueue_search(fpm_ctx* ctx) {
         ra.thr = P.layer_score[l];
         const int total_rois = P.C * P.n3;
         const bool small = roi_small_fits(tl.w, tl.h);   // one-kernel refinement of the ROI in LDS
-        // FPM_ROI_FUSED=1 (measurement only): K6+K7 as one kernel (k_roi_fused), the ROI kept on chip; bit-identical
-        // but 20-40 % slower than the split chain on MI355X, so not the default
-        const char* fused_env_s = getenv("FPM_ROI_FUSED");   // read when the search is recorded (once per plan)
-        const bool fused_env = fused_env_s && atoi(fused_env_s) != 0;
-        const bool fused = !small && fused_env && roi_fused_fits(tl.w);
-        ra.nparts = roi_fused_parts(tl.h);
         for (int base = 0; base < total_rois; base += P.slot_cap) {
             ra.slot_base = base;
             ra.slot_cap = std::min(P.slot_cap, total_rois - base);
             if (small) {
                 ProfScope ps(ctx, FPM_K_ROI_SMALL, 0);
                 launch_roi_small(ra, st);
-                continue;
-            }
-            if (fused) {
-                {
-                    ProfScope ps(ctx, FPM_K_ROI_CORR, 0);
-                    launch_roi_fused(ra, st);
-                }
-                ProfScope ps(ctx, FPM_K_ROI_EVAL, 0);
-                launch_roi_eval(ra, st);
                 continue;
             }
             {

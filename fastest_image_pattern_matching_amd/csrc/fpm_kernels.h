@@ -195,9 +195,11 @@ void launch_roi_tables(const RoiArgs& a, hipStream_t st);
 void launch_roi_warp(const RoiArgs& a, hipStream_t st);
 void launch_roi_corr(const RoiArgs& a, hipStream_t st);
 void launch_roi_eval(const RoiArgs& a, hipStream_t st);
+#ifdef FPM_EXPERIMENTAL   // measurement-only fused K6+K7 (scripts/fused_bench.hip; never in libfpm_hip.so)
 bool roi_fused_fits(int tw);           // the fused sampling + correlation kernel applies (templates <= 1024 wide)
 int roi_fused_parts(int th);           // runs of bands per ROI (work units per ROI) of k_roi_fused
 void launch_roi_fused(const RoiArgs& a, hipStream_t st);
+#endif
 bool roi_small_fits(int tw, int th);   // the single-kernel small-template refinement applies
 size_t roi_small_lds(int tw, int th);
 void launch_roi_small(const RoiArgs& a, hipStream_t st);

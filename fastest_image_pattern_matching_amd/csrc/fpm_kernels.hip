@@ -1517,12 +1517,12 @@ void launch_cand_init(const CandInitArgs& a, hipStream_t st) {
 // all in LDS -- no canvas or map round trip through HBM and two launches fewer per search.  The engine uses it when
 // the plain peak path applies and the largest canvas + map fit top_fused_lds() <= top_fused_lds_limit(); block 0 zeroes the
 // search's counters (as k_warp does on the split path).  Src7, 43 sources (1763 jobs): 75.5 us per launch against
-// 106.4 for k_warp + k_ncc_tile + k_nms; ablations (abl, profiling only: 1 no taps, 2 no correlation, 4 no peak
-// loop) put 21 us in the taps, 19 in the correlation, 3 in the peak loop.
+// 106.4 for k_warp + k_ncc_tile + k_nms; round-3 ablations (a profiling build, since removed from the product) put
+// 21 us in the taps, 19 in the correlation, 3 in the peak loop.
 constexpr int kTopThreads = 256;   // k_top_fused workgroup (measured: 512 threads per job no faster)
 __global__ __launch_bounds__(kTopThreads) void k_top_fused(const WarpJob* __restrict__ wjobs,
                                                            const NccJob* __restrict__ njobs,
-                                                           NmsArgs a, int32_t* zero, int nzero, int abl,
+                                                           NmsArgs a, int32_t* zero, int nzero,
                                                            CandInitArgs ci, int ci_mode, const int32_t* order) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tf_lds[];
     __shared__ float sv[kTopThreads / 64];
@@ -1567,7 +1567,7 @@ __global__ __launch_bounds__(kTopThreads) void k_top_fused(const WarpJob* __rest
             if (x >= dw) break;
             const int ad = tab[x], bd = tab[dw + x];
             const int X = (X0 + ad) >> (kAbBits - kInterBits), Y = (Y0 + bd) >> (kAbBits - kInterBits);
-            word |= (uint32_t)(abl & 1 ? 0 : warp_tap(w.src, w.sw, w.sh, w.sp, X, Y, w.border)) << (8 * b);
+            word |= (uint32_t)warp_tap(w.src, w.sw, w.sh, w.sp, X, Y, w.border) << (8 * b);
         }
         Cw[i] = word;
     }
@@ -1590,7 +1590,6 @@ __global__ __launch_bounds__(kTopThreads) void k_top_fused(const WarpJob* __rest
     // sums (<= 128 * 64 * 255^2 < 2^32)
     const int ngx = (ow + 3) >> 2;
     for (int it = tid; it < oh * ngx; it += kTopThreads) {
-        if (abl & 2) { const int y = it / ngx, q = it - y * ngx; for (int u = 0; u < 4 && 4 * q + u < ow; ++u) Mp[y * ow + 4 * q + u] = 0.5f + 1e-3f * (float)((y * 7 + q * 3 + u) % 97); continue; }
         const int y = it / ngx, q = it - y * ngx;
         uint32_t d[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
         for (int r = 0; r < th; ++r) {
@@ -1638,7 +1637,7 @@ __global__ __launch_bounds__(kTopThreads) void k_top_fused(const WarpJob* __rest
         if (ci_mode) { spk[0].x = px; spk[0].y = py; spk[0].score = v; }
     }
     ++cnt;
-    for (int itn = 0; itn < ((abl & 4) ? 0 : a.cap - 1); ++itn) {
+    for (int itn = 0; itn < a.cap - 1; ++itn) {
         const int sx = (int)(px - a.tw * (1 - ov)), sy = (int)(py - a.th * (1 - ov));
         const int rw = (int)(2 * a.tw * (1 - ov)), rh = (int)(2 * a.th * (1 - ov));
         if (rw > 0 && rh > 0) {
@@ -1693,7 +1692,6 @@ size_t top_fused_lds_limit() {
 void launch_top_fused(const WarpJob* wjobs, const NccJob* njobs, const NmsArgs& a, int njobs_n, size_t lds,
                       int32_t* zero, int nzero, hipStream_t st, const CandInitArgs* ci, const int32_t* order) {
     if (njobs_n <= 0) return;
-    static const int abl = getenv("FPM_TOP_ABL") ? atoi(getenv("FPM_TOP_ABL")) : 0;   // profiling ablations only
     CandInitArgs cz{};
     const bool fuse = ci && a.cap <= kNmsInitCap;
     const int mode = !fuse ? 0 : (ci->refine == 0 ? 1 : (ci->refine == 2 ? 3 : 2));
@@ -1704,9 +1702,8 @@ void launch_top_fused(const WarpJob* wjobs, const NccJob* njobs, const NmsArgs& 
                      mode);
         std::abort();
     }
-    static const bool use_order = !(getenv("FPM_TOP_ORDER") && atoi(getenv("FPM_TOP_ORDER")) == 0);   // A/B only
-    hipLaunchKernelGGL(k_top_fused, dim3(njobs_n), dim3(kTopThreads), lds, st, wjobs, njobs, a, zero, nzero, abl,
-                       fuse ? *ci : cz, mode, use_order ? order : nullptr);
+    hipLaunchKernelGGL(k_top_fused, dim3(njobs_n), dim3(kTopThreads), lds, st, wjobs, njobs, a, zero, nzero,
+                       fuse ? *ci : cz, mode, order);
 }
 
 // ============================================================================================== K6+K7+K8
@@ -2958,6 +2955,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
+#ifdef FPM_EXPERIMENTAL   // measurement-only kernel (scripts/fused_bench.hip); the product Makefile never defines it
 // ---- K6+K7 fused (templates too large for k_roi_small): the ROI never leaves the CU.  A work unit is one ROI and
 // one run of consecutive 32-row template bands; a workgroup walks its run band by band:
 //   the band's new ROI rows are sampled straight into an LDS ring of kBandSrc rows (32x32 tiles: the tile's
@@ -3212,6 +3210,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         }
     }
 }
+#endif   // FPM_EXPERIMENTAL
 
 // ---- K6-K8 for small templates: one workgroup per ROI does the whole refinement of the ROI in LDS (tables,
 // 32x32-tile sampling from wave footprints, exact row / window sums, the band-by-band banded GEMM on the matrix
@@ -3844,9 +3843,8 @@ void launch_roi_corr(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0 || a.equal1) return;
     const size_t lds = roi_corr_lds(a.roi_pitch, a.tw, a.rc, kCorrGlobalA);
     // register-A form where its staged rows fit one 64-lane pass and A fits 16 k-steps (templates <= 1024 wide);
-    // FPM_CORR_SLOTMAJOR=1 forces the slot-major form (profiling comparisons)
-    static const bool slot_major = getenv("FPM_CORR_SLOTMAJOR") && atoi(getenv("FPM_CORR_SLOTMAJOR")) != 0;
-    if (!slot_major && (a.roi_pitch >> 4) <= 64 && a.nk <= 16 && lds <= 65536) {
+    // the slot-major form below serves wider templates
+    if ((a.roi_pitch >> 4) <= 64 && a.nk <= 16 && lds <= 65536) {
         const long items = (long)a.slot_cap * ((a.th + kBandRows - 1) / kBandRows);
         if (a.nk <= 4) launch_corr_regs<4>(a, items, lds, st);
         else if (a.nk <= 8) launch_corr_regs<8>(a, items, lds, st);
@@ -3860,6 +3858,7 @@ void launch_roi_corr(const RoiArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((k_roi_corr<0, kCorrGlobalA, kCorrWaves>), dim3(grid), dim3(256), lds, st, a);
 }
 
+#ifdef FPM_EXPERIMENTAL
 void launch_roi_fused(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0 || a.equal1) return;
     const size_t lds = (size_t)fuse_layout(a.tw).total;
@@ -3870,6 +3869,7 @@ void launch_roi_fused(const RoiArgs& a, hipStream_t st) {
     else if (a.nk <= 12) hipLaunchKernelGGL(k_roi_fused<12>, dim3(grid), dim3(256), lds, st, a);
     else hipLaunchKernelGGL(k_roi_fused<16>, dim3(grid), dim3(256), lds, st, a);
 }
+#endif
 
 void launch_roi_eval(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0) return;

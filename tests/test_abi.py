@@ -58,3 +58,42 @@ def test_library_is_gfx950_code_object():
     blob = open(_lib.LIB_PATH, "rb").read()
     assert b"gfx950" in blob
     assert b"gfx942" not in blob and b"gfx90a" not in blob
+
+
+def _kernel_symbols():
+    import shutil
+    import subprocess
+
+    so = os.path.join(REPO, "fastest_image_pattern_matching_amd", "lib", "libfpm_hip.so")
+    nm = shutil.which("nm")
+    if not (nm and os.path.exists(so)):
+        pytest.skip("nm or libfpm_hip.so missing")
+    out = subprocess.run([nm, "-C", so], capture_output=True, text=True, check=True).stdout
+    return sorted({m.group(1) for m in re.finditer(r"(fpm::k_[a-z0-9_]+(?:<[^>]*>)?)\(", out)})
+
+
+def test_product_library_holds_no_measurement_kernels():
+    """The product library carries only result-path kernels: no fused K6+K7 experiment (FPM_EXPERIMENTAL builds
+    only, scripts/fused_bench.hip), and every ablation template parameter of k_roi_corr / k_roi_small (MODE) and
+    k_roi_warp (ABL) at its product value 0 -- the profiling instantiations exist only in scripts/*.hip."""
+    ks = _kernel_symbols()
+    assert any(k.startswith("fpm::k_roi_warp3") for k in ks) and any(k.startswith("fpm::k_roi_corr<") for k in ks)
+    assert not [k for k in ks if "k_roi_fused" in k]
+    for k in ks:
+        args = k[k.index("<") + 1:-1].split(", ") if "<" in k else []
+        if k.startswith(("fpm::k_roi_corr<", "fpm::k_roi_small<", "fpm::k_pyr_down<")):
+            assert args[0] == "0", k
+        if k.startswith("fpm::k_roi_warp<"):
+            assert args[1] == "0", k
+
+
+def test_product_switches_are_result_neutral():
+    """Every environment switch the product library reads is a schedule or diagnostic knob whose both settings are
+    parity-tested (DESIGN.md section 1 lists them); none selects an ablation."""
+    csrc = os.path.join(REPO, "fastest_image_pattern_matching_amd", "csrc")
+    names = set()
+    for f in os.listdir(csrc):
+        if f.endswith((".hip", ".cpp", ".h")):
+            names |= set(re.findall(r'getenv\("(FPM_[A-Z0-9_]+)"\)', open(os.path.join(csrc, f)).read()))
+    assert names <= {"FPM_SCRATCH_MB", "FPM_TOP_FUSED", "FPM_OVERLAP_DEVICE_MIN", "FPM_TAIL_TIMES", "FPM_PYR_WGS",
+                     "FPM_PYR_OH", "FPM_WARP3", "FPM_HOST_THREADS", "FPM_POOL_TRACE", "FPM_HOST_WARM"}, names

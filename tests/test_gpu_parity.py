@@ -129,15 +129,19 @@ def test_src7_full_search(hip, templates):
     assert len(gpu) == 3
 
 
-def test_src7_fused_refinement(gpu_matcher_factory, templates, monkeypatch):
-    """The opt-in fused K6+K7 kernel (FPM_ROI_FUSED=1, read when a fresh context records its search) on the full
-    Src7 search: every result field and per-layer live count equal the oracle's, as with the default split chain."""
-    monkeypatch.setenv("FPM_ROI_FUSED", "1")
+def test_wide_template_slot_major_correlation(gpu_matcher_factory):
+    """A template wider than 1024 px (18 k-steps of 64 bytes): layer 0's correlation runs the slot-major
+    k_roi_corr form (the register-A form holds at most 16 k-steps) -- every result field and live count equal the
+    oracle's."""
+    t = synth.box_blur(synth.noise(1100, 300, 128, 50, 61), 3)
+    s = synth.box_blur(synth.noise(2600, 1400, 128, 50, 62), 3)
+    synth.paste_rotated(s, t, 1300.0, 420.0, 4.0)
+    synth.paste_rotated(s, t, 1290.0, 1000.0, -7.0)
     m = gpu_matcher_factory()
-    s, t = synth.src7_scene(templates["Dst7"])
-    gpu, orc, ostats, gstats = _run_both(m, s, t, max_pos=3, tolerance_angle=180.0, score=0.7)
+    gpu, orc, ostats, gstats = _run_both(m, s, t, max_pos=2, tolerance_angle=10.0, score=0.6)
     assert gstats == ostats
-    assert_same_results(gpu, orc, "src7 fused")
+    assert_same_results(gpu, orc, "wide template")
+    assert len(gpu) == 2
 
 
 @pytest.mark.parametrize("top_fused", ["0", "1"])
