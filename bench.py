@@ -148,6 +148,23 @@ def cpu_baseline(templ, src, budget_s):
     return base, variants
 
 
+def oracle_verify(templ, sources, refs):
+    """The timed work against the parity oracle: the oracle's search of each given source equals the GPU results of
+    that source field for field (the GPU results are the reference pass's, which the timed pass reproduces exactly,
+    `verify`).  Test infrastructure as the checker only; returns the number of sources checked or raises."""
+    from tests import oracle
+
+    o = oracle.OracleMatcher().set(**PARAMS)
+    assert o.learnPattern(templ)
+    for s, r in zip(sources, refs):
+        exp = o.match(s)
+        got = [x.as_tuple() for x in r]
+        if got != exp:
+            log("[bench] GPU results differ from the oracle on a timed source:\n{got}\n{exp}")
+            sys.exit(4)
+    return len(sources)
+
+
 def kernel_pass(m, sources, steps, L):
     """Kernel-level pass: one context over its share of the step's sources (the same launches as one context's pass
     in the timed run), eager launches with HIP events around each kernel on the library's stream (the kernels' own
@@ -478,6 +495,14 @@ def main():
         "roofline_corr": roofline_corr,
     }
     if world == 1 and rank == 0 and args.cpu_budget > 0:
+        # the CPU leg first checks the timed work against the oracle: the reference pass (== the timed pass, verify)
+        # equals the oracle on the first source of every context -- the benched 128-source, 3-context configuration
+        # itself; exit 4 on any difference
+        firsts = [i * args.batch // G for i in range(G)]
+        out["oracle_verified"] = {
+            "sources": oracle_verify(templ, [sources[i] for i in firsts], [ref[i] for i in firsts]),
+            "of": args.batch, "what": "first source of every context: GPU results == oracle/fpm_oracle.cpp, every "
+                                      "s_SingleTargetMatch field bit-identical (else exit 4)"}
         log("[rank 0] CPU baseline (oracle restatement: 1 thread, fast-math 1 thread, all cores)")
         out["cpu_baseline"], out["cpu_baseline_variants"] = cpu_baseline(templ, sources[0], args.cpu_budget)
         out["cpu_baseline"].update(cpu_identity())

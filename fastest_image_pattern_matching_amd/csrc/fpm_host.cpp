@@ -115,8 +115,19 @@ Pool* pool_instance(int workers) {
 }
 }  // namespace
 
+// FPM_HOST_WARM: 0 turns the warm-up off (processes sharing the host with other work), a positive value caps the
+// spin in microseconds (default 10000); the warm-up only moves when the tail's workers start, never its results
+static int host_warm_cap_us() {
+    static const int cap = [] {
+        const char* e = std::getenv("FPM_HOST_WARM");
+        return e ? std::max(0, atoi(e)) : 10000;
+    }();
+    return cap;
+}
+
 void host_pool_warm(int us) {
     const int nthreads = host_thread_count();
+    us = std::min(us, host_warm_cap_us());
     if (nthreads <= 1 || us <= 0) return;
     Pool* p = pool_instance(nthreads - 1);
     p->spin_until.store(Pool::now_ns() + (int64_t)us * 1000, std::memory_order_relaxed);

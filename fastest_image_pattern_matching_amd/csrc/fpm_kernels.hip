@@ -4016,6 +4016,9 @@ __global__ __launch_bounds__(256) void k_overlap_pairs(const OvRect* __restrict_
         }
         if (lane == 0) { offcnt[2 * i] = base; offcnt[2 * i + 1] = nd; }
     }
+    // lists / offcnt / meta live in mapped pinned host memory (not coherent by default): make every store visible
+    // at system scope before the kernel ends, as k_pack does
+    __threadfence_system();
 }
 
 void launch_overlap_pairs(const OvRect* r, const float4* box, int n, double max_overlap, int32_t* lists, int list_cap,
