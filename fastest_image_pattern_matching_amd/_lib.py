@@ -91,6 +91,8 @@ SIGNATURES = {
                                      C.c_int32, C.c_int32, C.c_size_t, C.c_int32]),
     "fpm_op_ncc_map": (C.c_int, [_P, _U8P, C.c_int32, C.c_int32, C.c_size_t, C.c_int32, C.c_int32,
                                  C.POINTER(C.c_float)]),
+    "fpm_op_overlap_filter": (C.c_int, [_P, C.POINTER(C.c_float), C.POINTER(C.c_double), C.c_int32, C.c_double,
+                                        C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "fpm_template_info": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "fpm_template_level": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                      C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double),

@@ -610,7 +610,9 @@ int layout_sources(fpm_ctx* ctx, int count, int w, int h) {
         lw = (lw + 1) / 2;
         lh = (lh + 1) / 2;
     }
-    HIP_TRY(ctx->d_src.ensure(off));
+    // slack: the ROI sampler's footprint staging reads up to 3 rows past a box (k_roi_warp3), i.e. past the last
+    // image's spare row
+    HIP_TRY(ctx->d_src.ensure(off + 4 * (size_t)ctx->src[0].pitch + 256));
     return FPM_OK;
 }
 
@@ -957,10 +959,16 @@ static bool select_distinct_scores(const fpm_params& prm, const fpm_candidate* c
 // caller runs the host filter) without a context, for short lists, or when a rectangle has more overlapping
 // partners than the kernel keeps.
 constexpr int kOverlapDeviceMin = 1024;   // FPM_OVERLAP_DEVICE_MIN overrides (tests force small lists through it)
-static bool overlap_filter_device(fpm_ctx* ctx, std::vector<HostMatch>& v, double max_overlap) {
+struct OverlapStats {
+    int host_pairs = 0, flags = 0, entries = 0;
+};
+static bool overlap_filter_device(fpm_ctx* ctx, std::vector<HostMatch>& v, double max_overlap, int min_n = 0,
+                                  OverlapStats* st = nullptr) {
     const int n = (int)v.size();
-    int min_n = kOverlapDeviceMin;
-    if (const char* e = getenv("FPM_OVERLAP_DEVICE_MIN")) min_n = std::max(1, atoi(e));
+    if (min_n <= 0) {
+        min_n = kOverlapDeviceMin;
+        if (const char* e = getenv("FPM_OVERLAP_DEVICE_MIN")) min_n = std::max(1, atoi(e));
+    }
     if (!ctx || n < min_n) return false;
     const int cap = 48 * n;
     const size_t boff = (sizeof(OvRect) * (size_t)n + 15) / 16 * 16;
@@ -1003,6 +1011,7 @@ static bool overlap_filter_device(fpm_ctx* ctx, std::vector<HostMatch>& v, doubl
         hipStreamSynchronize(ctx->stream) != hipSuccess)
         return false;
     const clk::time_point q2 = clk::now();
+    if (st) { st->flags = hout[1]; st->entries = hout[0]; }
     if (hout[1] != 0) return false;   // a rectangle with too many partners, or the list overflowed
     // the outputs, written by the device into mapped host memory, read once into ordinary memory
     std::vector<int32_t> local((size_t)2 * n + hout[0]);
@@ -1032,6 +1041,7 @@ static bool overlap_filter_device(fpm_ctx* ctx, std::vector<HostMatch>& v, doubl
     for (int i = 0; i < n; ++i)
         if (!del[i]) v[w++] = v[i];
     v.resize(w);
+    if (st) st->host_pairs = host_pairs;
     if (tail_times) {
         auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         fprintf(stderr, "overlap-dev n=%d geom %.3f device %.3f read %.3f replay %.3f ms, %d pair entries, %d decided on the host\n",
@@ -1608,6 +1618,36 @@ int fpm_search_stats(const fpm_ctx* ctx, int64_t* stats, int32_t cap) {
     for (int64_t v : ctx->stats)
         if (n < cap) stats[n++] = v;
     return n;
+}
+
+int fpm_op_overlap_filter(fpm_ctx* ctx, const float* corners, const double* scores, int32_t n, double max_overlap,
+                          int32_t mode, int32_t* keep, int32_t* n_keep, int32_t* stats) {
+    if (!ctx || !n_keep || n < 0 || (n > 0 && (!corners || !scores || !keep)) || (mode != 0 && mode != 1))
+        return FPM_E_INVALID_ARG;
+    *n_keep = 0;
+    if (stats) stats[0] = stats[1] = stats[2] = stats[3] = 0;
+    HIP_TRY(hipSetDevice(ctx->device));
+    std::vector<HostMatch> v((size_t)n);
+    for (int i = 0; i < n; ++i) {
+        HostMatch& m = v[(size_t)i];
+        m = HostMatch{};
+        const float* c = corners + 6 * (size_t)i;
+        m.rect = rrect_from3(f2(c[0], c[1]), f2(c[2], c[3]), f2(c[4], c[5]));
+        m.score = scores[i];
+        m.id = i;
+    }
+    int path = 0;
+    OverlapStats st;
+    if (mode == 1 && n > 0) {
+        path = overlap_filter_device(ctx, v, max_overlap, 1, &st) ? 1 : 2;
+        if (path == 2) filter_with_rotated_rect(v, max_overlap);
+    } else {
+        filter_with_rotated_rect(v, max_overlap);
+    }
+    for (size_t i = 0; i < v.size(); ++i) keep[i] = v[i].id;
+    *n_keep = (int32_t)v.size();
+    if (stats) { stats[0] = path; stats[1] = st.host_pairs; stats[2] = st.flags; stats[3] = st.entries; }
+    return FPM_OK;
 }
 
 int fpm_template_info(const fpm_ctx* ctx, int32_t* levels, int32_t* border_color) {

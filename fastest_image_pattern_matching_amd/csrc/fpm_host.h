@@ -21,6 +21,7 @@ struct HostMatch {
     bool del;
     bool on_border;
     double vec[3][3];
+    int32_t id;   // caller's index (fpm_op_overlap_filter)
 };
 
 RRect rrect_from3(F2 p1, F2 p2, F2 p3);                              // cv::RotatedRect(p1, p2, p3)

@@ -1725,6 +1725,13 @@ constexpr int ROI_FT = 4096;         // per-wave LDS footprint buffer (bytes) >=
 // banks) and a compile-time constant, so a tap's second row is the same ds_read's immediate offset and the byte address
 // is one multiply-add with a constant; boxes up to 16 dwords wide and ROI_FT / 68 = 60 rows stage into LDS
 constexpr int kFtPitch = 68;
+// The per-ROI warp tables in HBM (k_roi_tables) carry OpenCV's AB_BITS fixed point scaled by 2^kTabShift: 16
+// fractional bits, so in a sum of a row and a column entry the integer coordinate is the high half-word (read by the
+// samplers' SDWA word selects, no shift) and OpenCV's INTER_BITS coordinate is the sum >> kTapShift (the scaling is
+// exact: (a << 6) + (b << 6) = (a + b) << 6, and every rounding below the 5 kept fraction bits is a floor either way).
+constexpr int kTabShift = 6;
+constexpr int kTabFrac = kAbBits + kTabShift;           // 16
+constexpr int kTapShift = kTabFrac - kInterBits;        // 11
 
 int roi_pick_rc(int /*tw*/, int th) { return th < ROI_RC ? th : ROI_RC; }
 
@@ -1869,21 +1876,21 @@ __device__ __forceinline__ uint32_t bilerp_row4(const int v[4][4], const int fx[
 // 1689 vs 399 us, round 3): the LDS serves unaligned halfwords, slowly.
 template <int PITCH>
 __device__ __forceinline__ void lds_taps16(const uint32_t off[4], int v[4][4]) {
-#define FPM_TAPS(U)                                                                                                     \
-    asm volatile("ds_read_u8 %0, %4\n\tds_read_u8 %1, %4 offset:1\n\tds_read_u8 %2, %4 offset:%5\n\t"                \
-                 "ds_read_u8 %3, %4 offset:%6"                                                                          \
-                 : "=&v"(v[U][0]), "=&v"(v[U][1]), "=&v"(v[U][2]), "=&v"(v[U][3])                                       \
-                 : "v"(off[U]), "i"(PITCH), "i"(PITCH + 1))
-    FPM_TAPS(0);
-    FPM_TAPS(1);
-    FPM_TAPS(2);
-    FPM_TAPS(3);
-#undef FPM_TAPS
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(v[0][0]), "+v"(v[0][1]), "+v"(v[0][2]), "+v"(v[0][3]), "+v"(v[1][0]), "+v"(v[1][1]),
-                   "+v"(v[1][2]), "+v"(v[1][3]), "+v"(v[2][0]), "+v"(v[2][1]), "+v"(v[2][2]), "+v"(v[2][3]),
-                   "+v"(v[3][0]), "+v"(v[3][1]), "+v"(v[3][2]), "+v"(v[3][3])
-                 :
+    // one statement: the 16 reads and the wait they end with (no compiler-placed copy of a result register can
+    // come between a read and its wait)
+    asm volatile("ds_read_u8 %0, %16\n\tds_read_u8 %1, %16 offset:1\n\tds_read_u8 %2, %16 offset:%20\n\t"
+                 "ds_read_u8 %3, %16 offset:%21\n\t"
+                 "ds_read_u8 %4, %17\n\tds_read_u8 %5, %17 offset:1\n\tds_read_u8 %6, %17 offset:%20\n\t"
+                 "ds_read_u8 %7, %17 offset:%21\n\t"
+                 "ds_read_u8 %8, %18\n\tds_read_u8 %9, %18 offset:1\n\tds_read_u8 %10, %18 offset:%20\n\t"
+                 "ds_read_u8 %11, %18 offset:%21\n\t"
+                 "ds_read_u8 %12, %19\n\tds_read_u8 %13, %19 offset:1\n\tds_read_u8 %14, %19 offset:%20\n\t"
+                 "ds_read_u8 %15, %19 offset:%21\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(v[0][0]), "=&v"(v[0][1]), "=&v"(v[0][2]), "=&v"(v[0][3]), "=&v"(v[1][0]), "=&v"(v[1][1]),
+                   "=&v"(v[1][2]), "=&v"(v[1][3]), "=&v"(v[2][0]), "=&v"(v[2][1]), "=&v"(v[2][2]), "=&v"(v[2][3]),
+                   "=&v"(v[3][0]), "=&v"(v[3][1]), "=&v"(v[3][2]), "=&v"(v[3][3])
+                 : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "i"(PITCH), "i"(PITCH + 1)
                  : "memory");
 }
 
@@ -2044,7 +2051,7 @@ __global__ __launch_bounds__(256) void k_roi_tables(RoiArgs a) {
         __syncthreads();   // previous slot's descriptors are done with the LDS tables
         for (int x = threadIdx.x; x < a.tabw; x += 256) {
             const int ad = rint_i(M[0] * x * kAbScale), bd = rint_i(M[3] * x * kAbScale);
-            t[x] = ad; t[a.tabw + x] = bd;
+            t[x] = ad * (1 << kTabShift); t[a.tabw + x] = bd * (1 << kTabShift);
             lad[x] = ad; lbd[x] = bd;
         }
         for (int y = threadIdx.x; y < a.tabh; y += 256) {
@@ -2053,7 +2060,7 @@ __global__ __launch_bounds__(256) void k_roi_tables(RoiArgs a) {
             const int x0 = rint_i((M[1] * yc + M[2]) * kAbScale) + kRoundDelta;
             const int y0 = rint_i((M[4] * yc + M[5]) * kAbScale) + kRoundDelta;
             const int q = roi_tab_row_pos(y);
-            t[2 * a.tabw + q] = x0; t[2 * a.tabw + a.tabh + q] = y0;
+            t[2 * a.tabw + q] = x0 * (1 << kTabShift); t[2 * a.tabw + a.tabh + q] = y0 * (1 << kTabShift);
             lx0[y] = x0; ly0[y] = y0;
         }
         __syncthreads();
@@ -2220,8 +2227,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 uint32_t pk = 0;
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    const int X = (X0r[i] + adv[u]) >> (kAbBits - kInterBits);
-                    const int Y = (Y0r[i] + bdv[u]) >> (kAbBits - kInterBits);
+                    const int X = (X0r[i] + adv[u]) >> kTapShift;
+                    const int Y = (Y0r[i] + bdv[u]) >> kTapShift;
                     const int off = mad24(Y >> kInterBits, ftw, (X >> kInterBits) - obase);
                     pk |= (uint32_t)ft_tap_interior(FT, off, ftw, X, Y) << (8 * u);
                 }
@@ -2233,7 +2240,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             // columns past the ROI's right edge are zero: one byte mask per lane instead of a select per pixel
             const int nvalid = RW - c0;
             const uint32_t colmask = nvalid >= 4 ? 0xffffffffu : (1u << (8 * nvalid)) - 1u;
-            const int xo = ((int)lds_offset_of(FT) - bxa) << kAbBits, yo = -(by0 << kAbBits);
+            const int xo = ((int)lds_offset_of(FT) - bxa) << kTabFrac, yo = -(by0 << kTabFrac);
             // one output row (4 pixels) at a time: all 16 tap reads issued before any arithmetic (measured: 126.8 ->
             // 113.1 us per Src7 layer-0 launch at 8 sources with the folded addressing, scripts/warp_exp.hip; rows
             // past the tile repeat its last row's coordinates and are not stored)
@@ -2245,9 +2252,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int sxv = x0r + adv[u], syv = y0r + bdv[u];
-                    fxv[u] = __builtin_amdgcn_ubfe(sxv, kAbBits - kInterBits, kInterBits);
-                    fyv[u] = __builtin_amdgcn_ubfe(syv, kAbBits - kInterBits, kInterBits);
-                    off[u] = (uint32_t)mad24(syv >> kAbBits, ftw, sxv >> kAbBits);
+                    fxv[u] = __builtin_amdgcn_ubfe(sxv, kTapShift, kInterBits);
+                    fyv[u] = __builtin_amdgcn_ubfe(syv, kTapShift, kInterBits);
+                    off[u] = (uint32_t)mad24(syv >> kTabFrac, ftw, sxv >> kTabFrac);
                 }
                 // the 16 reads together ahead of the arithmetic (measured: the compiler's scheduling otherwise
                 // interleaves them with waits, 241 -> 280 us per launch)
@@ -2287,8 +2294,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             uint32_t pk = 0;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int X = (X0r[i] + adv[u]) >> (kAbBits - kInterBits);
-                const int Y = (Y0r[i] + bdv[u]) >> (kAbBits - kInterBits);
+                const int X = (X0r[i] + adv[u]) >> kTapShift;
+                const int Y = (Y0r[i] + bdv[u]) >> kTapShift;
                 int v;
                 if (in_lds) {
                     const int sx = sat_s16(X >> kInterBits), sy = sat_s16(Y >> kInterBits);
@@ -2320,21 +2327,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
+// The LDS byte address of a tap from two folded 16-fraction-bit coordinates: row (high half of y) * pitch + byte column
+// (high half of x), as two SDWA word-select instructions (instead of two shifts and a multiply-add)
+__device__ __forceinline__ uint32_t tap_lds_addr(uint32_t x, uint32_t y, uint32_t pitch) {
+    uint32_t t, r;
+    asm("v_mul_u32_u24_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
+        : "=v"(t) : "v"(y), "v"(pitch));
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
+        : "=v"(r) : "v"(x), "v"(t));
+    return r;
+}
+// a raw buffer over a footprint box (gfx9 dword 3), so its rows load with the row offset in an SGPR (soffset) and the
+// lane's offset in a VGPR fixed for the kernel: no VALU per staged row
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t box_rsrc(const uint8_t* base) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+}
+
 // ---- K6b over a candidate's three angle ROIs at once (n3 == 3): the three ROIs of one candidate sample nearly the
 // same source region (their angles differ by the layer's angle step, a fraction of a degree), so a task is one tile
 // position of all three: their footprint boxes' union is staged into LDS once (when it fits the wave's buffer) and
 // the three tiles are sampled from it one after the other -- the same taps, addressed from the union's origin, so
-// the same bytes as k_roi_warp.  A union that does not fit falls back to staging each ROI's own box.  PF 1: the
-// next task's descriptors loaded during the current one (wave-uniform, in SGPRs; measured 412 vs 404 us per Src7
-// layer-0 microbenchmark launch at 43 sources without, profiles/r03_r).  TH0 1: the first ROI's table loads issued
-// before the union staging
-template <int FB, int WPE, int PF = 0, int TH0 = 1>
+// the same bytes as k_roi_warp.  A union that does not fit falls back to staging each ROI's own box.
+// Round 4, the VALU budget (the kernel is VALU-issue bound):
+//  * staging at zero VALU per row: a lane's global offset (row lane >> 4, dword column lane & 15) and LDS address are
+//    kernel constants, the box origin advances in SGPRs and every LDS store carries its row as the instruction's
+//    immediate offset; all of a box's rows (<= 15 per lane) are in flight together; the row count per lane is
+//    ceil(fth / 4) for every lane, so a lane group may stage up to 3 rows past the box (the level slab carries slack
+//    rows for that read, and the LDS rows land inside the wave's buffer: fth <= 60 rows of 68 bytes);
+//  * per task, not per ROI: the lane's table offsets, the column mask and the row masks (the three ROIs share them);
+//  * the interior pixel: the tables' 16-fraction-bit scale (kTabShift) puts the integer tap coordinate in the high
+//    half-word, read by SDWA word selects, and the 16 tap reads and their wait are one asm statement.
+template <int WPE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_warp3(RoiArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t ft_all[4 * ROI_FT + 16];
+    constexpr int ftw = 64;   // footprint row pitch: one LDS-DMA instruction fills 4 rows of 16 dwords
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint8_t* FT = ft_all + wv * ROI_FT;
-    const int RW = a.tw + 6, RH = a.th + 6, W = a.W, H = a.H;
+    const uint32_t ft_lds = lds_offset_of(FT);
+    const int RW = a.tw + 6, RH = a.th + 6, W = a.W, H = a.H, P = a.P;
     const int txn = (RW + ROI_T - 1) / ROI_T, tyn = (RH + ROI_T - 1) / ROI_T;
     const int per_roi = txn * tyn;
     const int tasks = roi_count(a) / 3 * per_roi;
@@ -2342,34 +2373,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const XcdSplit xs = xcd_split(tasks);
     const int tstride = xs.nk * 4;
     const uint32_t st_lane = 4u * lg + 32u * lr;
-    constexpr int ftw = kFtPitch;
-    // the next task's three tile descriptors are loaded (wave-uniform) while the current task runs
-    int task = xs.lo + xs.k * 4 + wv;
-    int4 nd[3];
-    auto prefetch = [&](int t) {
-        const int c_ = t / per_roi, r_ = t - c_ * per_roi;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const int4 d = a.tdesc[(size_t)(3 * c_ + j) * a.tdesc_stride + r_];
-            nd[j] = make_int4(__builtin_amdgcn_readfirstlane(d.x), __builtin_amdgcn_readfirstlane(d.y),
-                              __builtin_amdgcn_readfirstlane(d.z), __builtin_amdgcn_readfirstlane(d.w));
-        }
+    // LDS-DMA staging: lane -> row lane >> 4, dword column lane & 15 of each 4-row group (the box's full 64-byte
+    // width: columns past it read the row's slack / the next row and are never sampled)
+    const uint32_t dma_goff = (uint32_t)((lane >> 4) * P + 4 * (lane & 15));
+    const size_t tab_stride = (size_t)2 * (a.tabw + a.tabh);
+    const uint32_t pitch_v = __builtin_amdgcn_readfirstlane(ftw);   // the LDS pitch as an SDWA operand
+    auto stage = [&](int fth, const uint8_t* gsrc) {
+        const int n = (fth + 3) >> 2;   // wave-uniform; the row group's base advances in SGPRs, M0 per instruction
+        for (int k = 0; k < n; ++k)
+            __builtin_amdgcn_global_load_lds((fpm_gbl_vp)(gsrc + (size_t)k * 4 * P + dma_goff), (fpm_lds_vp)(FT + 256 * k),
+                                             4, 0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     };
-    if (PF && task < xs.hi) prefetch(task);
-    for (; task < xs.hi; task += tstride) {
-        if (!PF) prefetch(task);
+    for (int task = xs.lo + xs.k * 4 + wv; task < xs.hi; task += tstride) {
         const int cand = task / per_roi;
         const int rem = task - cand * per_roi;
         const int ty = rem / txn, tx = rem - ty * txn;
         const int cx0 = tx * ROI_T, cx1 = min(cx0 + ROI_T, RW) - 1;
         const int ry0 = ty * ROI_T, ry1 = min(ry0 + ROI_T, RH) - 1;
         const int c0 = cx0 + 4 * lg;
-        int4 cd[3] = {nd[0], nd[1], nd[2]};
-        if (PF && task + tstride < xs.hi) prefetch(task + tstride);
         int bx[3], by[3], wp[3], fh[3], fl[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            const int4 d = cd[j];
+            const int4 d = a.tdesc[(size_t)(3 * cand + j) * a.tdesc_stride + rem];
             bx[j] = __builtin_amdgcn_readfirstlane(d.x);
             by[j] = __builtin_amdgcn_readfirstlane(d.y);
             const int dz = __builtin_amdgcn_readfirstlane(d.z);
@@ -2388,22 +2414,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             }
         const bool any_lds = ux0 != INT_MAX;
         const int uwpr = any_lds ? (ux1 - ux0) >> 2 : 0, ufth = any_lds ? uy1 - uy0 : 0;
-        const bool uni = any_lds && uwpr <= 16 && kFtPitch * ufth <= ROI_FT;
-        // the lane's warp-table entries of one ROI (columns c0 .. c0 + 3, rows ry0 + lr + 8i); the first ROI's are
-        // requested before the staging, whose round trip they then share
-        const int cc = min(c0, cx1 & ~3);
+        const bool uni = any_lds && uwpr <= 16 && ftw * ufth <= ROI_FT;
+        // per task: the lane's table offsets (columns c0 .. c0 + 3, rows ry0 + lr + 8i), column mask, row masks
+        const int cc = min(c0, cx1 & ~3);   // tables are read in bounds even for idle lanes
+        const uint32_t oA = 4u * cc, oB = 4u * (a.tabw + cc), oX = 4u * (2 * a.tabw + ry0 + 4 * lr),
+                       oY = oX + 4u * a.tabh;
+        const int nvalid = RW - c0;
+        const uint32_t colmask = nvalid >= 4 ? 0xffffffffu : (1u << (8 * max(nvalid, 0))) - 1u;
         int4 tA, tB, tX, tY;
         auto load_tabs = [&](int slot_) {
-            const int32_t* tb = a.tab + (size_t)slot_ * 2 * (a.tabw + a.tabh);
-            tA = ld_at<int4>(tb, 4u * cc);
-            tB = ld_at<int4>(tb, 4u * (a.tabw + cc));
-            tX = ld_at<int4>(tb, 4u * (2 * a.tabw + ry0 + 4 * lr));
-            tY = ld_at<int4>(tb, 4u * (2 * a.tabw + a.tabh + ry0 + 4 * lr));
+            const int32_t* tb = a.tab + (size_t)slot_ * tab_stride;
+            tA = ld_at<int4>(tb, oA);
+            tB = ld_at<int4>(tb, oB);
+            tX = ld_at<int4>(tb, oX);
+            tY = ld_at<int4>(tb, oY);
         };
-        if (TH0) load_tabs(3 * cand);
+        load_tabs(3 * cand);   // the first ROI's tables share the staging's round trip
         if (uni) {
             wave_sync();   // previous task's gathers are done with FT
-            stage_footprint32<FB, kFtPitch>(FT, uwpr, ufth, lvl + (size_t)uy0 * a.P + ux0, a.P, lane);
+            stage(ufth, lvl + (size_t)uy0 * P + ux0);
             wave_sync();
         }
 #pragma unroll 1
@@ -2416,32 +2445,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 bxa = ux0; by0 = uy0;
             } else {
                 wave_sync();
-                if ((flags & kTileAny) && in_lds)
-                    stage_footprint32<FB, kFtPitch>(FT, wp[j], fh[j], lvl + (size_t)by0 * a.P + bxa, a.P, lane);
+                if ((flags & kTileAny) && in_lds) stage(fh[j], lvl + (size_t)by0 * P + bxa);
                 wave_sync();
             }
-            if (!TH0 || j > 0) load_tabs(slot);
-            const int adv[4] = {tA.x, tA.y, tA.z, tA.w}, bdv[4] = {tB.x, tB.y, tB.z, tB.w};
-            const int X0r[4] = {tX.x, tX.y, tX.z, tX.w}, Y0r[4] = {tY.x, tY.y, tY.z, tY.w};
+            if (j > 0) load_tabs(slot);
+            const uint32_t adv[4] = {(uint32_t)tA.x, (uint32_t)tA.y, (uint32_t)tA.z, (uint32_t)tA.w};
+            const uint32_t bdv[4] = {(uint32_t)tB.x, (uint32_t)tB.y, (uint32_t)tB.z, (uint32_t)tB.w};
+            const uint32_t X0r[4] = {(uint32_t)tX.x, (uint32_t)tX.y, (uint32_t)tX.z, (uint32_t)tX.w};
+            const uint32_t Y0r[4] = {(uint32_t)tY.x, (uint32_t)tY.y, (uint32_t)tY.z, (uint32_t)tY.w};
             uint8_t* tile = a.roi + (size_t)slot * a.roi_stride + ((size_t)rem << 10);
             if (c0 > cx1) continue;
             if ((flags & kTileInterior) && in_lds) {
-                const int nvalid = RW - c0;
-                const uint32_t colmask = nvalid >= 4 ? 0xffffffffu : (1u << (8 * nvalid)) - 1u;
-                const int xo = ((int)lds_offset_of(FT) - bxa) << kAbBits, yo = -(by0 << kAbBits);
+                // folded coordinates: (X0 + adv + xo) >> 16 is the tap's LDS byte column (footprint base included),
+                // (Y0 + bdv + yo) >> 16 its footprint row; both lie in [0, 2^15), so the high half-words are exact
+                const uint32_t xo = (ft_lds - (uint32_t)bxa) << kTabFrac, yo = 0u - ((uint32_t)by0 << kTabFrac);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const int x0r = X0r[i] + xo, y0r = Y0r[i] + yo;
+                    const uint32_t x0r = X0r[i] + xo, y0r = Y0r[i] + yo;
                     uint32_t off[4];
                     int fxv[4], fyv[4], v[4][4];
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
-                        const int sxv = x0r + adv[u], syv = y0r + bdv[u];
-                        fxv[u] = __builtin_amdgcn_ubfe(sxv, kAbBits - kInterBits, kInterBits);
-                        fyv[u] = __builtin_amdgcn_ubfe(syv, kAbBits - kInterBits, kInterBits);
-                        off[u] = (uint32_t)mad24(syv >> kAbBits, ftw, sxv >> kAbBits);
+                        const uint32_t sxv = x0r + adv[u], syv = y0r + bdv[u];
+                        off[u] = tap_lds_addr(sxv, syv, pitch_v);
+                        fxv[u] = (int)((sxv >> kTapShift) & (kInterTab - 1));
+                        fyv[u] = (int)((syv >> kTapShift) & (kInterTab - 1));
                     }
-                    lds_taps16<kFtPitch>(off, v);
+                    lds_taps16<ftw>(off, v);
                     const uint32_t pk = bilerp_row4(v, fxv, fyv);
                     if (ry0 + lr + 8 * i <= ry1) st_at<uint32_t>(tile, st_lane + 256u * i, pk & colmask);
                 }
@@ -2453,8 +2483,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 uint32_t pk = 0;
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    const int X = (X0r[i] + adv[u]) >> (kAbBits - kInterBits);
-                    const int Y = (Y0r[i] + bdv[u]) >> (kAbBits - kInterBits);
+                    const int X = (int)(X0r[i] + adv[u]) >> kTapShift;
+                    const int Y = (int)(Y0r[i] + bdv[u]) >> kTapShift;
                     int v;
                     if (in_lds) {
                         const int sx = sat_s16(X >> kInterBits), sy = sat_s16(Y >> kInterBits);
@@ -3802,8 +3832,7 @@ void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
         const long want3 = (tiles / 3 + 3) / 4;
         // 7 waves per SIMD with the first ROI's tables requested before the staging (8 would spill them): microbenchmark
         // 405.5 / 406.3 -> 400.6 / 402.0 us (round 3)
-        hipLaunchKernelGGL((k_roi_warp3<kWarpFootBatch, 7, 0, 1>), dim3((int)(want3 < 16384 ? want3 : 16384)),
-                           dim3(256), 0, st, a);
+        hipLaunchKernelGGL((k_roi_warp3<7>), dim3((int)(want3 < 16384 ? want3 : 16384)), dim3(256), 0, st, a);
         return;
     }
     hipLaunchKernelGGL((k_roi_warp<kWarpFootBatch, 0, kWarpWaves>), dim3(grid), dim3(256), 0, st, a);

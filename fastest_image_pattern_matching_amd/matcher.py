@@ -328,6 +328,25 @@ class TemplateMatcher:
             raise ValueError(self.last_error())
         return out
 
+    def overlap_filter(self, corners, scores, max_overlap: float, device: bool = True):
+        """filterWithRotatedRect (TemplateMatcher.cpp:1133-1194) on rectangles given as rows (ltx, lty, rtx, rty, rbx,
+        rby) with their scores, in the given order: (indices of the survivors, stats) -- stats as fpm_op_overlap_filter
+        (path, host-decided pairs, device fallback flags, pair entries)."""
+        c = np.ascontiguousarray(corners, np.float32).reshape(-1, 6)
+        sc = np.ascontiguousarray(scores, np.float64).ravel()
+        n = c.shape[0]
+        assert sc.shape[0] == n
+        keep = np.zeros(max(n, 1), np.int32)
+        st = np.zeros(4, np.int32)
+        nk = C.c_int32()
+        rc = self._lib.fpm_op_overlap_filter(self._ctx, c.ctypes.data_as(C.POINTER(C.c_float)),
+                                             sc.ctypes.data_as(C.POINTER(C.c_double)), n, float(max_overlap),
+                                             1 if device else 0, keep.ctypes.data_as(C.POINTER(C.c_int32)),
+                                             C.byref(nk), st.ctypes.data_as(C.POINTER(C.c_int32)))
+        if rc != L.FPM_OK:
+            raise ValueError(self.last_error())
+        return keep[:nk.value].tolist(), st.tolist()
+
     def template_info(self):
         lv, border = C.c_int32(), C.c_int32()
         rc = self._lib.fpm_template_info(self._ctx, C.byref(lv), C.byref(border))

@@ -179,6 +179,17 @@ int fpm_op_warp_affine(fpm_ctx* ctx, const uint8_t* src, int32_t w, int32_t h, s
  * (:496-510), fold=0 the TM_CCORR path (:514).  out is (w-tw+1) x (h-th+1) f32, dense. */
 int fpm_op_ncc_map(fpm_ctx* ctx, const uint8_t* src, int32_t w, int32_t h, size_t src_stride,
                    int32_t layer, int32_t fold, float* out);
+/* filterWithRotatedRect (TemplateMatcher.cpp:1133-1194, with sortPtWithCenter :1093-1131) on n rectangles given as
+ * corners[6 i .. 6 i + 5] = ptLT, ptRT, ptRB (cv::RotatedRect(p1, p2, p3), as match() builds them, :380-390) with
+ * scores[i], in the caller's order (the reference's: by descending score).  mode 0 runs the host filter, mode 1 the
+ * device pair test (k_overlap_pairs, whatever n) with the host replaying its decisions and falling back to the host
+ * filter where the device lists cannot hold the pairs -- the two paths of a search's tail.  keep receives the indices
+ * of the surviving rectangles in order (*n_keep of them); stats (may be NULL) receives [0] the path taken (0 host,
+ * 1 device, 2 device fell back to the host), [1] pairs whose point order the host decided with acos, [2] the device
+ * fallback flags (1: a rectangle with more partners than the kernel keeps, 2: the pair list overflowed), [3] the
+ * device pair-list entries. */
+int fpm_op_overlap_filter(fpm_ctx* ctx, const float* corners, const double* scores, int32_t n, double max_overlap,
+                          int32_t mode, int32_t* keep, int32_t* n_keep, int32_t* stats);
 /* Learned-template introspection: number of pyramid levels, per-level size and statistics
  * (s_TemplData, DataStructures.h:16-55). */
 int fpm_template_info(const fpm_ctx* ctx, int32_t* levels, int32_t* border_color);

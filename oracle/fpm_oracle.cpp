@@ -1395,6 +1395,22 @@ int orc_ncc_map(void* h, const uint8_t* src, int w, int hh, size_t ss, int layer
     return FPM_OK;
 }
 
+// filterWithRotatedRect (TemplateMatcher.cpp:1133-1194) on n rectangles (corners[6i..6i+5] = ptLT, ptRT, ptRB) with
+// scores, in the given order: the surviving indices in order; returns their count
+int orc_filter_rotated_rect(const float* corners, const double* scores, int n, double max_overlap, int32_t* keep) {
+    std::vector<orc::MatchParam> v((size_t)n);
+    for (int i = 0; i < n; ++i) {
+        const float* c = corners + 6 * (size_t)i;
+        v[i].rectR = orc::rotrect_from3(orc::P2f(c[0], c[1]), orc::P2f(c[2], c[3]), orc::P2f(c[4], c[5]));
+        v[i].score = scores[i];
+        v[i].origin = i;
+        v[i].del = false;
+    }
+    orc::Matcher::filter_with_rotated_rect(v, max_overlap);
+    for (size_t i = 0; i < v.size(); ++i) keep[i] = v[i].origin;
+    return (int)v.size();
+}
+
 // rotated-rectangle overlap primitive (filterWithRotatedRect's building block) for KATs:
 // rects given as (ptLT, ptRT, ptRB); returns the intersection type, *area = contourArea after sortPtWithCenter
 int orc_rotrect_overlap(const float a[6], const float b[6], double* area, int* npts) {

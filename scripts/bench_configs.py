@@ -3,7 +3,14 @@ per config the device-resident ms per search on one GPU (sources staged in HBM, 
 the staged batch; latency view: one context, pass after pass), the pipelined ms per search (two contexts as a
 stream of passes, host tail overlapped: throughput view) next to one oracle search on the host (the CPU
 restatement, one thread), plus the result count of each.  Writes one JSON line per config.
-usage: python scripts/bench_configs.py [reps] [--no-cpu] [--only=K ...] [--with-64]"""
+
+The reference's own shipped inputs with a published time (README.md:65, 68-70; --ref-only runs just these): Test6
+(Src6/Dst6), Test4 (Src3/Dst3), Test5 (Src4/Dst4) and Test1 (Src9/Dst9) with the parameters of the screenshot pins
+(tests/golden/reference_pins.json: the published ones where README states them, Test1 also at its published Score
+0.8), MFC semantics (the README times are the MFC tool's), next to the README figure; for these the single-search
+end-to-end time of TemplateMatcher.match on the host array (upload included: the drop-in's use) is reported too,
+and the result count is asserted equal to the pin's.
+usage: python scripts/bench_configs.py [reps] [--no-cpu] [--only=K ...] [--with-64] [--ref-only]"""
 import json
 import os
 import sys
@@ -22,7 +29,39 @@ ALL64 = "--with-64" in sys.argv
 PIPE = "--no-pipe" not in sys.argv   # --no-pipe: latency view only (one context: clean kernel traces)   # also the whole 64-source configs[3] at 1 deg on one GPU (~1 GB of sources)
 
 
+REF_ONLY = "--ref-only" in sys.argv
+# README.md:65, 68-70 (i7-10700): (test, pin name, README ms with SIMD where stated, README ms without)
+README_TESTS = [("Test6", "test6_src6", 657.0, 1157.0), ("Test4", "test4_src3", 21.0, None),
+                ("Test5", "test5_src4", 27.0, None), ("Test1", "test1_src9", 80.0, 164.0)]
+
+
+def reference_inputs():
+    from fastest_image_pattern_matching_amd.images import imread_gray
+
+    golden = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
+    pins = {p["name"]: p for p in json.load(open(os.path.join(golden, "reference_pins.json")))}
+
+    def img(name):
+        path = os.path.join(golden, "ref", name)
+        return imread_gray(path if os.path.exists(path) else os.path.join(golden, name))
+
+    for test, name, simd_ms, plain_ms in README_TESTS:
+        pin = pins[name]
+        s, t = img(pin["source"]), img(pin["template"])
+        runs = [("pin", pin["params"], pin["count"])]
+        if pin.get("count_at_published") is not None:
+            runs.append(("published", pin["published"], pin["count_at_published"]))
+        for tag, prm, count in runs:
+            label = (f"README {test}: {pin['source']} {s.shape[1]}x{s.shape[0]} / {pin['template']} "
+                     f"{t.shape[1]}x{t.shape[0]}, {tag} parameters {prm}")
+            yield (label, [s], t, dict(prm, semantics=1),
+                   {"readme_ms_simd": simd_ms, "readme_ms_no_simd": plain_ms, "expect_matches": count,
+                    "fitted": pin["fitted"] if tag == "pin" else []})
+
+
 def configs():
+    if REF_ONLY:
+        return
     T = synth.load_templates()
     s10, t10 = synth.src10_scene(T["Dst10"])
     yield ("configs[2] Src10 3648x3648 / Dst10 54x54, Tol 0, TargetNum 100 (s_BlockMax)", [s10], t10,
@@ -73,8 +112,20 @@ def pipelined(m, srcs, t, prm):
             "pipelined_searches_per_s": round(1e3 * len(srcs) / pipe_ms, 1)}
 
 
+def end_to_end_ms(m, src):
+    """TemplateMatcher.match on the host array (upload + device pass + host tail): median of REPS calls."""
+    m.match(src)
+    ts = []
+    for _ in range(REPS):
+        t0 = time.perf_counter()
+        m.match(src)
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)) * 1e3
+
+
 def main():
-    for pos, (name, srcs, t, prm) in enumerate(configs()):
+    items = [(n, s_, t_, p_, None) for n, s_, t_, p_ in configs()] + list(reference_inputs())
+    for pos, (name, srcs, t, prm, ref) in enumerate(items):
         if ONLY and pos not in ONLY:
             continue
         m = TemplateMatcher(0)
@@ -95,6 +146,11 @@ def main():
                "last_pass_device_ms": round(dev_ms, 3), "last_pass_host_ms": round(host_ms, 3),
                "gpu_ms_per_search": round(ms / len(srcs), 3), "gpu_searches_per_s": round(1e3 * len(srcs) / ms, 1),
                "matches": [int(x) for x in cnt]}
+        if ref is not None:
+            out.update(ref)
+            assert out["matches"] == [ref["expect_matches"]], (name, out["matches"])
+            out["gpu_ms_end_to_end"] = round(end_to_end_ms(m, srcs[0]), 3)
+            out["readme_over_gpu_latency"] = round(ref["readme_ms_simd"] / out["gpu_ms_per_search"], 1)
         if PIPE:
             out.update(pipelined(m, srcs, t, prm))
         if CPU:

@@ -35,7 +35,7 @@ int main(int argc, char** argv) {
     const int nsrc = envi("MB_NSRC", 8), ncand = 11, n3 = 3;
     const float sc = W / 4024.f;
     const int reps = argc > 1 ? atoi(argv[1]) : 20;
-    std::vector<uint8_t> img((size_t)P * (H + 1) * nsrc), tm((size_t)TP * (TH + 1));
+    std::vector<uint8_t> img((size_t)P * (H + 1) * nsrc + 4 * (size_t)P + 256), tm((size_t)TP * (TH + 1));
     srand(1);
     for (auto& v : img) v = rand() & 255;
     for (auto& v : tm) v = rand() & 255;
@@ -116,9 +116,9 @@ int main(int argc, char** argv) {
             timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 0, 7>), dim3(grid), dim3(256), 0, 0, a); }, "warp b12 7 waves");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp<8, 0, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp b8 8 waves");
             const int grid3 = (int)std::min<long>((tiles / 3 + 3) / 4, 16384);
-            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<12, 8, 0, 0>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 b12 8w");
-            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<12, 8, 0, 1>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 b12 8w tables early");
-            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<12, 7, 0, 1>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 b12 7w tables early");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<8>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 8w");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 7w");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<6>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 6w");
 
             timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 5, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp no stores");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 6, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp gathers only");

@@ -58,6 +58,8 @@ def load(path: str = ORACLE_LIB):
     lib.orc_set_ccorr_mode.argtypes = [C.c_void_p, C.c_int]
     lib.orc_cross_corr_f32.argtypes = [_U8P, C.c_int, C.c_int, C.c_size_t, _U8P, C.c_int, C.c_int, C.c_size_t,
                                        C.POINTER(C.c_float)]
+    lib.orc_filter_rotated_rect.argtypes = [C.POINTER(C.c_float), C.POINTER(C.c_double), C.c_int, C.c_double,
+                                            C.POINTER(C.c_int32)]
     lib.fpm_params_default.argtypes = [C.POINTER(Params)]
     _libs[path] = lib
     return lib
@@ -102,6 +104,17 @@ def cross_corr_f32(img: np.ndarray, templ: np.ndarray) -> np.ndarray:
                                    out.ctypes.data_as(C.POINTER(C.c_float)))
     assert rc == 0
     return out
+
+
+def filter_rotated_rect(corners, scores, max_overlap):
+    """filterWithRotatedRect on rectangles given as (ltx, lty, rtx, rty, rbx, rby) rows with scores, in the given order:
+    the indices of the survivors in order."""
+    c = np.ascontiguousarray(corners, np.float32).reshape(-1, 6)
+    sc = np.ascontiguousarray(scores, np.float64).ravel()
+    keep = np.zeros(max(len(sc), 1), np.int32)
+    n = load().orc_filter_rotated_rect(c.ctypes.data_as(C.POINTER(C.c_float)), sc.ctypes.data_as(C.POINTER(C.c_double)),
+                                       len(sc), float(max_overlap), keep.ctypes.data_as(C.POINTER(C.c_int32)))
+    return keep[:n].tolist()
 
 
 def rotrect_overlap(a, b):
