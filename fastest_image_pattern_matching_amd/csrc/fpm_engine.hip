@@ -610,9 +610,9 @@ int layout_sources(fpm_ctx* ctx, int count, int w, int h) {
         lw = (lw + 1) / 2;
         lh = (lh + 1) / 2;
     }
-    // slack: the ROI sampler's footprint staging reads up to 3 rows past a box (k_roi_warp3), i.e. past the last
-    // image's spare row
-    HIP_TRY(ctx->d_src.ensure(off + 4 * (size_t)ctx->src[0].pitch + 256));
+    // slack: the ROI sampler's footprint staging reads whole 16-row groups, up to 15 rows past a box (k_roi_warp3),
+    // i.e. past the last image's spare row
+    HIP_TRY(ctx->d_src.ensure(off + 16 * (size_t)ctx->src[0].pitch + 256));
     return FPM_OK;
 }
 

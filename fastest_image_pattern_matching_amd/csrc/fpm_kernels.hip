@@ -1732,6 +1732,9 @@ constexpr int kFtPitch = 68;
 constexpr int kTabShift = 6;
 constexpr int kTabFrac = kAbBits + kTabShift;           // 16
 constexpr int kTapShift = kTabFrac - kInterBits;        // 11
+// The ROI scratch holds every sampled byte XOR 0x80 (u8 -> the i8 the matrix cores take, x ^ 0x80 = x - 128): the
+// samplers write it flipped (one bit-op per 4 pixels), so k_roi_corr stages rows into LDS as they are
+constexpr uint32_t kRoiFlip = 0x80808080u;
 
 int roi_pick_rc(int /*tw*/, int th) { return th < ROI_RC ? th : ROI_RC; }
 
@@ -2232,7 +2235,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                     const int off = mad24(Y >> kInterBits, ftw, (X >> kInterBits) - obase);
                     pk |= (uint32_t)ft_tap_interior(FT, off, ftw, X, Y) << (8 * u);
                 }
-                st_at<uint32_t>(tile, st_lane + 256u * i, pk & colmask);
+                st_at<uint32_t>(tile, st_lane + 256u * i, (pk & colmask) ^ kRoiFlip);
             }
             continue;
         }
@@ -2283,7 +2286,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 if (ABL >= 5) {
                     if ((pk & colmask) == 0x9e3779b9u && (lane ^ bxa) == 977) st_at<uint32_t>(tile, st_lane, pk);
                 } else if (ry0 + lr + 8 * i <= ry1) {
-                    st_at<uint32_t>(tile, st_lane + 256u * i, pk & colmask);
+                    st_at<uint32_t>(tile, st_lane + 256u * i, (pk & colmask) ^ kRoiFlip);
                 }
             }
             continue;
@@ -2322,7 +2325,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 if (c0 + u >= RW) v = 0;
                 pk |= (uint32_t)v << (8 * u);
             }
-            st_at<uint32_t>(tile, st_lane + 256u * i, pk);
+            st_at<uint32_t>(tile, st_lane + 256u * i, pk ^ kRoiFlip);
         }
     }
 }
@@ -2349,11 +2352,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t box_rsrc(const uint8_t* base) 
 // the three tiles are sampled from it one after the other -- the same taps, addressed from the union's origin, so
 // the same bytes as k_roi_warp.  A union that does not fit falls back to staging each ROI's own box.
 // Round 4, the VALU budget (the kernel is VALU-issue bound):
-//  * staging at zero VALU per row: a lane's global offset (row lane >> 4, dword column lane & 15) and LDS address are
-//    kernel constants, the box origin advances in SGPRs and every LDS store carries its row as the instruction's
-//    immediate offset; all of a box's rows (<= 15 per lane) are in flight together; the row count per lane is
-//    ceil(fth / 4) for every lane, so a lane group may stage up to 3 rows past the box (the level slab carries slack
-//    rows for that read, and the LDS rows land inside the wave's buffer: fth <= 60 rows of 68 bytes);
+//  * staging in 16-byte pieces: a lane's global offset (row lane >> 2, chunk lane & 3) and LDS address are kernel
+//    constants, every LDS store carries its row group as the instruction's immediate offset, and all of a box's rows
+//    (<= 4 loads per lane) are in flight together; whole 16-row groups are staged, so up to 15 rows past the box are
+//    read (the level slab carries slack rows for that) and land inside the wave's 64 x 64-byte buffer;
 //  * per task, not per ROI: the lane's table offsets, the column mask and the row masks (the three ROIs share them);
 //  * the interior pixel: the tables' 16-fraction-bit scale (kTabShift) puts the integer tap coordinate in the high
 //    half-word, read by SDWA word selects, and the 16 tap reads and their wait are one asm statement.
@@ -2373,17 +2375,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const XcdSplit xs = xcd_split(tasks);
     const int tstride = xs.nk * 4;
     const uint32_t st_lane = 4u * lg + 32u * lr;
-    // LDS-DMA staging: lane -> row lane >> 4, dword column lane & 15 of each 4-row group (the box's full 64-byte
-    // width: columns past it read the row's slack / the next row and are never sampled)
-    const uint32_t dma_goff = (uint32_t)((lane >> 4) * P + 4 * (lane & 15));
+    // footprint staging: lane -> 16-byte chunk lane & 3 of rows lane >> 2 (+ 16 k): a box's full 64-byte width (columns
+    // past it read the row's slack / the next row and are never sampled), <= 4 dwordx4 loads per lane all in flight,
+    // then 16-byte LDS stores at the row's immediate offset
+    const uint32_t stage_goff = (uint32_t)((lane >> 2) * P + 16 * (lane & 3));
+    const uint32_t stage_lds = ft_lds + (uint32_t)((lane >> 2) * ftw + 16 * (lane & 3));
     const size_t tab_stride = (size_t)2 * (a.tabw + a.tabh);
     const uint32_t pitch_v = __builtin_amdgcn_readfirstlane(ftw);   // the LDS pitch as an SDWA operand
     auto stage = [&](int fth, const uint8_t* gsrc) {
-        const int n = (fth + 3) >> 2;   // wave-uniform; the row group's base advances in SGPRs, M0 per instruction
-        for (int k = 0; k < n; ++k)
-            __builtin_amdgcn_global_load_lds((fpm_gbl_vp)(gsrc + (size_t)k * 4 * P + dma_goff), (fpm_lds_vp)(FT + 256 * k),
-                                             4, 0, 0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int n = (fth + 15) >> 4;   // wave-uniform, <= 4
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (k < n) v[k] = ld_at<u32x4>(gsrc + (size_t)k * 16 * P, stage_goff);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (k < n) *(__attribute__((address_space(3))) u32x4*)(size_t)(stage_lds + 16 * ftw * k) = v[k];
     };
     for (int task = xs.lo + xs.k * 4 + wv; task < xs.hi; task += tstride) {
         const int cand = task / per_roi;
@@ -2473,7 +2481,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                     }
                     lds_taps16<ftw>(off, v);
                     const uint32_t pk = bilerp_row4(v, fxv, fyv);
-                    if (ry0 + lr + 8 * i <= ry1) st_at<uint32_t>(tile, st_lane + 256u * i, pk & colmask);
+                    if (ry0 + lr + 8 * i <= ry1) st_at<uint32_t>(tile, st_lane + 256u * i, (pk & colmask) ^ kRoiFlip);
                 }
                 continue;
             }
@@ -2511,7 +2519,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                     if (c0 + u >= RW) v = 0;
                     pk |= (uint32_t)v << (8 * u);
                 }
-                st_at<uint32_t>(tile, st_lane + 256u * i, pk);
+                st_at<uint32_t>(tile, st_lane + 256u * i, pk ^ kRoiFlip);
             }
         }
     }
@@ -2649,8 +2657,11 @@ __device__ __forceinline__ void band_mfma_regs(const fpm_v4i* A, const uint8_t* 
 // totals by LDS atomics, a separate edge phase, one thread per partial), 2 = as 1 with the partials before the GEMM
 // SE: the band's row results are written into LDS by the epilogue and copied to HBM as 16-byte runs during the next
 // item's staging (after the loads of its rows are issued, so waiting for those loads does not wait for these stores)
-template <int MODE, bool GA, int WPE, int NK = 0, bool PFR = true, int RS = 1, bool SE = false>
+// DMA (register-A form, no row prefetch): the item's ROI rows go global -> LDS by LDS-DMA (one global_load_lds_dwordx4
+// per row and wave, the scratch already flipped): no staging registers and no VALU per staged row
+template <int MODE, bool GA, int WPE, int NK = 0, bool PFR = true, int RS = 1, bool SE = false, bool DMA = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_corr(RoiArgs a) {
+    static_assert(!DMA || (NK > 0 && !PFR), "LDS-DMA staging replaces the register staging of the register-A form");
     static_assert(NK == 0 || (GA && MODE != 3), "the register-A form stages no template rows");
     static_assert(!SE || NK > 0, "the staged epilogue is flushed in the register-A form's staging phase");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -2731,16 +2742,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             // this item's rows (loaded during the previous item) ^ 0x80 into LDS; this wave's A fragments when the
             // band changes (workgroup-uniform); then the next item's row loads
             const bool in_roi = lane < 2 * txn;
+            if (DMA) {
+                // rows wv + 4i of the item: SGPR row address, the lane's 16-byte chunk of it (lanes past the ROI width
+                // idle: the LDS chunks past the ROI are multiplied by the template's zero padding and never summed)
+                const uint8_t* rsrc = a.roi + (size_t)slot * a.roi_stride;
+                const uint32_t lane_off = ((uint32_t)(lane >> 1) << 10) + 16u * (uint32_t)(lane & 1);
+                const int wvu = __builtin_amdgcn_readfirstlane(wv);
+#pragma unroll
+                for (int i = 0; i < kStageRows; ++i) {
+                    const int r = wvu + 4 * i;
+                    if (r < nsrc && in_roi) {
+                        const int R = T0 + r;
+                        const uint8_t* g = rsrc + ((size_t)((R >> 5) * txn) << 10) + (R & 31) * ROI_T + lane_off;
+                        const uint32_t ldsa = __builtin_amdgcn_readfirstlane(lds_offset_of(SB + (size_t)r * SBp));
+                        uint32_t keep;
+                        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                                     "s_mov_b32 m0, %0"
+                                     : "=&s"(keep) : "v"(g), "s"(ldsa) : "memory");
+                    }
+                }
+                flush();
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            } else {
             if (!PFR) load_rows(item);
             flush();
 #pragma unroll
             for (int i = 0; i < kStageRows; ++i) {
                 const int r = wv + 4 * i;
-                if (r < nsrc && lane < q4) {
-                    uint4 x = in_roi ? pv[i] : make_uint4(0, 0, 0, 0);
-                    x.x ^= 0x80808080u; x.y ^= 0x80808080u; x.z ^= 0x80808080u; x.w ^= 0x80808080u;
-                    *(uint4*)(SB + (size_t)r * SBp + 16 * lane) = x;
-                }
+                // the scratch is stored flipped (kRoiFlip); columns past the ROI: flipped zeros
+                if (r < nsrc && lane < q4)
+                    *(uint4*)(SB + (size_t)r * SBp + 16 * lane) = in_roi ? pv[i] : make_uint4(kRoiFlip, kRoiFlip, kRoiFlip, kRoiFlip);
+            }
             }
             if (band != a_band) {
                 a_band = band;
@@ -2767,16 +2799,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                         const int R = T0 + r;
                         v[i] = (r < nsrc && c < 2 * txn)
                                    ? *(const uint4*)(rsrc + ((size_t)((R >> 5) * txn + (c >> 1)) << 10) + (R & 31) * ROI_T + 16 * (c & 1))
-                                   : make_uint4(0, 0, 0, 0);
+                                   : make_uint4(kRoiFlip, kRoiFlip, kRoiFlip, kRoiFlip);
                     }
 #pragma unroll
                     for (int i = 0; i < kStageBatch; ++i) {
                         const int r = wv + 4 * (i0 + i);
-                        if (r < nsrc && c < q4) {
-                            uint4 x = v[i];
-                            x.x ^= 0x80808080u; x.y ^= 0x80808080u; x.z ^= 0x80808080u; x.w ^= 0x80808080u;
-                            *(uint4*)(SB + (size_t)r * SBp + 16 * c) = x;
-                        }
+                        if (r < nsrc && c < q4) *(uint4*)(SB + (size_t)r * SBp + 16 * c) = v[i];
                     }
                 }
             }

@@ -23,7 +23,7 @@ int main(int argc, char** argv) {
     const int nsrc = envi("MB_NSRC", 8), ncand = 11, n3 = 3;
     const float sc = W / 4024.f;
     const int reps = argc > 1 ? atoi(argv[1]) : 20;
-    std::vector<uint8_t> img((size_t)P * (H + 1) * nsrc + 4 * (size_t)P + 256), tm((size_t)TP * (TH + 1));
+    std::vector<uint8_t> img((size_t)P * (H + 1) * nsrc + 16 * (size_t)P + 256), tm((size_t)TP * (TH + 1));
     srand(1);
     for (auto& v : img) v = rand() & 255;
     for (auto& v : tm) v = rand() & 255;

@@ -26,6 +26,168 @@ __global__ __launch_bounds__(256) void k_stream_copy(const uint4* __restrict__ s
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) dst[i] = src[i];
 }
 
+// ---- the round-3 k_roi_warp3 (per-row staging loop into VGPRs, 68-byte footprint pitch, shift + mad24 tap
+// addressing), kept here as the A/B reference of the product kernel; reads the product's scaled tables
+template <int FB, int WPE, int PF = 0, int TH0 = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_warp3_r03(RoiArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t ft_all[4 * ROI_FT + 16];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t* FT = ft_all + wv * ROI_FT;
+    const int RW = a.tw + 6, RH = a.th + 6, W = a.W, H = a.H;
+    const int txn = (RW + ROI_T - 1) / ROI_T, tyn = (RH + ROI_T - 1) / ROI_T;
+    const int per_roi = txn * tyn;
+    const int tasks = roi_count(a) / 3 * per_roi;
+    const int lr = lane >> 3, lg = lane & 7;
+    const XcdSplit xs = xcd_split(tasks);
+    const int tstride = xs.nk * 4;
+    const uint32_t st_lane = 4u * lg + 32u * lr;
+    constexpr int ftw = kFtPitch;
+    // the next task's three tile descriptors are loaded (wave-uniform) while the current task runs
+    int task = xs.lo + xs.k * 4 + wv;
+    int4 nd[3];
+    auto prefetch = [&](int t) {
+        const int c_ = t / per_roi, r_ = t - c_ * per_roi;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int4 d = a.tdesc[(size_t)(3 * c_ + j) * a.tdesc_stride + r_];
+            nd[j] = make_int4(__builtin_amdgcn_readfirstlane(d.x), __builtin_amdgcn_readfirstlane(d.y),
+                              __builtin_amdgcn_readfirstlane(d.z), __builtin_amdgcn_readfirstlane(d.w));
+        }
+    };
+    if (PF && task < xs.hi) prefetch(task);
+    for (; task < xs.hi; task += tstride) {
+        if (!PF) prefetch(task);
+        const int cand = task / per_roi;
+        const int rem = task - cand * per_roi;
+        const int ty = rem / txn, tx = rem - ty * txn;
+        const int cx0 = tx * ROI_T, cx1 = min(cx0 + ROI_T, RW) - 1;
+        const int ry0 = ty * ROI_T, ry1 = min(ry0 + ROI_T, RH) - 1;
+        const int c0 = cx0 + 4 * lg;
+        int4 cd[3] = {nd[0], nd[1], nd[2]};
+        if (PF && task + tstride < xs.hi) prefetch(task + tstride);
+        int bx[3], by[3], wp[3], fh[3], fl[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int4 d = cd[j];
+            bx[j] = __builtin_amdgcn_readfirstlane(d.x);
+            by[j] = __builtin_amdgcn_readfirstlane(d.y);
+            const int dz = __builtin_amdgcn_readfirstlane(d.z);
+            wp[j] = dz & 0xffff;
+            fh[j] = dz >> 16;
+            fl[j] = __builtin_amdgcn_readfirstlane(d.w);
+        }
+        const uint8_t* lvl = a.level + (size_t)(fl[0] >> kTileSrcShift) * a.level_stride;   // one candidate, one source
+        // union of the boxes that stage into LDS
+        int ux0 = INT_MAX, uy0 = INT_MAX, ux1 = INT_MIN, uy1 = INT_MIN;
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            if ((fl[j] & kTileAny) && (fl[j] & kTileLds)) {
+                ux0 = min(ux0, bx[j]); uy0 = min(uy0, by[j]);
+                ux1 = max(ux1, bx[j] + 4 * wp[j]); uy1 = max(uy1, by[j] + fh[j]);
+            }
+        const bool any_lds = ux0 != INT_MAX;
+        const int uwpr = any_lds ? (ux1 - ux0) >> 2 : 0, ufth = any_lds ? uy1 - uy0 : 0;
+        const bool uni = any_lds && uwpr <= 16 && kFtPitch * ufth <= ROI_FT;
+        // the lane's warp-table entries of one ROI (columns c0 .. c0 + 3, rows ry0 + lr + 8i); the first ROI's are
+        // requested before the staging, whose round trip they then share
+        const int cc = min(c0, cx1 & ~3);
+        int4 tA, tB, tX, tY;
+        auto load_tabs = [&](int slot_) {
+            const int32_t* tb = a.tab + (size_t)slot_ * 2 * (a.tabw + a.tabh);
+            tA = ld_at<int4>(tb, 4u * cc);
+            tB = ld_at<int4>(tb, 4u * (a.tabw + cc));
+            tX = ld_at<int4>(tb, 4u * (2 * a.tabw + ry0 + 4 * lr));
+            tY = ld_at<int4>(tb, 4u * (2 * a.tabw + a.tabh + ry0 + 4 * lr));
+        };
+        if (TH0) load_tabs(3 * cand);
+        if (uni) {
+            wave_sync();   // previous task's gathers are done with FT
+            stage_footprint32<FB, kFtPitch>(FT, uwpr, ufth, lvl + (size_t)uy0 * a.P + ux0, a.P, lane);
+            wave_sync();
+        }
+#pragma unroll 1
+        for (int j = 0; j < 3; ++j) {
+            const int slot = 3 * cand + j;
+            const int flags = fl[j];
+            const bool in_lds = (flags & kTileLds) != 0;
+            int bxa = bx[j], by0 = by[j];
+            if (uni) {
+                bxa = ux0; by0 = uy0;
+            } else {
+                wave_sync();
+                if ((flags & kTileAny) && in_lds)
+                    stage_footprint32<FB, kFtPitch>(FT, wp[j], fh[j], lvl + (size_t)by0 * a.P + bxa, a.P, lane);
+                wave_sync();
+            }
+            if (!TH0 || j > 0) load_tabs(slot);
+            const int adv[4] = {tA.x, tA.y, tA.z, tA.w}, bdv[4] = {tB.x, tB.y, tB.z, tB.w};
+            const int X0r[4] = {tX.x, tX.y, tX.z, tX.w}, Y0r[4] = {tY.x, tY.y, tY.z, tY.w};
+            uint8_t* tile = a.roi + (size_t)slot * a.roi_stride + ((size_t)rem << 10);
+            if (c0 > cx1) continue;
+            if ((flags & kTileInterior) && in_lds) {
+                const int nvalid = RW - c0;
+                const uint32_t colmask = nvalid >= 4 ? 0xffffffffu : (1u << (8 * nvalid)) - 1u;
+                const int xo = ((int)lds_offset_of(FT) - bxa) << kTabFrac, yo = -(by0 << kTabFrac);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int x0r = X0r[i] + xo, y0r = Y0r[i] + yo;
+                    uint32_t off[4];
+                    int fxv[4], fyv[4], v[4][4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int sxv = x0r + adv[u], syv = y0r + bdv[u];
+                        fxv[u] = __builtin_amdgcn_ubfe(sxv, kTapShift, kInterBits);
+                        fyv[u] = __builtin_amdgcn_ubfe(syv, kTapShift, kInterBits);
+                        off[u] = (uint32_t)mad24(syv >> kTabFrac, ftw, sxv >> kTabFrac);
+                    }
+                    lds_taps16<kFtPitch>(off, v);
+                    const uint32_t pk = bilerp_row4(v, fxv, fyv);
+                    if (ry0 + lr + 8 * i <= ry1) st_at<uint32_t>(tile, st_lane + 256u * i, pk & colmask);
+                }
+                continue;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (ry0 + lr + 8 * i > ry1) break;
+                uint32_t pk = 0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int X = (X0r[i] + adv[u]) >> kTapShift;
+                    const int Y = (Y0r[i] + bdv[u]) >> kTapShift;
+                    int v;
+                    if (in_lds) {
+                        const int sx = sat_s16(X >> kInterBits), sy = sat_s16(Y >> kInterBits);
+                        const int fx = X & (kInterTab - 1), fy = Y & (kInterTab - 1);
+                        const uint8_t* p = FT + (sy - by0) * ftw + (sx - bxa);
+                        int v0, v1, v2, v3;
+                        if ((unsigned)sx < (unsigned)(W - 1) && (unsigned)sy < (unsigned)(H - 1)) {
+                            v0 = p[0]; v1 = p[1]; v2 = p[ftw]; v3 = p[ftw + 1];
+                        } else if (sx >= W || sx + 1 < 0 || sy >= H || sy + 1 < 0) {
+                            v0 = v1 = v2 = v3 = 0;
+                        } else {
+                            const bool x0 = sx >= 0 && sx < W, x1 = sx + 1 >= 0 && sx + 1 < W;
+                            const bool y0 = sy >= 0 && sy < H, y1 = sy + 1 >= 0 && sy + 1 < H;
+                            v0 = x0 && y0 ? p[0] : 0;
+                            v1 = x1 && y0 ? p[1] : 0;
+                            v2 = x0 && y1 ? p[ftw] : 0;
+                            v3 = x1 && y1 ? p[ftw + 1] : 0;
+                        }
+                        const int h0 = 32 * v0 + fx * (v1 - v0), h1 = 32 * v2 + fx * (v3 - v2);
+                        v = (32 * h0 + fy * (h1 - h0) + 512) >> 10;
+                    } else {
+                        v = roi_tap(lvl, W, H, a.P, X, Y);
+                    }
+                    if (c0 + u >= RW) v = 0;
+                    pk |= (uint32_t)v << (8 * u);
+                }
+                st_at<uint32_t>(tile, st_lane + 256u * i, pk);
+            }
+        }
+    }
+}
+
+
 int main(int argc, char** argv) {
     // problem shape (defaults: Src7 layer 0); MB_W / MB_H / MB_P / MB_TW / MB_TH / MB_NSRC override (layer-1 shape:
     // MB_W=2012 MB_H=1518 MB_P=2048 MB_TW=381 MB_TH=261); MB_WARP_ONLY=1 stops after the warp section
@@ -35,7 +197,7 @@ int main(int argc, char** argv) {
     const int nsrc = envi("MB_NSRC", 8), ncand = 11, n3 = 3;
     const float sc = W / 4024.f;
     const int reps = argc > 1 ? atoi(argv[1]) : 20;
-    std::vector<uint8_t> img((size_t)P * (H + 1) * nsrc + 4 * (size_t)P + 256), tm((size_t)TP * (TH + 1));
+    std::vector<uint8_t> img((size_t)P * (H + 1) * nsrc + 16 * (size_t)P + 256), tm((size_t)TP * (TH + 1));
     srand(1);
     for (auto& v : img) v = rand() & 255;
     for (auto& v : tm) v = rand() & 255;
@@ -116,6 +278,7 @@ int main(int argc, char** argv) {
             timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 0, 7>), dim3(grid), dim3(256), 0, 0, a); }, "warp b12 7 waves");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp<8, 0, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp b8 8 waves");
             const int grid3 = (int)std::min<long>((tiles / 3 + 3) / 4, 16384);
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3_r03<12, 7, 0, 1>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 r03 7w");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<8>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 8w");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 7w");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<6>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 6w");
@@ -133,6 +296,7 @@ int main(int argc, char** argv) {
         printf("tiles %ld\n", tiles);
     }
     if (envi("MB_WARP_ONLY", 0)) return 0;
+    launch_roi_warp(a, 0);   // the product's ROIs (the warp variants above may have left other bytes)
     timeit([&] { launch_roi_corr(a, 0); }, "prod corr");
     if (TW > 512 && TW <= 768) {   // register-A form (12 k-steps, the Src7 layer-0 product) and its phase ablations
         const size_t lds = roi_corr_lds(a.roi_pitch, a.tw, a.rc, true);
@@ -141,6 +305,9 @@ int main(int argc, char** argv) {
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA full");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 12, false, 0>), dim3(grid), dim3(256), lds, 0, a); }, "corrA RS0 full");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 12, false, 1, true>), dim3(grid), dim3(256), lds, 0, a); }, "corrA SE full");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 12, false, 1, true, true>), dim3(grid), dim3(256), lds, 0, a); }, "corrA SE DMA 3w");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 4, 12, false, 1, true, true>), dim3((int)std::min<long>(items, 1024)), dim3(256), lds, 0, a); }, "corrA SE DMA 4w");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 4, 12, false, 1, false, true>), dim3((int)std::min<long>(items, 1024)), dim3(256), lds, 0, a); }, "corrA DMA 4w");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<2, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA no mfma+epi");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<4, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA no edges");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<5, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA no stores");
@@ -154,6 +321,7 @@ int main(int argc, char** argv) {
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 8, false>), dim3((int)std::min<long>(items, 768)), dim3(256), lds, 0, a); }, "corrA8 3 waves");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 8, false, 1, true>), dim3((int)std::min<long>(items, 768)), dim3(256), lds, 0, a); }, "corrA8 SE 3 waves");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 4, 8, false, 1, true>), dim3((int)std::min<long>(items, 1024)), dim3(256), lds, 0, a); }, "corrA8 SE 4 waves");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 4, 8, false, 1, true, true>), dim3((int)std::min<long>(items, 1024)), dim3(256), lds, 0, a); }, "corrA8 SE DMA 4w");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 8, false, 0>), dim3((int)std::min<long>(items, 768)), dim3(256), lds, 0, a); }, "corrA8 RS0 3 waves");
     }
     timeit([&] { launch_roi_eval(a, 0); }, "prod eval");
@@ -170,6 +338,15 @@ int main(int argc, char** argv) {
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<3, true, 3>), dim3(grid), dim3(256), lds1, 0, a); }, "corr globA w3 no stage");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<2, true, 3>), dim3(grid), dim3(256), lds1, 0, a); }, "corr globA w3 no mfma");
         launch_roi_corr(a, 0);
+        if (envi("MB_DMA_CHECK", 0)) {   // the host check below then checks the LDS-DMA staged form
+            hipMemset(a.rowsum, 0xff, (size_t)C * n3 * ((TH * 49 + 3) & ~3) * 4);
+            const long items = (long)a.slot_cap * ((TH + 31) / 32);
+            if (TW > 512 && TW <= 768)
+                hipLaunchKernelGGL((k_roi_corr<0, true, 4, 12, false, 1, true, true>), dim3((int)std::min<long>(items, 1024)), dim3(256), lds1, 0, a);
+            else if (TW > 256 && TW <= 512)
+                hipLaunchKernelGGL((k_roi_corr<0, true, 4, 8, false, 1, true, true>), dim3((int)std::min<long>(items, 1024)), dim3(256), lds1, 0, a);
+            printf("host check of the DMA form\n");
+        }
         if (envi("MB_SE_CHECK", 0)) {   // the host check below then checks the LDS-staged epilogue form
             hipMemset(a.rowsum, 0xff, (size_t)C * n3 * ((TH * 49 + 3) & ~3) * 4);
             const long items = (long)a.slot_cap * ((TH + 31) / 32);
@@ -186,7 +363,7 @@ int main(int argc, char** argv) {
         for (int slot : {0, 1, 131, C * n3 - 1}) {
             std::vector<uint8_t> roi_t(a.roi_stride);
             const int txn = (TW + 6 + 31) / 32;
-            auto roi_at = [&](int r, int c) { return roi_t[((size_t)((r >> 5) * txn + (c >> 5)) << 10) + (r & 31) * 32 + (c & 31)]; };
+            auto roi_at = [&](int r, int c) { return (uint8_t)(roi_t[((size_t)((r >> 5) * txn + (c >> 5)) << 10) + (r & 31) * 32 + (c & 31)] ^ 0x80); };   // stored flipped
             std::vector<uint32_t> rs((size_t)TH * 49), ws((size_t)a.nchunk * 49);
             std::vector<uint64_t> wq((size_t)a.nchunk * 49);
             CK(hipMemcpy(roi_t.data(), a.roi + (size_t)slot * a.roi_stride, a.roi_stride, hipMemcpyDeviceToHost));

@@ -73,12 +73,13 @@ def test_overlap_too_many_partners(m):
 
 
 def test_overlap_list_overflow(m):
-    """150 mutually overlapping rectangles: 11175 partner entries > 48 n = 7200 -> flag 2, host filter."""
+    """150 mutually overlapping rectangles at MaxOverlap 0 (every overlapping pair deletes one of the two, so every
+    pair is listed): 11175 entries > 48 n = 7200 -> flag 2, host filter."""
     rng = np.random.default_rng(6)
     n = 150
     c = rects(300 + rng.uniform(-4, 4, n), 300 + rng.uniform(-4, 4, n), 80.0, 60.0, rng.uniform(-10, 10, n))
     s = np.sort(rng.uniform(0.5, 1.0, n))[::-1]
-    st = check(m, c, s, 0.9)
+    st = check(m, c, s, 0.0)
     assert st[0] == 2 and st[2] == 2
 
 
