@@ -106,7 +106,7 @@ struct Plan {
     // device buffers owned by the plan
     DevBuf d_ncand;                            // s_BlockMax candidate lists (k_nms_blocks -> k_nms_fast)
     DevBuf d_canvas, d_map, d_bmax, d_bloc, d_jobs, d_nodes, d_top, d_topn, d_peaks, d_counts, d_state,
-        d_live, d_livecnt, d_rec, d_rowsum, d_wsum, d_wsq, d_tab, d_roi, d_tdesc;
+        d_live, d_livecnt, d_rec, d_rowsum, d_wsum, d_wsq, d_tab, d_roi, d_tdesc, d_state2, d_rec2;
     int tabw = 0, tabh = 0, roi_pitch = 0, tdesc_stride = 1;
     size_t roi_stride = 0;
     int slot_cap = 0;                          // ROIs per refinement round (bounded scratch)
@@ -116,7 +116,7 @@ struct Plan {
     char* h_dev = nullptr;   // device-side address of h_out (k_pack writes it over PCIe)
     void release() {
         for (DevBuf* b : {&d_ncand, &d_canvas, &d_map, &d_bmax, &d_bloc, &d_jobs, &d_nodes, &d_top, &d_topn, &d_peaks,
-                          &d_counts, &d_state, &d_live, &d_livecnt, &d_rec, &d_rowsum, &d_wsum, &d_wsq, &d_tab, &d_roi, &d_tdesc})
+                          &d_counts, &d_state, &d_live, &d_livecnt, &d_rec, &d_rowsum, &d_wsum, &d_wsq, &d_tab, &d_roi, &d_tdesc, &d_state2, &d_rec2})
             b->release();
         h_out.release();
         valid = false;
@@ -464,6 +464,9 @@ int build_plan(fpm_ctx* ctx) {
     P.nzero = L + 2 + (P.by_block ? P.off_skey - (L + 2) + 9 * J : 0);
     HIP_TRY(P.d_livecnt.ensure(sizeof(int32_t) * (size_t)P.nzero));
     HIP_TRY(P.d_rec.ensure(sizeof(RoiRecord) * (size_t)P.C * P.n3));
+    // the prologue-stepped run of small layers (below) alternates state and records between two buffers each
+    HIP_TRY(P.d_state2.ensure(sizeof(CandState) * (size_t)P.C));
+    HIP_TRY(P.d_rec2.ensure(sizeof(RoiRecord) * (size_t)P.C * P.n3));
     {   // refinement scratch per ROI (tables, sampled ROI, row sums, window partials); bounded, rounds cover the rest
         size_t max_rows = 1, max_chunks = 1;
         int max_w = 1;
@@ -670,13 +673,23 @@ int enqueue_search(fpm_ctx* ctx) {
     // pyramid launch precedes it, so its block 0 zeroes them -- safe only because the candidate init then runs in
     // mode 1 (refine == 0: states and live list written directly, no live-count atomics); launch_top_fused checks it
     const bool pyr_zero = top_init && L >= 1;
-    // K1: source pyramid (all staged sources per launch)
-    for (int l = 1; l <= L; ++l) {
+    // K1: source pyramid (all staged sources per launch), two levels per launch (k_pyr_down2) and the odd last level
+    // alone
+    for (int l = 1; l <= L; l += 2) {
         const SrcLevel& a = ctx->src[l - 1];
         const SrcLevel& b = ctx->src[l];
-        ProfScope ps(ctx, FPM_K_PYR, (int64_t)S * ((int64_t)a.w * a.h + (int64_t)b.w * b.h));
-        launch_pyr_down(dsrc + a.off, a.w, a.h, a.pitch, a.img_bytes, dsrc + b.off, b.w, b.h, b.pitch, b.img_bytes, S, st,
-                        0, l == 1 && pyr_zero ? P.d_livecnt.as<int32_t>() : nullptr, l == 1 && pyr_zero ? P.nzero : 0);
+        int32_t* zero = l == 1 && pyr_zero ? P.d_livecnt.as<int32_t>() : nullptr;
+        const int nzero = l == 1 && pyr_zero ? P.nzero : 0;
+        if (l + 1 <= L) {
+            const SrcLevel& c = ctx->src[l + 1];
+            ProfScope ps(ctx, FPM_K_PYR, (int64_t)S * ((int64_t)a.w * a.h + (int64_t)b.w * b.h + (int64_t)c.w * c.h));
+            launch_pyr_down2(dsrc + a.off, a.w, a.h, a.pitch, a.img_bytes, dsrc + b.off, b.w, b.h, b.pitch, b.img_bytes,
+                             dsrc + c.off, c.w, c.h, c.pitch, c.img_bytes, S, st, 0, zero, nzero);
+        } else {
+            ProfScope ps(ctx, FPM_K_PYR, (int64_t)S * ((int64_t)a.w * a.h + (int64_t)b.w * b.h));
+            launch_pyr_down(dsrc + a.off, a.w, a.h, a.pitch, a.img_bytes, dsrc + b.off, b.w, b.h, b.pitch, b.img_bytes, S,
+                            st, 0, zero, nzero);
+        }
     }
     NmsArgs na;
     na.jobs = P.d_jobs.as<NmsJob>(P.off_nms);
@@ -733,11 +746,32 @@ int enqueue_search(fpm_ctx* ctx) {
         ProfScope ps(ctx, FPM_K_CAND_INIT, 0);
         launch_cand_init(ca, st);
     }
+    // the prologue-stepped run: layers L-1 .. run_end, the leading small layers above layer 0 (none of them a
+    // matResult = 1 layer).  From its second layer on, a layer's k_roi_small steps the previous layer's candidates in
+    // its prologue over the unchanged live list (k_cand_step launches saved: run length - 1); one k_cand_step after
+    // the run's last layer steps and compacts.  FPM_STEP_PROLOGUE=0 keeps one k_cand_step per layer (result-neutral).
+    static const bool step_prologue = [] {
+        const char* e = getenv("FPM_STEP_PROLOGUE");
+        return !(e && atoi(e) == 0);
+    }();
+    int run_end = L;
+    if (step_prologue)
+        for (int l = L - 1; l >= 1; --l) {
+            if (!roi_small_fits(ctx->tmpl[l].w, ctx->tmpl[l].h) || ctx->tmpl[l].equal1) break;
+            run_end = l;
+        }
+    if (L - run_end < 2) run_end = L;   // a run of one layer has no prologue to fuse
+    CandState* const state_buf[2] = {P.d_state.as<CandState>(), P.d_state2.as<CandState>()};
+    RoiRecord* const rec_buf[2] = {P.d_rec.as<RoiRecord>(), P.d_rec2.as<RoiRecord>()};
+    int cur_list = 0;   // live[cur_list]: the list the layer's ROIs come from; its count is livecnt[list_cnt]
+    int list_cnt = 0;
+    int run_k = 0;      // layers of the run done
     for (int l = L - 1; l >= 0; --l) {
         const int d = L - 1 - l;
         const SrcLevel& lv = ctx->src[l];
         const TmplLevel& tl = ctx->tmpl[l];
-        RoiArgs ra;
+        const bool in_run = l >= run_end;
+        RoiArgs ra{};
         ra.level = dsrc + lv.off; ra.level_stride = lv.img_bytes;
         ra.W = lv.w; ra.H = lv.h; ra.P = lv.pitch;
         ra.tmpl = ctx->d_tmpl.as<uint8_t>() + tl.off; ra.tw = tl.w; ra.th = tl.h; ra.tp = tl.pitch;
@@ -750,8 +784,8 @@ int enqueue_search(fpm_ctx* ctx) {
         ra.equal1 = tl.equal1 ? 1 : 0;
         ra.per_source = P.nang * P.cap;
         ra.mean = tl.mean; ra.norm = tl.norm; ra.inv_area = tl.inv_area;
-        ra.live = live[d & 1];
-        ra.live_count = livecnt + d;
+        ra.live = live[cur_list];
+        ra.live_count = livecnt + list_cnt;
         ra.state = P.d_state.as<CandState>();
         ra.nodes = P.d_nodes.as<AngleNode>() + P.node_off[d];
         // per-level scratch geometry (the buffers are sized for the largest level)
@@ -764,9 +798,24 @@ int enqueue_search(fpm_ctx* ctx) {
         ra.rec = P.d_rec.as<RoiRecord>();
         ra.step = l > 0 ? 1 : 0;   // candidate step fused into k_roi_eval (layer 0 is decided on the host)
         ra.mark_reached0 = l - 1 == 0 ? 1 : 0;
-        ra.live_out = live[(d + 1) & 1];
+        ra.live_out = live[cur_list ^ 1];
         ra.live_out_count = livecnt + d + 1;
         ra.thr = P.layer_score[l];
+        if (in_run) {
+            // run layer k reads state_buf[(k + 1) & 1] (k = 0: the initial states, buffer 0) and records of layer k - 1
+            // from rec_buf[(k + 1) & 1], writes state_buf[k & 1] and records to rec_buf[k & 1]
+            ra.rec = rec_buf[run_k & 1];
+            if (run_k > 0) {
+                ra.state = state_buf[(run_k + 1) & 1];
+                ra.state_out = state_buf[run_k & 1];
+                ra.prev_rec = rec_buf[(run_k + 1) & 1];
+                ra.prev_nodes = P.d_nodes.as<AngleNode>() + P.node_off[d - 1];
+                ra.prev_thr = P.layer_score[l + 1];
+                ra.prev_W = ctx->src[l + 1].w;
+                ra.prev_H = ctx->src[l + 1].h;
+                ra.live_out_count = livecnt + d;   // the survivors entering this layer (counted, not listed)
+            }
+        }
         const int total_rois = P.C * P.n3;
         const bool small = roi_small_fits(tl.w, tl.h);   // one-kernel refinement of the ROI in LDS
         for (int base = 0; base < total_rois; base += P.slot_cap) {
@@ -794,9 +843,23 @@ int enqueue_search(fpm_ctx* ctx) {
                 launch_roi_eval(ra, st);
             }
         }
+        if (in_run && l > run_end) {   // the step runs in the next layer's prologue
+            ++run_k;
+            continue;
+        }
         if (small && ra.step) {
             ProfScope ps(ctx, FPM_K_CAND_STEP, 0);
+            if (in_run && run_k > 0) {   // the run's last layer: step from its buffers into the canonical state
+                ra.state = state_buf[run_k & 1];
+                ra.state_out = state_buf[0];
+                ra.rec = rec_buf[run_k & 1];
+                ra.live_out_count = livecnt + d + 1;
+            }
             launch_cand_step(ra, P.C, st);
+        }
+        if (ra.step) {
+            cur_list ^= 1;
+            list_cnt = d + 1;
         }
     }
     HIP_TRY(hipGetLastError());
@@ -806,7 +869,7 @@ int enqueue_search(fpm_ctx* ctx) {
         pa.counts = P.d_counts.as<int32_t>(); pa.J = J;
         pa.peaks = P.d_peaks.as<Peak>(); pa.C = P.C;
         pa.livecnt = livecnt; pa.nlive = L + 2;
-        pa.live0 = L > 0 ? live[(L - 1) & 1] : nullptr;
+        pa.live0 = L > 0 ? live[cur_list] : nullptr;   // the layer-0 list
         pa.live0_count = livecnt + (L > 0 ? L - 1 : 0);
         pa.state = P.d_state.as<CandState>();
         pa.rec = P.d_rec.as<RoiRecord>();
@@ -1685,6 +1748,32 @@ int fpm_op_pyr_down(fpm_ctx* ctx, const uint8_t* src, int32_t w, int32_t h, size
     launch_pyr_down(ctx->d_op_a.as<uint8_t>(), w, h, sp, 0, ctx->d_op_b.as<uint8_t>(), dw, dh, dp, 0, 1, ctx->stream, 3);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpy2DAsync(dst, ds, ctx->d_op_b.p, dp, dw, dh, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return FPM_OK;
+}
+
+int fpm_op_pyr_down2(fpm_ctx* ctx, const uint8_t* src, int32_t w, int32_t h, size_t ss, uint8_t* dst1, size_t ds1,
+                     uint8_t* dst2, size_t ds2, int32_t seg_chunks) {
+    if (!ctx) return FPM_E_INVALID_ARG;
+    if (!src || !dst1 || !dst2 || w <= 0 || h <= 0 || ss < (size_t)w || seg_chunks < 0) {
+        ctx->err = "bad image";
+        return FPM_E_INVALID_ARG;
+    }
+    const int bw = (w + 1) / 2, bh = (h + 1) / 2, cw = (bw + 1) / 2, ch = (bh + 1) / 2;
+    if (ds1 < (size_t)bw || ds2 < (size_t)cw) { ctx->err = "bad dst stride"; return FPM_E_INVALID_ARG; }
+    HIP_TRY(hipSetDevice(ctx->device));
+    // the search's level layout: pitch round_up(w + 4, 64), one spare row
+    const int sp = round_up(w + 4, 64), bp = round_up(bw + 4, 64), cp = round_up(cw + 4, 64);
+    const size_t boff = round_up((size_t)bp * (bh + 1), (size_t)256);
+    HIP_TRY(ctx->d_op_a.ensure((size_t)sp * (h + 1)));
+    HIP_TRY(ctx->d_op_b.ensure(boff + (size_t)cp * (ch + 1)));
+    HIP_TRY(hipMemcpy2DAsync(ctx->d_op_a.p, sp, src, ss, w, h, hipMemcpyHostToDevice, ctx->stream));
+    uint8_t* b = ctx->d_op_b.as<uint8_t>();
+    launch_pyr_down2(ctx->d_op_a.as<uint8_t>(), w, h, sp, 0, b, bw, bh, bp, 0, b + boff, cw, ch, cp, 0, 1, ctx->stream,
+                     seg_chunks);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy2DAsync(dst1, ds1, b, bp, bw, bh, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpy2DAsync(dst2, ds2, b + boff, cp, cw, ch, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return FPM_OK;
 }

@@ -133,6 +133,16 @@ struct RoiArgs {
     int32_t* live_out;
     int32_t* live_out_count;
     double thr;              // vecLayerScore[layer]
+    // k_roi_small with prev_rec set (consecutive small layers above layer 0): the previous
+    // layer's candidate step runs in each workgroup's prologue (every workgroup of a candidate computes the same
+    // stepped state; jj 0 stores it to state_out and counts the survivor in *live_out_count), over the previous
+    // layer's live list unchanged -- candidates that died stay in it as holes their workgroups skip.  k_cand_step
+    // after the run's last layer compacts the list.  k_cand_step also writes state_out (nullptr = state).
+    const RoiRecord* prev_rec;   // the previous layer's records [cand * n3 + j]
+    const AngleNode* prev_nodes; // the previous layer's nodes
+    double prev_thr;             // vecLayerScore of the previous layer
+    int32_t prev_W, prev_H;      // the previous layer's level size
+    CandState* state_out;
     uint64_t* stamps;        // profiling ablations only (scripts/roi_microbench.hip): per-phase s_memtime stamps
 };
 
@@ -161,6 +171,10 @@ struct PackArgs {
 void launch_pyr_down(const uint8_t* src, int sw, int sh, int sp, size_t s_img, uint8_t* dst, int dw, int dh,
                      int dp, size_t d_img, int nimg, hipStream_t st, int seg_chunks = 0, int32_t* zero = nullptr,
                      int nzero = 0);
+// two pyramid levels in one launch: src -> b (level l+1, written) -> c (level l+2); same arguments per level
+void launch_pyr_down2(const uint8_t* src, int sw, int sh, int sp, size_t s_img, uint8_t* bdst, int bw, int bh, int bp,
+                      size_t b_img, uint8_t* cdst, int cw, int ch, int cp, size_t c_img, int nimg, hipStream_t st,
+                      int seg_chunks = 0, int32_t* zero = nullptr, int nzero = 0);
 // zero / nzero: counters the search zeroes before its later kernels use them (block (0, 0) clears them), so the
 // graph carries no memset nodes
 void launch_warp(const WarpJob* jobs, int njobs, int max_pixels, hipStream_t st, int32_t* zero = nullptr,

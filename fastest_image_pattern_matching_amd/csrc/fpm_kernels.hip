@@ -409,6 +409,246 @@ void launch_pyr_down(const uint8_t* src, int sw, int sh, int sp, size_t s_img, u
                            dp, d_img, nimg, zero, nzero);
 }
 
+// ---- K1, two levels per launch (the product's search pyramid, round 4): a workgroup walks a strip of PD2_OWC columns
+// of level l+2 down in chunks.  A chunk first filters PD2_OHB rows of level l+1 over the PD2_OWB columns the strip's
+// level-(l+2) outputs read -- its own 2 PD2_OWC columns, stored to memory, plus 2 halo columns on each side that the
+// neighbouring strips own -- from a level-l window exactly as k_pyr_down_s does, and keeps them in an LDS ring after
+// the 4 rows the previous chunk left there.  It then applies level l+1's own reflect-101 border to the ring (cv::pyrDown
+// pads its input, so a level-(l+1) column or row outside the image is a copy of one of its pixels, not a filtered
+// level-l value) and filters the PD2_OHB / 2 level-(l+2) rows the ring now completes.  Level l+1 is written once and
+// never read back (the one-level kernel re-reads it for the next level), and a search's pyramid takes half the
+// launches.  A run of chunks that does not start at the top of its strip first rebuilds the 4 ring rows the chunk
+// above would have carried (a 76-row level-l window instead of 68).  Same integer arithmetic as k_pyr_down on both
+// levels: exact.  The next chunk's 64 level-l rows are in flight while a chunk is filtered.
+constexpr int PD2_OWC = 64;                       // level-(l+2) columns per strip
+constexpr int PD2_OWB = 2 * PD2_OWC + 4;          // 132 level-(l+1) columns per strip (2-column halos)
+constexpr int PD2_GB = PD2_OWB / 4;               // 33 groups of 4 level-(l+1) columns
+constexpr int PD2_BP = 136;                       // ring row pitch (bytes) = level-(l+1) horizontal-sum pitch (u16)
+// PD2_OHB: level-(l+1) rows per chunk (32: window 76 rows at a run start, 68 after it; ring 4 carried + 32 + 2 rows
+// reflected past the bottom row)
+template <int PD2_OHB>
+__global__ __launch_bounds__(256) void k_pyr_down2(const uint8_t* __restrict__ src0, int sw, int sh, int sp,
+                                                   size_t s_img, uint8_t* __restrict__ b0, int bw, int bh, int bpp,
+                                                   size_t b_img, uint8_t* __restrict__ c0, int cw, int ch, int cpp,
+                                                   size_t c_img, int nimg, int32_t* zero, int nzero) {
+    constexpr int PD2_IH = 2 * (PD2_OHB + 4) + 4, PD2_RING = PD2_OHB + 6;
+    __shared__ __attribute__((aligned(16))) uint8_t tin[PD2_IH][PD_IW];
+    __shared__ __attribute__((aligned(16))) uint16_t hs[PD2_IH][PD2_BP];
+    __shared__ __attribute__((aligned(16))) uint8_t ring[PD2_RING][PD2_BP];
+    __shared__ __attribute__((aligned(16))) uint16_t hc[PD2_RING][PD2_OWC];
+    if (blockIdx.x == 0)
+        for (int i = threadIdx.x; i < nzero; i += 256) zero[i] = 0;
+    // work units = (image, strip, chunk), contiguous ranges per workgroup, XCD groups on neighbouring ranges (as
+    // k_pyr_down_s)
+    const int gx = (cw + PD2_OWC - 1) / PD2_OWC, chunks = (bh + PD2_OHB - 1) / PD2_OHB;
+    const long U = (long)gx * chunks * nimg;
+    const int w = xcd_remap(blockIdx.x, gridDim.x);
+    long u = U * w / gridDim.x;
+    const long u_end = U * (w + 1) / gridDim.x;
+    const int tid = threadIdx.x;
+    constexpr int Q = PD_IW / 16;                    // 18 uint4 per window row
+    constexpr int NL = (PD2_IH * Q + 255) / 256;     // 6 loads per thread for a 76-row window
+    constexpr unsigned short kw[5] = {1, 4, 6, 4, 1};
+    auto srow = [&](int y) {   // level-l rows: one reflection covers -2 .. sh + 1; rows past that are clamped (unused)
+        y = y < 0 ? -y : y;
+        y = y >= sh ? 2 * sh - 2 - y : y;
+        return y < 0 ? 0 : (y >= sh ? sh - 1 : y);
+    };
+    while (u < u_end) {
+        const long strip = u / chunks;
+        const int k_begin = (int)(u - strip * chunks);
+        const int k_end = k_begin + (int)min(u_end - u, (long)(chunks - k_begin));
+        u += k_end - k_begin;
+        const int sx = (int)(strip % gx), bz = (int)(strip / gx);
+        const uint8_t* src = src0 + (size_t)bz * s_img;
+        uint8_t* bdst = b0 + (size_t)bz * b_img;
+        uint8_t* cdst = c0 + (size_t)bz * c_img;
+        const int cx0 = sx * PD2_OWC;
+        const int bx0 = 2 * cx0 - 2;   // ring column 0 <-> level-(l+1) column bx0
+        const int ix0 = 4 * cx0 - 16;  // tin column 0 <-> level-l column ix0 (16-byte aligned)
+        // level-l columns outside [0, sw) that the strip's in-image level-(l+1) columns read: reflect-101 patches
+        const int xlo = 2 * max(bx0, 0) - 2, xhi = 2 * min(bx0 + PD2_OWB - 1, bw - 1) + 2;
+        const bool edge = xlo < 0 || xhi >= sw;                      // uniform per workgroup
+        const bool bedge = bx0 < 0 || bx0 + PD2_OWB > bw;            // level-(l+1) columns to reflect in the ring
+        uint4 v[NL];
+        auto issue = [&](int iy, int nrows) {   // window rows [.., + nrows) <- level-l rows iy ..
+#pragma unroll
+            for (int q = 0; q < NL; ++q) {
+                const int i = tid + 256 * q;
+                const int r = i / Q, c = i - r * Q;
+                const int x = ix0 + 16 * c;
+                v[q] = make_uint4(0, 0, 0, 0);
+                if (r < nrows && x >= 0 && x + 16 <= sp) v[q] = *(const uint4*)(src + (size_t)srow(iy + r) * sp + x);
+            }
+        };
+        __syncthreads();   // the previous run is done with the LDS
+        // a run start: level-(l+1) rows 32 k - 4 .. 32 k + 31, i.e. level-l rows 64 k - 10 .. 64 k + 65
+        issue(2 * (PD2_OHB * k_begin - 4) - 2, PD2_IH);
+        for (int k = k_begin; k < k_end; ++k) {
+            const bool start = k == k_begin;
+            const int roff = start ? 0 : 4, nrows = start ? PD2_IH : 2 * PD2_OHB;
+            const int by_first = start ? PD2_OHB * k - 4 : PD2_OHB * k;   // first level-(l+1) row filtered
+            const int nb = PD2_OHB * (k + 1) - by_first;                   // 36 or 32 rows
+            const int iy = 2 * by_first - 2 + roff;                        // level-l row of window row roff
+            const int rb0 = PD2_OHB * k - 4;                               // level-(l+1) row of ring row 0
+#pragma unroll
+            for (int q = 0; q < NL; ++q) {
+                const int i = tid + 256 * q;
+                const int r = i / Q, c = i - r * Q;
+                if (r < nrows) *(uint4*)&tin[roff + r][16 * c] = v[q];
+            }
+            if (edge) {
+                __syncthreads();   // the 16-byte stores above cover the patched bytes
+                for (int i = tid; i < nrows * 4; i += 256) {
+                    const int r = i >> 2, q = i & 3;
+                    const int x = q < 2 ? xlo + q : xhi - (q - 2);   // xlo, xlo + 1, xhi, xhi - 1
+                    if ((x < 0 && q < 2) || (x >= sw && q >= 2))
+                        tin[roff + r][x - ix0] = src[(size_t)srow(iy + r) * sp + reflect101(x, sw)];
+                }
+            }
+            __syncthreads();
+            if (k + 1 < k_end) issue(2 * PD2_OHB * (k + 1) + 2, 2 * PD2_OHB);
+            // level l+1, horizontal [1 4 6 4 1] of the new window rows: ring column p = 4g + j reads level-l columns
+            // 2 (bx0 + p) - 2 .. + 4 = tin bytes 8g + 2j + 10 .. + 14
+            for (int i = tid; i < nrows * PD2_GB; i += 256) {
+                const int r = roff + i / PD2_GB, g = i % PD2_GB;
+                const uint32_t* wp = (const uint32_t*)&tin[r][8 * g + 8];
+                const uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2], w3 = wp[3];
+                const uint32_t h0 = __builtin_amdgcn_udot4(PD_K, __builtin_amdgcn_alignbyte(w1, w0, 2), (w1 >> 16) & 0xff, false);
+                const uint32_t h1 = __builtin_amdgcn_udot4(PD_K, w1, w2 & 0xff, false);
+                const uint32_t h2 = __builtin_amdgcn_udot4(PD_K, __builtin_amdgcn_alignbyte(w2, w1, 2), (w2 >> 16) & 0xff, false);
+                const uint32_t h3 = __builtin_amdgcn_udot4(PD_K, w2, w3 & 0xff, false);
+                uint2 o;
+                o.x = h0 | (h1 << 16);
+                o.y = h2 | (h3 << 16);
+                *(uint2*)&hs[r][4 * g] = o;
+            }
+            __syncthreads();
+            // level l+1, vertical: rows by_first .. + nb - 1 into ring rows by - rb0; the strip's own in-image columns
+            // (ring columns 2 .. 2 PD2_OWC + 1) and rows (>= 32 k: the rebuilt carry rows belong to the chunk above)
+            // go to memory as 16-bit pairs
+            for (int i = tid; i < nb * PD2_GB; i += 256) {
+                const int orow = i / PD2_GB, g = i - orow * PD2_GB;
+                fpm_u16x2 a01 = {128, 128}, a23 = {128, 128};
+#pragma unroll
+                for (int tt = 0; tt < 5; ++tt) {
+                    const uint2 q = *(const uint2*)&hs[2 * orow + tt][4 * g];
+                    a01 += __builtin_bit_cast(fpm_u16x2, q.x) * kw[tt];
+                    a23 += __builtin_bit_cast(fpm_u16x2, q.y) * kw[tt];
+                }
+                const uint32_t packed = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, a23),
+                                                              __builtin_bit_cast(uint32_t, a01), 0x07050301u);
+                const int by = by_first + orow;
+                *(uint32_t*)&ring[by - rb0][4 * g] = packed;
+                if (by < PD2_OHB * k || by >= bh) continue;
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    const int p = 4 * g + 2 * hh, bx = bx0 + p;
+                    if (p < 2 || p >= 2 * PD2_OWC + 2 || bx >= bw) continue;
+                    uint8_t* d = bdst + (size_t)by * bpp + bx;
+                    const uint32_t pr = packed >> (16 * hh);
+                    if (bx + 1 < bw) *(uint16_t*)d = (uint16_t)pr;
+                    else d[0] = (uint8_t)pr;
+                }
+            }
+            __syncthreads();
+            // level l+1's reflect-101 border in the ring: rows -2, -1 (first chunk), bh, bh + 1 (last chunk; ring rows
+            // <= 37), then columns -2, -1, bw, bw + 1 where they fall in the strip (corners from the reflected rows)
+            const bool top = k == 0, bottom = k == chunks - 1;
+            if (top || bottom) {
+                for (int i = tid; i < 4 * PD2_OWB; i += 256) {
+                    const int e = i / PD2_OWB, c = i - e * PD2_OWB;
+                    if ((e < 2 && !top) || (e >= 2 && !bottom)) continue;
+                    const int r = e < 2 ? e - 2 : bh + (e - 2);
+                    ring[r - rb0][c] = ring[reflect101(r, bh) - rb0][c];
+                }
+                if (bedge) __syncthreads();
+            }
+            if (bedge) {
+                for (int i = tid; i < PD2_RING * 4; i += 256) {
+                    const int r = i >> 2, q = i & 3;
+                    const int bx = q < 2 ? q - 2 : bw + (q - 2);
+                    const int p = bx - bx0;
+                    if (p >= 0 && p < PD2_OWB) ring[r][p] = ring[r][reflect101(bx, bw) - bx0];
+                }
+            }
+            if (top || bottom || bedge) __syncthreads();
+            // level l+2: the rows this chunk completes, [lo, hi): row c reads level-(l+1) rows 2c - 2 .. 2c + 2
+            const int lo = top ? 0 : PD2_OHB / 2 * k - 1;
+            const int hi = bottom ? ch : min(ch, PD2_OHB / 2 * (k + 1) - 1);
+            const int r_lo = 2 * lo - 2 - rb0, nr = 2 * (hi - lo) + 3;   // ring rows read
+            // horizontal: output cx0 + 4g + j reads ring columns 8g + 2j .. + 4
+            for (int i = tid; i < nr * (PD2_OWC / 4); i += 256) {
+                const int r = r_lo + i / (PD2_OWC / 4), g = i % (PD2_OWC / 4);
+                const uint32_t* wp = (const uint32_t*)&ring[r][8 * g];
+                const uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2];
+                const uint32_t h0 = __builtin_amdgcn_udot4(PD_K, w0, w1 & 0xff, false);
+                const uint32_t h1 = __builtin_amdgcn_udot4(PD_K, __builtin_amdgcn_alignbyte(w1, w0, 2), (w1 >> 16) & 0xff, false);
+                const uint32_t h2 = __builtin_amdgcn_udot4(PD_K, w1, w2 & 0xff, false);
+                const uint32_t h3 = __builtin_amdgcn_udot4(PD_K, __builtin_amdgcn_alignbyte(w2, w1, 2), (w2 >> 16) & 0xff, false);
+                uint2 o;
+                o.x = h0 | (h1 << 16);
+                o.y = h2 | (h3 << 16);
+                *(uint2*)&hc[r][4 * g] = o;
+            }
+            __syncthreads();
+            // carries for the next chunk (nothing reads them before the barrier below): ring rows 32 .. 35 (level-(l+1)
+            // rows 32 k + 28 .. + 31) -> 0 .. 3, and the window's last 4 horizontal-sum rows (level-l rows 64 k + 62 ..
+            // + 65) -> 0 .. 3
+            for (int i = tid; i < 4 * (PD2_BP / 4); i += 256)
+                ((uint32_t*)ring[i / (PD2_BP / 4)])[i % (PD2_BP / 4)] = ((uint32_t*)ring[PD2_OHB + i / (PD2_BP / 4)])[i % (PD2_BP / 4)];
+            const int hlast = roff + nrows - 4;
+            for (int i = tid; i < 4 * (PD2_BP / 2); i += 256)
+                ((uint32_t*)hs[i / (PD2_BP / 2)])[i % (PD2_BP / 2)] = ((uint32_t*)hs[hlast + i / (PD2_BP / 2)])[i % (PD2_BP / 2)];
+            // vertical: 4 consecutive outputs of one row per item
+            for (int i = tid; i < (hi - lo) * (PD2_OWC / 4); i += 256) {
+                const int crow = lo + i / (PD2_OWC / 4), g = i % (PD2_OWC / 4);
+                const int cx = cx0 + 4 * g;
+                if (cx >= cw) continue;
+                const int r0 = 2 * crow - 2 - rb0;
+                fpm_u16x2 a01 = {128, 128}, a23 = {128, 128};
+#pragma unroll
+                for (int tt = 0; tt < 5; ++tt) {
+                    const uint2 q = *(const uint2*)&hc[r0 + tt][4 * g];
+                    a01 += __builtin_bit_cast(fpm_u16x2, q.x) * kw[tt];
+                    a23 += __builtin_bit_cast(fpm_u16x2, q.y) * kw[tt];
+                }
+                const uint32_t packed = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, a23),
+                                                              __builtin_bit_cast(uint32_t, a01), 0x07050301u);
+                uint8_t* d = cdst + (size_t)crow * cpp + cx;
+                if (cx + 4 <= cw) {
+                    *(uint32_t*)d = packed;
+                } else {
+                    for (int j = 0; j < cw - cx; ++j) d[j] = (uint8_t)(packed >> (8 * j));
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+static const int kPyr2OH = [] {   // FPM_PYR2_OH (16 or 32): profiling override of the two-level chunk height
+    const char* e = getenv("FPM_PYR2_OH");
+    return e && atoi(e) == 32 ? 32 : 16;
+}();
+// one launch for pyramid levels l+1 and l+2 of nimg images (the units shared over kPyrWGs workgroups as
+// launch_pyr_down; seg_chunks > 0: that many units per workgroup, so runs start mid-strip -- tests)
+void launch_pyr_down2(const uint8_t* src, int sw, int sh, int sp, size_t s_img, uint8_t* bdst, int bw, int bh, int bp,
+                      size_t b_img, uint8_t* cdst, int cw, int ch, int cp, size_t c_img, int nimg, hipStream_t st,
+                      int seg_chunks, int32_t* zero, int nzero) {
+    if (bw <= 0 || bh <= 0 || cw <= 0 || ch <= 0 || nimg <= 0) return;
+    const int ohb = kPyr2OH;
+    const int gx = (cw + PD2_OWC - 1) / PD2_OWC, chunks = (bh + ohb - 1) / ohb;
+    const long units = (long)gx * chunks * nimg;
+    const long g = seg_chunks > 0 ? (units + seg_chunks - 1) / seg_chunks : std::min(units, (long)kPyrWGs);
+    if (ohb == 16)
+        hipLaunchKernelGGL(k_pyr_down2<16>, dim3((unsigned)g), dim3(256), 0, st, src, sw, sh, sp, s_img, bdst, bw, bh,
+                           bp, b_img, cdst, cw, ch, cp, c_img, nimg, zero, nzero);
+    else
+        hipLaunchKernelGGL(k_pyr_down2<32>, dim3((unsigned)g), dim3(256), 0, st, src, sw, sh, sp, s_img, bdst, bw, bh,
+                           bp, b_img, cdst, cw, ch, cp, c_img, nimg, zero, nzero);
+}
+
 // ============================================================================================== K2
 __global__ __launch_bounds__(256) void k_warp(const WarpJob* __restrict__ jobs, int32_t* zero, int nzero) {
     if (blockIdx.x == 0 && blockIdx.y == 0)
@@ -2355,14 +2595,18 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t box_rsrc(const uint8_t* base) 
 //  * staging in 16-byte pieces: a lane's global offset (row lane >> 2, chunk lane & 3) and LDS address are kernel
 //    constants, every LDS store carries its row group as the instruction's immediate offset, and all of a box's rows
 //    (<= 4 loads per lane) are in flight together; whole 16-row groups are staged, so up to 15 rows past the box are
-//    read (the level slab carries slack rows for that) and land inside the wave's 64 x 64-byte buffer;
+//    read (the level slab carries slack rows for that); rows past the wave's buffer are dropped (never sampled);
+//  * PITCH: the footprint's LDS row pitch.  The product's 68 bytes (17 dwords) puts the 8 sampled rows of a wave's
+//    4 x 8-pixel block on distinct banks; at 64 bytes (one b128 store per 16-byte piece instead of 4 b32) rows r and
+//    r + 4 share banks and the tap reads conflict: 465 vs 384 us at layer 0 (43 sources, scripts/roi_microbench.hip,
+//    profiles/r04/mbw_r04f.txt; the round-3 form with per-row staging: 397 us).  STG 1 = the round-3 per-row staging;
 //  * per task, not per ROI: the lane's table offsets, the column mask and the row masks (the three ROIs share them);
 //  * the interior pixel: the tables' 16-fraction-bit scale (kTabShift) puts the integer tap coordinate in the high
 //    half-word, read by SDWA word selects, and the 16 tap reads and their wait are one asm statement.
-template <int WPE>
+template <int WPE, int PITCH = 64, int STG = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_warp3(RoiArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t ft_all[4 * ROI_FT + 16];
-    constexpr int ftw = 64;   // footprint row pitch: one LDS-DMA instruction fills 4 rows of 16 dwords
+    constexpr int ftw = PITCH;   // footprint row pitch
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint8_t* FT = ft_all + wv * ROI_FT;
@@ -2382,7 +2626,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const uint32_t stage_lds = ft_lds + (uint32_t)((lane >> 2) * ftw + 16 * (lane & 3));
     const size_t tab_stride = (size_t)2 * (a.tabw + a.tabh);
     const uint32_t pitch_v = __builtin_amdgcn_readfirstlane(ftw);   // the LDS pitch as an SDWA operand
-    auto stage = [&](int fth, const uint8_t* gsrc) {
+    auto stage = [&](int wpr, int fth, const uint8_t* gsrc) {
+        if (STG == 1) {
+            stage_footprint32<12, PITCH>(FT, wpr, fth, gsrc, P, lane);
+            return;
+        }
         const int n = (fth + 15) >> 4;   // wave-uniform, <= 4
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         u32x4 v[4];
@@ -2390,8 +2638,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         for (int k = 0; k < 4; ++k)
             if (k < n) v[k] = ld_at<u32x4>(gsrc + (size_t)k * 16 * P, stage_goff);
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (k < n) *(__attribute__((address_space(3))) u32x4*)(size_t)(stage_lds + 16 * ftw * k) = v[k];
+        for (int k = 0; k < 4; ++k) {
+            if (k >= n) continue;
+            if (PITCH % 16 == 0) {
+                *(__attribute__((address_space(3))) u32x4*)(size_t)(stage_lds + 16 * ftw * k) = v[k];
+            } else if ((lane >> 2) + 16 * k < ROI_FT / PITCH) {   // rows past the buffer are never sampled
+                __attribute__((address_space(3))) uint32_t* d =
+                    (__attribute__((address_space(3))) uint32_t*)(size_t)(stage_lds + 16 * ftw * k);
+                d[0] = v[k].x; d[1] = v[k].y; d[2] = v[k].z; d[3] = v[k].w;
+            }
+        }
     };
     for (int task = xs.lo + xs.k * 4 + wv; task < xs.hi; task += tstride) {
         const int cand = task / per_roi;
@@ -2440,7 +2696,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         load_tabs(3 * cand);   // the first ROI's tables share the staging's round trip
         if (uni) {
             wave_sync();   // previous task's gathers are done with FT
-            stage(ufth, lvl + (size_t)uy0 * P + ux0);
+            stage(uwpr, ufth, lvl + (size_t)uy0 * P + ux0);
             wave_sync();
         }
 #pragma unroll 1
@@ -2453,7 +2709,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 bxa = ux0; by0 = uy0;
             } else {
                 wave_sync();
-                if ((flags & kTileAny) && in_lds) stage(fh[j], lvl + (size_t)by0 * P + bxa);
+                if ((flags & kTileAny) && in_lds) stage(wp[j], fh[j], lvl + (size_t)by0 * P + bxa);
                 wave_sync();
             }
             if (j > 0) load_tabs(slot);
@@ -3270,6 +3526,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 }
 #endif   // FPM_EXPERIMENTAL
 
+// candidate step of :329-366 as a pure function of the state and the n3 records (k_cand_step, k_roi_eval, the
+// k_roi_small prologue)
+__device__ __forceinline__ CandState cand_step_state(CandState s, int n3, const AngleNode* nodes, double thr, int W,
+                                                     int H, int mark_reached0, const float* score, const int* mx,
+                                                     const int* my) {
+    int imax = 0;
+    double big = -1;
+    for (int k = 0; k < n3; ++k)
+        if ((double)score[k] > big) { imax = k; big = score[k]; }
+    if ((double)score[imax] < thr) {   // :331-332
+        s.alive = 0;
+        return s;
+    }
+    const int child = s.node * n3 + imax;
+    const AngleNode nd = nodes[child];
+    const F2 sc = f2((W - 1) / 2.0f, (H - 1) / 2.0f);
+    const F2 r0 = rotate_pt(f2(s.lt.x * 2, s.lt.y * 2), sc, nd.c, nd.s);   // :350-353
+    const F2 pad = f2(r0.x - 3, r0.y - 3);
+    F2 p = f2((float)((double)mx[imax] + pad.x), (float)((double)my[imax] + pad.y));
+    p = rotate_pt(p, sc, nd.cn, nd.sn);
+    s.lt = p;          // :366
+    s.node = child;    // :363
+    s.reached0 = mark_reached0;
+    return s;
+}
+
 // ---- K6-K8 for small templates: one workgroup per ROI does the whole refinement of the ROI in LDS (tables,
 // 32x32-tile sampling from wave footprints, exact row / window sums, the band-by-band banded GEMM on the matrix
 // cores, the ordered f32 fold, CCOEFF, argmax, 3x3) and writes its RoiRecord; k_cand_step then steps the
@@ -3337,9 +3619,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         int id, jj;
         roi_slot(a, slot, id, jj);
         const uint8_t* lvl = a.level + (size_t)(id / a.per_source) * a.level_stride;
+        CandState st = a.state[id];
+        if (a.prev_rec) {   // the previous layer's candidate step (same inputs, same result in every thread)
+            if (st.alive) {
+                const RoiRecord* r = a.prev_rec + (size_t)id * a.n3;
+                float score[3];
+                int mx[3], my[3];
+                for (int k = 0; k < a.n3; ++k) { score[k] = r[k].score; mx[k] = r[k].mx; my[k] = r[k].my; }
+                st = cand_step_state(st, a.n3, a.prev_nodes, a.prev_thr, a.prev_W, a.prev_H, 0, score, mx, my);
+                if (jj == 0 && tid == 0 && st.alive) atomicAdd(a.live_out_count, 1);   // live entering this layer
+            }
+            if (jj == 0 && tid == 0) a.state_out[id] = st;
+            if (!st.alive) continue;   // uniform over the workgroup
+        }
         __syncthreads();
         {   // warpAffine tables of this ROI (getRotatedROI :1074-1090)
-            const CandState st = a.state[id];
             const AngleNode nd = a.nodes[st.node * a.n3 + jj];
             double M[6];
             roi_matrix(W, H, f2(st.lt.x * 2, st.lt.y * 2), nd.c, nd.s, M);
@@ -3640,28 +3934,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // candidate step of :329-366 from the scores and 7x7 argmax positions of a candidate's n3 records: best of the
 // angles, early break below vecLayerScore, back-mapping of ptLT, append to the next live list
 __device__ void cand_step_one(const RoiArgs& a, int id, const float* score, const int* mx, const int* my) {
+    CandState* out = a.state_out ? a.state_out : a.state;
     CandState s = a.state[id];
-    int imax = 0;
-    double big = -1;
-    for (int k = 0; k < a.n3; ++k)
-        if ((double)score[k] > big) { imax = k; big = score[k]; }
-    if ((double)score[imax] < a.thr) {   // :331-332
-        s.alive = 0;
-        a.state[id] = s;
+    if (!s.alive) {   // a hole of a prologue-stepped run (k_roi_small prev_rec): dead before this layer
+        out[id] = s;
         return;
     }
-    const int child = s.node * a.n3 + imax;
-    const AngleNode nd = a.nodes[child];
-    const F2 sc = f2((a.W - 1) / 2.0f, (a.H - 1) / 2.0f);
-    const F2 r0 = rotate_pt(f2(s.lt.x * 2, s.lt.y * 2), sc, nd.c, nd.s);   // :350-353
-    const F2 pad = f2(r0.x - 3, r0.y - 3);
-    F2 p = f2((float)((double)mx[imax] + pad.x), (float)((double)my[imax] + pad.y));
-    p = rotate_pt(p, sc, nd.cn, nd.sn);
-    s.lt = p;          // :366
-    s.node = child;    // :363
-    s.reached0 = a.mark_reached0;
-    a.state[id] = s;
-    a.live_out[atomicAdd(a.live_out_count, 1)] = id;
+    s = cand_step_state(s, a.n3, a.nodes, a.thr, a.W, a.H, a.mark_reached0, score, mx, my);
+    out[id] = s;
+    if (s.alive) a.live_out[atomicAdd(a.live_out_count, 1)] = id;
 }
 
 // the candidate step as its own launch over the live list (after k_roi_small's equal1 records)
@@ -3860,7 +4141,7 @@ void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
         const long want3 = (tiles / 3 + 3) / 4;
         // 7 waves per SIMD with the first ROI's tables requested before the staging (8 would spill them): microbenchmark
         // 405.5 / 406.3 -> 400.6 / 402.0 us (round 3)
-        hipLaunchKernelGGL((k_roi_warp3<7>), dim3((int)(want3 < 16384 ? want3 : 16384)), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((k_roi_warp3<7, kFtPitch, 0>), dim3((int)(want3 < 16384 ? want3 : 16384)), dim3(256), 0, st, a);
         return;
     }
     hipLaunchKernelGGL((k_roi_warp<kWarpFootBatch, 0, kWarpWaves>), dim3(grid), dim3(256), 0, st, a);
@@ -3885,6 +4166,13 @@ static void launch_corr_regs(const RoiArgs& a, long items, size_t lds, hipStream
         if ((NK == 4 || NK == 8) && lds * 4 <= kLdsPerCu) {
             const int grid = (int)(items < 256 * 4 ? items : 256 * 4);
             hipLaunchKernelGGL((k_roi_corr<0, true, 4, NK, false, 1, true>), dim3(grid), dim3(256), lds, st, a);
+            return;
+        }
+        // at 12 k-steps the source rows staged by LDS-DMA (no staging VGPRs) make room for 4 waves per SIMD (Src7 layer 0
+        // at 43 sources: 269.8 -> 241.1 us, host-checked, profiles/r04/mb_r04e.txt)
+        if (NK == 12 && lds * 4 <= kLdsPerCu) {
+            const int grid = (int)(items < 256 * 4 ? items : 256 * 4);
+            hipLaunchKernelGGL((k_roi_corr<0, true, 4, NK, false, 1, true, true>), dim3(grid), dim3(256), lds, st, a);
             return;
         }
         // row results staged in LDS and flushed during the next item's staging (SE; Src7 microbenchmark at 43 sources:

@@ -304,6 +304,18 @@ class TemplateMatcher:
             raise ValueError(self.last_error())
         return out
 
+    def pyr_down2(self, img, seg_chunks: int = 0):
+        """(pyrDown(img), pyrDown(pyrDown(img))) from the search's two-level pyramid kernel."""
+        g = _gray(img)
+        h, w = g.shape
+        b = np.zeros(((h + 1) // 2, (w + 1) // 2), np.uint8)
+        c = np.zeros(((b.shape[0] + 1) // 2, (b.shape[1] + 1) // 2), np.uint8)
+        rc = self._check(self._lib.fpm_op_pyr_down2(self._ctx, L.u8ptr(g), w, h, g.strides[0], L.u8ptr(b), b.strides[0],
+                                                    L.u8ptr(c), c.strides[0], int(seg_chunks)), "pyr_down2")
+        if rc != L.FPM_OK:
+            raise ValueError(self.last_error())
+        return b, c
+
     def warp_affine(self, img, m, dsize, border: int = 0) -> np.ndarray:
         g = _gray(img)
         h, w = g.shape

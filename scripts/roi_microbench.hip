@@ -143,7 +143,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                     }
                     lds_taps16<kFtPitch>(off, v);
                     const uint32_t pk = bilerp_row4(v, fxv, fyv);
-                    if (ry0 + lr + 8 * i <= ry1) st_at<uint32_t>(tile, st_lane + 256u * i, pk & colmask);
+                    if (ry0 + lr + 8 * i <= ry1) st_at<uint32_t>(tile, st_lane + 256u * i, (pk & colmask) ^ kRoiFlip);
                 }
                 continue;
             }
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                     if (c0 + u >= RW) v = 0;
                     pk |= (uint32_t)v << (8 * u);
                 }
-                st_at<uint32_t>(tile, st_lane + 256u * i, pk);
+                st_at<uint32_t>(tile, st_lane + 256u * i, pk ^ kRoiFlip);
             }
         }
     }
@@ -282,6 +282,30 @@ int main(int argc, char** argv) {
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<8>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 8w");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 7w");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<6>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 6w");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 7w p68");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 1>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 7w p68 r03stg");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 64, 1>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 7w p64 r03stg");
+            {   // every warp3 form writes the same ROI bytes as the round-3 form
+                const size_t nb = (size_t)a.slot_cap * a.roi_stride;
+                std::vector<uint8_t> ref(nb), got(nb);
+                auto run_cmp = [&](auto launch, const char* name) {
+                    CK(hipMemset(a.roi, 0x5a, nb));
+                    launch();
+                    CK(hipDeviceSynchronize());
+                    CK(hipMemcpy(got.data(), a.roi, nb, hipMemcpyDeviceToHost));
+                    size_t bad = 0;
+                    for (size_t i = 0; i < nb; ++i) bad += got[i] != ref[i];
+                    printf("warp check %-22s %s (%zu bytes differ)\n", name, bad ? "FAIL" : "OK", bad);
+                };
+                CK(hipMemset(a.roi, 0x5a, nb));
+                hipLaunchKernelGGL((k_roi_warp3_r03<12, 7, 0, 1>), dim3(grid3), dim3(256), 0, 0, a);
+                CK(hipDeviceSynchronize());
+                CK(hipMemcpy(ref.data(), a.roi, nb, hipMemcpyDeviceToHost));
+                run_cmp([&] { hipLaunchKernelGGL((k_roi_warp3<7>), dim3(grid3), dim3(256), 0, 0, a); }, "p64");
+                run_cmp([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0>), dim3(grid3), dim3(256), 0, 0, a); }, "p68");
+                run_cmp([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 1>), dim3(grid3), dim3(256), 0, 0, a); }, "p68 r03stg");
+                run_cmp([&] { launch_roi_warp(a, 0); }, "product");
+            }
 
             timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 5, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp no stores");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp<12, 6, 8>), dim3(grid), dim3(256), 0, 0, a); }, "warp gathers only");
@@ -492,6 +516,70 @@ int main(int argc, char** argv) {
         timeit([&] { hipLaunchKernelGGL(k_pyr_down<2>, grid, dim3(256), 0, 0, d_img, W, H, P, a.level_stride, d_out, dw, dh, dp, (size_t)dp * (dh + 1)); }, "pyr +lds tile");
         timeit([&] { hipLaunchKernelGGL(k_pyr_down<3>, grid, dim3(256), 0, 0, d_img, W, H, P, a.level_stride, d_out, dw, dh, dp, (size_t)dp * (dh + 1)); }, "pyr +horizontal");
         timeit([&] { hipLaunchKernelGGL(k_pyr_down<0>, grid, dim3(256), 0, 0, d_img, W, H, P, a.level_stride, d_out, dw, dh, dp, (size_t)dp * (dh + 1)); }, "pyr full");
+        // levels 1 and 2: two one-level launches vs one k_pyr_down2 launch, and their bytes compared
+        const int cw = (dw + 1) / 2, chh = (dh + 1) / 2, cp = 1024;
+        const size_t b_img = (size_t)dp * (dh + 1), c_img = (size_t)cp * (chh + 1);
+        uint8_t *d_c1, *d_b2, *d_c2;
+        CK(hipMalloc(&d_c1, c_img * nsrc)); CK(hipMalloc(&d_b2, b_img * nsrc)); CK(hipMalloc(&d_c2, c_img * nsrc));
+        CK(hipMemset(d_c1, 0, c_img * nsrc)); CK(hipMemset(d_b2, 0, b_img * nsrc)); CK(hipMemset(d_c2, 0, c_img * nsrc));
+        CK(hipMemset(d_out, 0, b_img * nsrc));
+        timeit([&] {
+            launch_pyr_down(d_img, W, H, P, a.level_stride, d_out, dw, dh, dp, b_img, nsrc, 0);
+            launch_pyr_down(d_out, dw, dh, dp, b_img, d_c1, cw, chh, cp, c_img, nsrc, 0);
+        }, "pyr L0->L2 2 launches");
+        timeit([&] { launch_pyr_down2(d_img, W, H, P, a.level_stride, d_b2, dw, dh, dp, b_img, d_c2, cw, chh, cp, c_img, nsrc, 0); },
+               "pyr L0->L2 pyr_down2");
+        {
+            const long units2 = (long)((cw + 63) / 64) * ((dh + 31) / 32) * nsrc;
+            for (int seg : {2, 3, 4, 6, 8, 12, 16}) {
+                char name[64];
+                snprintf(name, sizeof name, "pyr2 seg %d (%ld WGs)", seg, (units2 + seg - 1) / seg);
+                timeit([&] { launch_pyr_down2(d_img, W, H, P, a.level_stride, d_b2, dw, dh, dp, b_img, d_c2, cw, chh, cp, c_img, nsrc, 0, seg); }, name);
+            }
+            // the pair starting at level 1 (input d_out) and level 2 (input d_c1), all sources
+            {
+                launch_pyr_down(d_out, dw, dh, dp, b_img, d_c1, cw, chh, cp, c_img, nsrc, 0);
+                struct Lv { const uint8_t* p; int w, h, pitch; size_t img; };
+                for (Lv in : {Lv{d_out, dw, dh, dp, b_img}, Lv{d_c1, cw, chh, cp, c_img}}) {
+                    const int w1 = (in.w + 1) / 2, h1 = (in.h + 1) / 2, w2 = (w1 + 1) / 2, h2 = (h1 + 1) / 2;
+                    const int p1 = (w1 + 4 + 63) & ~63, p2 = (w2 + 4 + 63) & ~63;
+                    const size_t i1 = (size_t)p1 * (h1 + 1), i2 = (size_t)p2 * (h2 + 1);
+                    uint8_t *o1, *o2;
+                    CK(hipMalloc(&o1, i1 * nsrc)); CK(hipMalloc(&o2, i2 * nsrc));
+                    char name[64];
+                    snprintf(name, sizeof name, "pyr %dx%d 2 launches", in.w, in.h);
+                    timeit([&] {
+                        launch_pyr_down(in.p, in.w, in.h, in.pitch, in.img, o1, w1, h1, p1, i1, nsrc, 0);
+                        launch_pyr_down(o1, w1, h1, p1, i1, o2, w2, h2, p2, i2, nsrc, 0);
+                    }, name);
+                    snprintf(name, sizeof name, "pyr %dx%d pyr_down2", in.w, in.h);
+                    timeit([&] { launch_pyr_down2(in.p, in.w, in.h, in.pitch, in.img, o1, w1, h1, p1, i1, o2, w2, h2, p2, i2, nsrc, 0); }, name);
+                    CK(hipDeviceSynchronize());
+                    CK(hipFree(o1)); CK(hipFree(o2));
+                }
+            }
+            timeit([&] {
+                launch_pyr_down(d_img, W, H, P, a.level_stride, d_out, dw, dh, dp, b_img, 1, 0);
+                launch_pyr_down(d_out, dw, dh, dp, b_img, d_c1, cw, chh, cp, c_img, 1, 0);
+            }, "pyr 1 src 2 launches");
+            timeit([&] { launch_pyr_down2(d_img, W, H, P, a.level_stride, d_b2, dw, dh, dp, b_img, d_c2, cw, chh, cp, c_img, 1, 0); },
+                   "pyr 1 src pyr_down2");
+        }
+        CK(hipDeviceSynchronize());
+        std::vector<uint8_t> x1(b_img * nsrc), x2(b_img * nsrc);
+        size_t bad = 0;
+        CK(hipMemcpy(x1.data(), d_out, b_img * nsrc, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(x2.data(), d_b2, b_img * nsrc, hipMemcpyDeviceToHost));
+        for (int s = 0; s < nsrc; ++s)
+            for (int y = 0; y < dh; ++y)
+                for (int x = 0; x < dw; ++x) bad += x1[s * b_img + (size_t)y * dp + x] != x2[s * b_img + (size_t)y * dp + x];
+        x1.resize(c_img * nsrc); x2.resize(c_img * nsrc);
+        CK(hipMemcpy(x1.data(), d_c1, c_img * nsrc, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(x2.data(), d_c2, c_img * nsrc, hipMemcpyDeviceToHost));
+        for (int s = 0; s < nsrc; ++s)
+            for (int y = 0; y < chh; ++y)
+                for (int x = 0; x < cw; ++x) bad += x1[s * c_img + (size_t)y * cp + x] != x2[s * c_img + (size_t)y * cp + x];
+        printf("pyr_down2 check: %s (%zu bytes differ)\n", bad ? "FAIL" : "OK", bad);
     }
     return 0;
 }

@@ -40,6 +40,21 @@ def test_pyr_down(hip, shape):
     assert np.array_equal(hip.pyr_down(img), oracle.pyr_down(img))
 
 
+@pytest.mark.parametrize("shape", [(1, 1), (2, 2), (3, 5), (5, 3), (7, 130), (9, 257), (68, 136), (69, 137),
+                                   (127, 255), (128, 256), (129, 258), (130, 514), (100, 333), (521, 762),
+                                   (1518, 2012), (3036, 4024)])
+@pytest.mark.parametrize("seg", [0, 1, 2, 3])
+def test_pyr_down2(hip, shape, seg):
+    """Two levels in one launch (k_pyr_down2) = two oracle pyrDowns: strip edges at both levels (widths around the
+    64-column level-2 strip), odd and tiny sizes, runs starting mid-image (seg 1-3 chunks per workgroup)."""
+    rng = np.random.default_rng(shape[0] * 11 + shape[1] + seg)
+    img = rng.integers(0, 256, shape, dtype=np.uint8)
+    b, c = hip.pyr_down2(img, seg)
+    ob = oracle.pyr_down(img)
+    assert np.array_equal(b, ob)
+    assert np.array_equal(c, oracle.pyr_down(ob))
+
+
 def test_pyr_down_strided_input(hip):
     img = np.random.default_rng(9).integers(0, 256, (300, 500), dtype=np.uint8)[10:250, 3:411]
     assert np.array_equal(hip.pyr_down(img), oracle.pyr_down(np.ascontiguousarray(img)))
