@@ -630,6 +630,9 @@ int check_sizes(fpm_ctx* ctx, int w, int h) {   // TemplateMatcher.cpp:99-114
 // ---------------------------------------------------------------------------------------------------------
 // search
 // ---------------------------------------------------------------------------------------------------------
+constexpr int kPrologueMaxSources = 2;            // step prologue of the small layers up to this batch size
+constexpr int64_t kPyr2MaxBytes = 16ll << 20;     // two-level pyramid launches up to this many input bytes
+
 int enqueue_search(fpm_ctx* ctx) {
     Plan& P = ctx->plan;
     const int L = P.L, S = P.S, J = S * P.nang;
@@ -673,15 +676,22 @@ int enqueue_search(fpm_ctx* ctx) {
     // pyramid launch precedes it, so its block 0 zeroes them -- safe only because the candidate init then runs in
     // mode 1 (refine == 0: states and live list written directly, no live-count atomics); launch_top_fused checks it
     const bool pyr_zero = top_init && L >= 1;
-    // K1: source pyramid (all staged sources per launch), two levels per launch (k_pyr_down2) and the odd last level
-    // alone
-    for (int l = 1; l <= L; l += 2) {
+    // K1: source pyramid (all staged sources per launch).  Two levels per launch (k_pyr_down2) where the pair's input
+    // is small (<= kPyr2MaxBytes over the batch: launch-bound levels, e.g. every pair of a single Src7 search: 14.8 ->
+    // 11.3 us for levels 0-2), else one level per launch (k_pyr_down_s keeps more workgroups in flight: 43 Src7 levels
+    // 0-2 in 197 us vs 217-258 us, profiles/r04/mb32_r04g.txt).  FPM_PYR2=0 / 1 forces one form.
+    const char* pyr2_env = getenv("FPM_PYR2");
+    const int pyr2_mode = pyr2_env ? atoi(pyr2_env) : -1;
+    for (int l = 1; l <= L;) {
         const SrcLevel& a = ctx->src[l - 1];
         const SrcLevel& b = ctx->src[l];
         int32_t* zero = l == 1 && pyr_zero ? P.d_livecnt.as<int32_t>() : nullptr;
         const int nzero = l == 1 && pyr_zero ? P.nzero : 0;
-        if (l + 1 <= L) {
-            const SrcLevel& c = ctx->src[l + 1];
+        const int64_t in_bytes = (int64_t)S * a.w * a.h;
+        const bool two = l + 1 <= L && (pyr2_mode >= 0 ? pyr2_mode != 0 : in_bytes <= kPyr2MaxBytes);
+        const SrcLevel& c = ctx->src[two ? l + 1 : l];
+        l += two ? 2 : 1;
+        if (two) {
             ProfScope ps(ctx, FPM_K_PYR, (int64_t)S * ((int64_t)a.w * a.h + (int64_t)b.w * b.h + (int64_t)c.w * c.h));
             launch_pyr_down2(dsrc + a.off, a.w, a.h, a.pitch, a.img_bytes, dsrc + b.off, b.w, b.h, b.pitch, b.img_bytes,
                              dsrc + c.off, c.w, c.h, c.pitch, c.img_bytes, S, st, 0, zero, nzero);
@@ -750,10 +760,12 @@ int enqueue_search(fpm_ctx* ctx) {
     // matResult = 1 layer).  From its second layer on, a layer's k_roi_small steps the previous layer's candidates in
     // its prologue over the unchanged live list (k_cand_step launches saved: run length - 1); one k_cand_step after
     // the run's last layer steps and compacts.  FPM_STEP_PROLOGUE=0 keeps one k_cand_step per layer (result-neutral).
-    static const bool step_prologue = [] {
-        const char* e = getenv("FPM_STEP_PROLOGUE");
-        return !(e && atoi(e) == 0);
-    }();
+    // Used for batches of at most kPrologueMaxSources sources, where the saved launches outweigh the prologue's
+    // dependent loads on every workgroup's critical path (single Src7 search: 23 dispatches, 236.8 us of kernels vs
+    // 25 and 244.6; a 43-source batch: k_roi_small 181 -> 218 us per pass, profiles/r04/gpu_r04g).
+    // FPM_STEP_PROLOGUE=1 forces it, =0 disables it (read when the search is recorded, once per plan).
+    const char* prol_env = getenv("FPM_STEP_PROLOGUE");
+    const bool step_prologue = prol_env ? atoi(prol_env) != 0 : S <= kPrologueMaxSources;
     int run_end = L;
     if (step_prologue)
         for (int l = L - 1; l >= 1; --l) {

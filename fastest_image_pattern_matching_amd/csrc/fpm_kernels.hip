@@ -627,9 +627,11 @@ __global__ __launch_bounds__(256) void k_pyr_down2(const uint8_t* __restrict__ s
     }
 }
 
-static const int kPyr2OH = [] {   // FPM_PYR2_OH (16 or 32): profiling override of the two-level chunk height
+// FPM_PYR2_OH (16 or 32): profiling override of the two-level chunk height (32 is faster at the sizes the engine
+// uses the kernel for: one Src7 source, levels 0-2, 11.3 vs 13.2 us; 16 at 43 sources, 217 vs 237 us)
+static const int kPyr2OH = [] {
     const char* e = getenv("FPM_PYR2_OH");
-    return e && atoi(e) == 32 ? 32 : 16;
+    return e && atoi(e) == 16 ? 16 : 32;
 }();
 // one launch for pyramid levels l+1 and l+2 of nimg images (the units shared over kPyrWGs workgroups as
 // launch_pyr_down; seg_chunks > 0: that many units per workgroup, so runs start mid-strip -- tests)
@@ -2159,15 +2161,17 @@ __device__ __forceinline__ int ft_tap_general(const uint8_t* FT, int ftw, int bx
     return (32 * h0 + fy * (h1 - h0) + 512) >> 10;
 }
 
+// this launch's live ROIs [slot_base, slot_base + count) (the host's rounds of whole candidates)
+__device__ __forceinline__ int roi_base(const RoiArgs& a) { return a.slot_base; }
 __device__ __forceinline__ void roi_slot(const RoiArgs& a, int slot, int& id, int& jj) {
-    const int ri = a.slot_base + slot;
+    const int ri = roi_base(a) + slot;
     const int li = ri / a.n3;
     jj = ri - li * a.n3;
     id = a.live[li];
 }
 
 __device__ __forceinline__ int roi_count(const RoiArgs& a) {
-    int rois = *a.live_count * a.n3 - a.slot_base;
+    int rois = *a.live_count * a.n3 - roi_base(a);
     return rois < 0 ? 0 : (rois > a.slot_cap ? a.slot_cap : rois);
 }
 
@@ -3528,9 +3532,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 
 // candidate step of :329-366 as a pure function of the state and the n3 records (k_cand_step, k_roi_eval, the
 // k_roi_small prologue)
+// next_nodes != nullptr: also loads the stepped candidate's next-layer node of angle jj into *next_nd (issued with the
+// child's own node, off the dependent-load chain of a k_roi_small prologue)
 __device__ __forceinline__ CandState cand_step_state(CandState s, int n3, const AngleNode* nodes, double thr, int W,
                                                      int H, int mark_reached0, const float* score, const int* mx,
-                                                     const int* my) {
+                                                     const int* my, const AngleNode* next_nodes = nullptr,
+                                                     int jj = 0, AngleNode* next_nd = nullptr) {
     int imax = 0;
     double big = -1;
     for (int k = 0; k < n3; ++k)
@@ -3541,6 +3548,7 @@ __device__ __forceinline__ CandState cand_step_state(CandState s, int n3, const 
     }
     const int child = s.node * n3 + imax;
     const AngleNode nd = nodes[child];
+    if (next_nodes) *next_nd = next_nodes[child * n3 + jj];
     const F2 sc = f2((W - 1) / 2.0f, (H - 1) / 2.0f);
     const F2 r0 = rotate_pt(f2(s.lt.x * 2, s.lt.y * 2), sc, nd.c, nd.s);   // :350-353
     const F2 pad = f2(r0.x - 3, r0.y - 3);
@@ -3620,21 +3628,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         roi_slot(a, slot, id, jj);
         const uint8_t* lvl = a.level + (size_t)(id / a.per_source) * a.level_stride;
         CandState st = a.state[id];
+        AngleNode nd;
         if (a.prev_rec) {   // the previous layer's candidate step (same inputs, same result in every thread)
             if (st.alive) {
                 const RoiRecord* r = a.prev_rec + (size_t)id * a.n3;
                 float score[3];
                 int mx[3], my[3];
                 for (int k = 0; k < a.n3; ++k) { score[k] = r[k].score; mx[k] = r[k].mx; my[k] = r[k].my; }
-                st = cand_step_state(st, a.n3, a.prev_nodes, a.prev_thr, a.prev_W, a.prev_H, 0, score, mx, my);
+                st = cand_step_state(st, a.n3, a.prev_nodes, a.prev_thr, a.prev_W, a.prev_H, 0, score, mx, my, a.nodes,
+                                     jj, &nd);
                 if (jj == 0 && tid == 0 && st.alive) atomicAdd(a.live_out_count, 1);   // live entering this layer
             }
             if (jj == 0 && tid == 0) a.state_out[id] = st;
             if (!st.alive) continue;   // uniform over the workgroup
+        } else {
+            nd = a.nodes[st.node * a.n3 + jj];
         }
         __syncthreads();
         {   // warpAffine tables of this ROI (getRotatedROI :1074-1090)
-            const AngleNode nd = a.nodes[st.node * a.n3 + jj];
             double M[6];
             roi_matrix(W, H, f2(st.lt.x * 2, st.lt.y * 2), nd.c, nd.s, M);
             for (int x = tid; x < RW; x += 256) {
@@ -4075,37 +4086,20 @@ __global__ __launch_bounds__(192) void k_roi_eval(RoiArgs a) {
     __shared__ RoiRecord recs[3];
     const int lane = threadIdx.x & 63, j = threadIdx.x >> 6;   // wave j <-> refinement angle j
     const int rois = roi_count(a);
-    const int c_lo = a.slot_base / a.n3, c_hi = (a.slot_base + rois) / a.n3;   // rounds hold whole candidates
+    const int base = roi_base(a);
+    const int c_lo = base / a.n3, c_hi = (base + rois) / a.n3;   // rounds hold whole candidates
     for (int li = c_lo + blockIdx.x; li < c_hi; li += gridDim.x) {
         const int id = a.live[li];
-        const int slot = li * a.n3 + j - a.slot_base;
+        const int slot = li * a.n3 + j - base;
         __syncthreads();   // previous candidate's records consumed
         eval_roi(a, slot, lane, blk_all[j], sc_all[j], a.rec + (size_t)id * a.n3 + j, &recs[j]);
         if (!a.step) continue;
         __syncthreads();
         if (threadIdx.x == 0) {   // TemplateMatcher.cpp:329-366
-            CandState s = a.state[id];
-            int imax = 0;
-            double big = -1;
-            for (int k = 0; k < a.n3; ++k)
-                if ((double)recs[k].score > big) { imax = k; big = recs[k].score; }
-            if ((double)recs[imax].score < a.thr) {   // :331-332
-                s.alive = 0;
-                a.state[id] = s;
-            } else {
-                const int child = s.node * a.n3 + imax;
-                const AngleNode nd = a.nodes[child];
-                const F2 sc = f2((a.W - 1) / 2.0f, (a.H - 1) / 2.0f);
-                const F2 r0 = rotate_pt(f2(s.lt.x * 2, s.lt.y * 2), sc, nd.c, nd.s);   // :350-353
-                const F2 pad = f2(r0.x - 3, r0.y - 3);
-                F2 p = f2((float)((double)recs[imax].mx + pad.x), (float)((double)recs[imax].my + pad.y));
-                p = rotate_pt(p, sc, nd.cn, nd.sn);
-                s.lt = p;          // :366
-                s.node = child;    // :363 (angle = node angle)
-                s.reached0 = a.mark_reached0;
-                a.state[id] = s;
-                a.live_out[atomicAdd(a.live_out_count, 1)] = id;
-            }
+            float score[3];
+            int mx[3], my[3];
+            for (int k = 0; k < a.n3; ++k) { score[k] = recs[k].score; mx[k] = recs[k].mx; my[k] = recs[k].my; }
+            cand_step_one(a, id, score, mx, my);
         }
     }
 }
@@ -4163,14 +4157,15 @@ static void launch_corr_regs(const RoiArgs& a, long items, size_t lds, hipStream
         // launch); at 8 / 12 k-steps the larger spills lose (136.5 -> 145.2, 301.1 -> 403.2 us)
         // ... and at 8 k-steps since the load addressing is scalar (136 VGPRs at 3 waves, 4 spilled at 4 waves: Src7
         // layer 1 107.7 -> 99.4 us per 43-source microbenchmark launch, profiles/r03_y)
-        if ((NK == 4 || NK == 8) && lds * 4 <= kLdsPerCu) {
+        if (NK == 4 && lds * 4 <= kLdsPerCu) {
             const int grid = (int)(items < 256 * 4 ? items : 256 * 4);
             hipLaunchKernelGGL((k_roi_corr<0, true, 4, NK, false, 1, true>), dim3(grid), dim3(256), lds, st, a);
             return;
         }
-        // at 12 k-steps the source rows staged by LDS-DMA (no staging VGPRs) make room for 4 waves per SIMD (Src7 layer 0
-        // at 43 sources: 269.8 -> 241.1 us, host-checked, profiles/r04/mb_r04e.txt)
-        if (NK == 12 && lds * 4 <= kLdsPerCu) {
+        // at 8 and 12 k-steps the source rows staged by LDS-DMA (no staging VGPRs) make room for 4 waves per SIMD
+        // (43 Src7 sources: layer 0 269.8 -> 241.1 us, profiles/r04/mb_r04e.txt; layer 1 103.0 -> 93.5 us,
+        // profiles/r04/mbl1_r04g.txt; host-checked)
+        if ((NK == 8 || NK == 12) && lds * 4 <= kLdsPerCu) {
             const int grid = (int)(items < 256 * 4 ? items : 256 * 4);
             hipLaunchKernelGGL((k_roi_corr<0, true, 4, NK, false, 1, true, true>), dim3(grid), dim3(256), lds, st, a);
             return;

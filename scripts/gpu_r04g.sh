@@ -22,3 +22,7 @@ MB_NSRC=43 MB_CORR=1 MB_W=2012 MB_H=1518 MB_P=2048 MB_TW=381 MB_TH=261 timeout -
 grep -E "prod|corrA8|check" gpurun_out/mbl1_$TAG.txt
 bash scripts/latency_trace.sh > gpurun_out/lat_$TAG.txt 2>&1 || exit $?
 head -40 gpurun_out/lat_$TAG.txt
+for rr in 1 2 4; do
+  FPM_REF_ROUNDS=$rr timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_rr${rr}_$TAG.json 2> gpurun_out/bench_rr${rr}_$TAG.err || exit $?
+  echo "rr $rr: $(python3 -c "import json,sys; d=json.loads(open('gpurun_out/bench_rr${rr}_$TAG.json').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d.get('roofline',{}).get('frac'))")"
+done

@@ -236,6 +236,48 @@ def test_refinement_rounds(gpu_matcher_factory, templates, monkeypatch, scratch_
     assert got == [o.match(s) for s in srcs]
 
 
+@pytest.mark.parametrize("prologue", ["0", "1"])
+def test_step_prologue_forms(gpu_matcher_factory, templates, monkeypatch, prologue):
+    """The candidate step of consecutive small layers in the next k_roi_small's prologue (FPM_STEP_PROLOGUE=1; by
+    default for batches of <= 2 sources; Src7 layers 5-3, dead candidates kept as holes of the live list until
+    k_cand_step compacts it after layer 3) and one k_cand_step launch per layer (FPM_STEP_PROLOGUE=0): a batch of three Src7 sources and one alone equal the oracle, result
+    fields and the per-layer live counts (the prologue counts the survivors entering each layer)."""
+    monkeypatch.setenv("FPM_STEP_PROLOGUE", prologue)
+    t = templates["Dst7"]
+    srcs = [synth.src7_scene(t, seed=31 + i)[0] for i in range(3)]
+    m = gpu_matcher_factory(max_pos=3, tolerance_angle=180.0, score=0.7)
+    assert m.learnPattern(t)
+    m.stage(srcs)
+    got = [[r.as_tuple() for r in rr] for rr in m.match_staged()]
+    o = oracle.OracleMatcher().set(max_pos=3, tolerance_angle=180.0, score=0.7)
+    o.learnPattern(t)
+    assert got == [o.match(s) for s in srcs]
+    gpu, orc, ostats, gstats = _run_both(m, srcs[0], t, max_pos=3, tolerance_angle=180.0, score=0.7)
+    assert gstats == ostats
+    assert_same_results(gpu, orc, f"src7 prologue={prologue}")
+    # a low score threshold keeps more candidates alive through the small layers (more holes, more survivors)
+    gpu, orc, ostats, gstats = _run_both(m, srcs[1], t, max_pos=8, tolerance_angle=180.0, score=0.3)
+    assert gstats == ostats
+    assert_same_results(gpu, orc, f"src7 prologue={prologue} score 0.3")
+
+
+@pytest.mark.parametrize("pyr2", ["0", "1"])
+def test_src7_batch_pyramid_forms(gpu_matcher_factory, templates, monkeypatch, pyr2):
+    """The search pyramid as one launch per level (FPM_PYR2=0) and as two levels per launch at every pair
+    (FPM_PYR2=1; by default only pairs whose input is small use it) on a batch of three Src7 sources: every search
+    equals the oracle."""
+    monkeypatch.setenv("FPM_PYR2", pyr2)
+    t = templates["Dst7"]
+    srcs = [synth.src7_scene(t, seed=41 + i)[0] for i in range(3)]
+    m = gpu_matcher_factory(max_pos=3, tolerance_angle=180.0, score=0.7)
+    assert m.learnPattern(t)
+    m.stage(srcs)
+    got = [[r.as_tuple() for r in rr] for rr in m.match_staged()]
+    o = oracle.OracleMatcher().set(max_pos=3, tolerance_angle=180.0, score=0.7)
+    o.learnPattern(t)
+    assert got == [o.match(s) for s in srcs]
+
+
 def test_constant_template(hip):
     t = np.full((40, 40), 90, np.uint8)
     s = synth.noise(200, 150, 90, 20, 12)
