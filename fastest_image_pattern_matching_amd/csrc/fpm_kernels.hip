@@ -409,10 +409,11 @@ void launch_pyr_down(const uint8_t* src, int sw, int sh, int sp, size_t s_img, u
                            dp, d_img, nimg, zero, nzero);
 }
 
-// ---- K1, two levels per launch (the product's search pyramid, round 4): a workgroup walks a strip of PD2_OWC columns
-// of level l+2 down in chunks.  A chunk first filters PD2_OHB rows of level l+1 over the PD2_OWB columns the strip's
-// level-(l+2) outputs read -- its own 2 PD2_OWC columns, stored to memory, plus 2 halo columns on each side that the
-// neighbouring strips own -- from a level-l window exactly as k_pyr_down_s does, and keeps them in an LDS ring after
+// ---- K1, two levels per launch (round 4; the engine uses it where a level pair's input is small): a workgroup walks a
+// strip of PD2_OWC columns of level l+2 down in chunks.  A chunk first filters PD2_OHB rows of level l+1 over the
+// PD2_OWB columns around the ones the strip's level-(l+2) outputs read -- its own 2 PD2_OWC columns, stored to memory,
+// plus halo columns on each side that the neighbouring strips own (4, of which 2 are read, so the own columns are whole
+// dword groups) -- from a level-l window exactly as k_pyr_down_s does, and keeps them in an LDS ring after
 // the 4 rows the previous chunk left there.  It then applies level l+1's own reflect-101 border to the ring (cv::pyrDown
 // pads its input, so a level-(l+1) column or row outside the image is a copy of one of its pixels, not a filtered
 // level-l value) and filters the PD2_OHB / 2 level-(l+2) rows the ring now completes.  Level l+1 is written once and
@@ -421,8 +422,8 @@ void launch_pyr_down(const uint8_t* src, int sw, int sh, int sp, size_t s_img, u
 // above would have carried (a 76-row level-l window instead of 68).  Same integer arithmetic as k_pyr_down on both
 // levels: exact.  The next chunk's 64 level-l rows are in flight while a chunk is filtered.
 constexpr int PD2_OWC = 64;                       // level-(l+2) columns per strip
-constexpr int PD2_OWB = 2 * PD2_OWC + 4;          // 132 level-(l+1) columns per strip (2-column halos)
-constexpr int PD2_GB = PD2_OWB / 4;               // 33 groups of 4 level-(l+1) columns
+constexpr int PD2_OWB = 2 * PD2_OWC + 8;          // 136 level-(l+1) columns per strip: 4-column halos (2 read), so
+constexpr int PD2_GB = PD2_OWB / 4;               // the own columns are groups 1 .. 32 of the 34 (dword stores)
 constexpr int PD2_BP = 136;                       // ring row pitch (bytes) = level-(l+1) horizontal-sum pitch (u16)
 // PD2_OHB: level-(l+1) rows per chunk (32: window 76 rows at a run start, 68 after it; ring 4 carried + 32 + 2 rows
 // reflected past the bottom row)
@@ -464,7 +465,7 @@ __global__ __launch_bounds__(256) void k_pyr_down2(const uint8_t* __restrict__ s
         uint8_t* bdst = b0 + (size_t)bz * b_img;
         uint8_t* cdst = c0 + (size_t)bz * c_img;
         const int cx0 = sx * PD2_OWC;
-        const int bx0 = 2 * cx0 - 2;   // ring column 0 <-> level-(l+1) column bx0
+        const int bx0 = 2 * cx0 - 4;   // ring column 0 <-> level-(l+1) column bx0
         const int ix0 = 4 * cx0 - 16;  // tin column 0 <-> level-l column ix0 (16-byte aligned)
         // level-l columns outside [0, sw) that the strip's in-image level-(l+1) columns read: reflect-101 patches
         const int xlo = 2 * max(bx0, 0) - 2, xhi = 2 * min(bx0 + PD2_OWB - 1, bw - 1) + 2;
@@ -509,10 +510,10 @@ __global__ __launch_bounds__(256) void k_pyr_down2(const uint8_t* __restrict__ s
             __syncthreads();
             if (k + 1 < k_end) issue(2 * PD2_OHB * (k + 1) + 2, 2 * PD2_OHB);
             // level l+1, horizontal [1 4 6 4 1] of the new window rows: ring column p = 4g + j reads level-l columns
-            // 2 (bx0 + p) - 2 .. + 4 = tin bytes 8g + 2j + 10 .. + 14
+            // 2 (bx0 + p) - 2 .. + 4 = tin bytes 8g + 2j + 6 .. + 10
             for (int i = tid; i < nrows * PD2_GB; i += 256) {
                 const int r = roff + i / PD2_GB, g = i % PD2_GB;
-                const uint32_t* wp = (const uint32_t*)&tin[r][8 * g + 8];
+                const uint32_t* wp = (const uint32_t*)&tin[r][8 * g + 4];
                 const uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2], w3 = wp[3];
                 const uint32_t h0 = __builtin_amdgcn_udot4(PD_K, __builtin_amdgcn_alignbyte(w1, w0, 2), (w1 >> 16) & 0xff, false);
                 const uint32_t h1 = __builtin_amdgcn_udot4(PD_K, w1, w2 & 0xff, false);
@@ -525,8 +526,8 @@ __global__ __launch_bounds__(256) void k_pyr_down2(const uint8_t* __restrict__ s
             }
             __syncthreads();
             // level l+1, vertical: rows by_first .. + nb - 1 into ring rows by - rb0; the strip's own in-image columns
-            // (ring columns 2 .. 2 PD2_OWC + 1) and rows (>= 32 k: the rebuilt carry rows belong to the chunk above)
-            // go to memory as 16-bit pairs
+            // (ring columns 4 .. 2 PD2_OWC + 3, groups 1 .. 32) and rows (>= 32 k: the rebuilt carry rows belong to the
+            // chunk above) go to memory as dwords
             for (int i = tid; i < nb * PD2_GB; i += 256) {
                 const int orow = i / PD2_GB, g = i - orow * PD2_GB;
                 fpm_u16x2 a01 = {128, 128}, a23 = {128, 128};
@@ -541,14 +542,13 @@ __global__ __launch_bounds__(256) void k_pyr_down2(const uint8_t* __restrict__ s
                 const int by = by_first + orow;
                 *(uint32_t*)&ring[by - rb0][4 * g] = packed;
                 if (by < PD2_OHB * k || by >= bh) continue;
-#pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
-                    const int p = 4 * g + 2 * hh, bx = bx0 + p;
-                    if (p < 2 || p >= 2 * PD2_OWC + 2 || bx >= bw) continue;
-                    uint8_t* d = bdst + (size_t)by * bpp + bx;
-                    const uint32_t pr = packed >> (16 * hh);
-                    if (bx + 1 < bw) *(uint16_t*)d = (uint16_t)pr;
-                    else d[0] = (uint8_t)pr;
+                const int bx = bx0 + 4 * g;
+                if (g < 1 || g > PD2_OWC / 2 || bx >= bw) continue;
+                uint8_t* d = bdst + (size_t)by * bpp + bx;
+                if (bx + 4 <= bw) {
+                    *(uint32_t*)d = packed;
+                } else {
+                    for (int j = 0; j < bw - bx; ++j) d[j] = (uint8_t)(packed >> (8 * j));
                 }
             }
             __syncthreads();
@@ -577,15 +577,15 @@ __global__ __launch_bounds__(256) void k_pyr_down2(const uint8_t* __restrict__ s
             const int lo = top ? 0 : PD2_OHB / 2 * k - 1;
             const int hi = bottom ? ch : min(ch, PD2_OHB / 2 * (k + 1) - 1);
             const int r_lo = 2 * lo - 2 - rb0, nr = 2 * (hi - lo) + 3;   // ring rows read
-            // horizontal: output cx0 + 4g + j reads ring columns 8g + 2j .. + 4
+            // horizontal: output cx0 + 4g + j reads ring columns 8g + 2j + 2 .. + 6
             for (int i = tid; i < nr * (PD2_OWC / 4); i += 256) {
                 const int r = r_lo + i / (PD2_OWC / 4), g = i % (PD2_OWC / 4);
                 const uint32_t* wp = (const uint32_t*)&ring[r][8 * g];
-                const uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2];
-                const uint32_t h0 = __builtin_amdgcn_udot4(PD_K, w0, w1 & 0xff, false);
-                const uint32_t h1 = __builtin_amdgcn_udot4(PD_K, __builtin_amdgcn_alignbyte(w1, w0, 2), (w1 >> 16) & 0xff, false);
-                const uint32_t h2 = __builtin_amdgcn_udot4(PD_K, w1, w2 & 0xff, false);
-                const uint32_t h3 = __builtin_amdgcn_udot4(PD_K, __builtin_amdgcn_alignbyte(w2, w1, 2), (w2 >> 16) & 0xff, false);
+                const uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2], w3 = wp[3];
+                const uint32_t h0 = __builtin_amdgcn_udot4(PD_K, __builtin_amdgcn_alignbyte(w1, w0, 2), (w1 >> 16) & 0xff, false);
+                const uint32_t h1 = __builtin_amdgcn_udot4(PD_K, w1, w2 & 0xff, false);
+                const uint32_t h2 = __builtin_amdgcn_udot4(PD_K, __builtin_amdgcn_alignbyte(w2, w1, 2), (w2 >> 16) & 0xff, false);
+                const uint32_t h3 = __builtin_amdgcn_udot4(PD_K, w2, w3 & 0xff, false);
                 uint2 o;
                 o.x = h0 | (h1 << 16);
                 o.y = h2 | (h3 << 16);
@@ -2139,6 +2139,44 @@ __device__ __forceinline__ void lds_taps16(const uint32_t off[4], int v[4][4]) {
                  : "memory");
 }
 
+// The same 16 taps read straight into the packed 16-bit lanes bilerp_row4 builds with byte permutes: ds_read_u8_d16
+// (low half, zero-extended) and ds_read_u8_d16_hi (high half) give a02 = (v0, v2) and a13 = (v1, v3) per pixel, 8
+// VALU fewer per row (round 4).  The two halves of a register are written by two reads in flight together; LDS
+// returns in order, so both land.
+template <int PITCH>
+__device__ __forceinline__ void lds_taps16_d16(const uint32_t off[4], uint32_t a02[4], uint32_t a13[4]) {
+    asm volatile("ds_read_u8_d16 %0, %8\n\tds_read_u8_d16_hi %0, %8 offset:%12\n\t"
+                 "ds_read_u8_d16 %1, %8 offset:1\n\tds_read_u8_d16_hi %1, %8 offset:%13\n\t"
+                 "ds_read_u8_d16 %2, %9\n\tds_read_u8_d16_hi %2, %9 offset:%12\n\t"
+                 "ds_read_u8_d16 %3, %9 offset:1\n\tds_read_u8_d16_hi %3, %9 offset:%13\n\t"
+                 "ds_read_u8_d16 %4, %10\n\tds_read_u8_d16_hi %4, %10 offset:%12\n\t"
+                 "ds_read_u8_d16 %5, %10 offset:1\n\tds_read_u8_d16_hi %5, %10 offset:%13\n\t"
+                 "ds_read_u8_d16 %6, %11\n\tds_read_u8_d16_hi %6, %11 offset:%12\n\t"
+                 "ds_read_u8_d16 %7, %11 offset:1\n\tds_read_u8_d16_hi %7, %11 offset:%13\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(a02[0]), "=&v"(a13[0]), "=&v"(a02[1]), "=&v"(a13[1]), "=&v"(a02[2]), "=&v"(a13[2]),
+                   "=&v"(a02[3]), "=&v"(a13[3])
+                 : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "i"(PITCH), "i"(PITCH + 1)
+                 : "memory");
+}
+// bilerp_row4 on taps already packed as (v0, v2) / (v1, v3) lanes
+__device__ __forceinline__ uint32_t bilerp_row4p(const uint32_t a02[4], const uint32_t a13[4], const int fx[4],
+                                                 const int fy[4]) {
+    uint32_t r[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const fpm_u16x2v d = __builtin_bit_cast(fpm_u16x2v, a13[u]) - __builtin_bit_cast(fpm_u16x2v, a02[u]);
+        const fpm_u16x2v b = __builtin_bit_cast(fpm_u16x2v, a02[u]) << (fpm_u16x2v)5;
+        uint32_t h;
+        asm("v_pk_mad_u16 %0, %1, %2, %3 op_sel_hi:[0,1,1]"
+            : "=v"(h) : "v"(fx[u]), "v"(__builtin_bit_cast(uint32_t, d)), "v"(__builtin_bit_cast(uint32_t, b)));
+        const uint32_t wy = (uint32_t)mad24(fy[u], 64 * 0x10000 - 64, 64 * 32);   // (64 (32 - fy), 64 fy)
+        r[u] = __builtin_amdgcn_udot2(__builtin_bit_cast(fpm_u16x2v, h), __builtin_bit_cast(fpm_u16x2v, wy), 64u * 512u,
+                                      false);
+    }
+    return __builtin_amdgcn_perm(r[1], r[0], 0x0c0c0602u) | __builtin_amdgcn_perm(r[3], r[2], 0x06020c0cu);
+}
+
 // One bilinear ROI pixel from a staged footprint, BORDER_CONSTANT(0) rules of remapBilinear (general path).
 __device__ __forceinline__ int ft_tap_general(const uint8_t* FT, int ftw, int bxa, int by0, int W, int H, int X, int Y) {
     const int sx = sat_s16(X >> kInterBits), sy = sat_s16(Y >> kInterBits);
@@ -2607,7 +2645,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t box_rsrc(const uint8_t* base) 
 //  * per task, not per ROI: the lane's table offsets, the column mask and the row masks (the three ROIs share them);
 //  * the interior pixel: the tables' 16-fraction-bit scale (kTabShift) puts the integer tap coordinate in the high
 //    half-word, read by SDWA word selects, and the 16 tap reads and their wait are one asm statement.
-template <int WPE, int PITCH = 64, int STG = 0>
+template <int WPE, int PITCH = 64, int STG = 0, int D16 = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_warp3(RoiArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t ft_all[4 * ROI_FT + 16];
     constexpr int ftw = PITCH;   // footprint row pitch
@@ -2731,7 +2769,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 for (int i = 0; i < 4; ++i) {
                     const uint32_t x0r = X0r[i] + xo, y0r = Y0r[i] + yo;
                     uint32_t off[4];
-                    int fxv[4], fyv[4], v[4][4];
+                    int fxv[4], fyv[4];
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         const uint32_t sxv = x0r + adv[u], syv = y0r + bdv[u];
@@ -2739,8 +2777,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                         fxv[u] = (int)((sxv >> kTapShift) & (kInterTab - 1));
                         fyv[u] = (int)((syv >> kTapShift) & (kInterTab - 1));
                     }
-                    lds_taps16<ftw>(off, v);
-                    const uint32_t pk = bilerp_row4(v, fxv, fyv);
+                    uint32_t pk;
+                    if (D16) {
+                        uint32_t a02[4], a13[4];
+                        lds_taps16_d16<ftw>(off, a02, a13);
+                        pk = bilerp_row4p(a02, a13, fxv, fyv);
+                    } else {
+                        int v[4][4];
+                        lds_taps16<ftw>(off, v);
+                        pk = bilerp_row4(v, fxv, fyv);
+                    }
                     if (ry0 + lr + 8 * i <= ry1) st_at<uint32_t>(tile, st_lane + 256u * i, (pk & colmask) ^ kRoiFlip);
                 }
                 continue;
