@@ -2095,7 +2095,9 @@ __device__ __forceinline__ int bilerp24(const int v[4], int fx, int fy) {
 // <= 8160; lane arithmetic mod 2^16, exact since the true value fits), fx taken from the low half of its register by
 // op_sel (no splat), the vertical pass as one u16 dot product with the weights (64 (32 - fy), 64 fy) plus 64 * 512:
 // 64 * (32 h0 + fy (h1 - h0) + 512) < 2^24, so the result byte is bits 16..23 and two byte permutes + one bitwise op
-// pack the row.  Taps must be zero-extended bytes (lds_taps16).
+// pack the row.  Taps must be zero-extended bytes (lds_taps16).  (Reading the taps straight into the lane pairs with
+// ds_read_u8_d16 / _d16_hi does not work on gfx950: with SRAM ECC the D16 loads zero the other half of the register
+// instead of preserving it -- found by the GPU suite, round 4 -- so the two halves would need an OR: no saving.)
 typedef unsigned short fpm_u16x2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t bilerp_row4(const int v[4][4], const int fx[4], const int fy[4]) {
     uint32_t r[4];
@@ -2137,44 +2139,6 @@ __device__ __forceinline__ void lds_taps16(const uint32_t off[4], int v[4][4]) {
                    "=&v"(v[3][0]), "=&v"(v[3][1]), "=&v"(v[3][2]), "=&v"(v[3][3])
                  : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "i"(PITCH), "i"(PITCH + 1)
                  : "memory");
-}
-
-// The same 16 taps read straight into the packed 16-bit lanes bilerp_row4 builds with byte permutes: ds_read_u8_d16
-// (low half, zero-extended) and ds_read_u8_d16_hi (high half) give a02 = (v0, v2) and a13 = (v1, v3) per pixel, 8
-// VALU fewer per row (round 4).  The two halves of a register are written by two reads in flight together; LDS
-// returns in order, so both land.
-template <int PITCH>
-__device__ __forceinline__ void lds_taps16_d16(const uint32_t off[4], uint32_t a02[4], uint32_t a13[4]) {
-    asm volatile("ds_read_u8_d16 %0, %8\n\tds_read_u8_d16_hi %0, %8 offset:%12\n\t"
-                 "ds_read_u8_d16 %1, %8 offset:1\n\tds_read_u8_d16_hi %1, %8 offset:%13\n\t"
-                 "ds_read_u8_d16 %2, %9\n\tds_read_u8_d16_hi %2, %9 offset:%12\n\t"
-                 "ds_read_u8_d16 %3, %9 offset:1\n\tds_read_u8_d16_hi %3, %9 offset:%13\n\t"
-                 "ds_read_u8_d16 %4, %10\n\tds_read_u8_d16_hi %4, %10 offset:%12\n\t"
-                 "ds_read_u8_d16 %5, %10 offset:1\n\tds_read_u8_d16_hi %5, %10 offset:%13\n\t"
-                 "ds_read_u8_d16 %6, %11\n\tds_read_u8_d16_hi %6, %11 offset:%12\n\t"
-                 "ds_read_u8_d16 %7, %11 offset:1\n\tds_read_u8_d16_hi %7, %11 offset:%13\n\t"
-                 "s_waitcnt lgkmcnt(0)"
-                 : "=&v"(a02[0]), "=&v"(a13[0]), "=&v"(a02[1]), "=&v"(a13[1]), "=&v"(a02[2]), "=&v"(a13[2]),
-                   "=&v"(a02[3]), "=&v"(a13[3])
-                 : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "i"(PITCH), "i"(PITCH + 1)
-                 : "memory");
-}
-// bilerp_row4 on taps already packed as (v0, v2) / (v1, v3) lanes
-__device__ __forceinline__ uint32_t bilerp_row4p(const uint32_t a02[4], const uint32_t a13[4], const int fx[4],
-                                                 const int fy[4]) {
-    uint32_t r[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const fpm_u16x2v d = __builtin_bit_cast(fpm_u16x2v, a13[u]) - __builtin_bit_cast(fpm_u16x2v, a02[u]);
-        const fpm_u16x2v b = __builtin_bit_cast(fpm_u16x2v, a02[u]) << (fpm_u16x2v)5;
-        uint32_t h;
-        asm("v_pk_mad_u16 %0, %1, %2, %3 op_sel_hi:[0,1,1]"
-            : "=v"(h) : "v"(fx[u]), "v"(__builtin_bit_cast(uint32_t, d)), "v"(__builtin_bit_cast(uint32_t, b)));
-        const uint32_t wy = (uint32_t)mad24(fy[u], 64 * 0x10000 - 64, 64 * 32);   // (64 (32 - fy), 64 fy)
-        r[u] = __builtin_amdgcn_udot2(__builtin_bit_cast(fpm_u16x2v, h), __builtin_bit_cast(fpm_u16x2v, wy), 64u * 512u,
-                                      false);
-    }
-    return __builtin_amdgcn_perm(r[1], r[0], 0x0c0c0602u) | __builtin_amdgcn_perm(r[3], r[2], 0x06020c0cu);
 }
 
 // One bilinear ROI pixel from a staged footprint, BORDER_CONSTANT(0) rules of remapBilinear (general path).
@@ -2645,7 +2609,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t box_rsrc(const uint8_t* base) 
 //  * per task, not per ROI: the lane's table offsets, the column mask and the row masks (the three ROIs share them);
 //  * the interior pixel: the tables' 16-fraction-bit scale (kTabShift) puts the integer tap coordinate in the high
 //    half-word, read by SDWA word selects, and the 16 tap reads and their wait are one asm statement.
-template <int WPE, int PITCH = 64, int STG = 0, int D16 = 1>
+template <int WPE, int PITCH = 64, int STG = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_warp3(RoiArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t ft_all[4 * ROI_FT + 16];
     constexpr int ftw = PITCH;   // footprint row pitch
@@ -2777,16 +2741,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                         fxv[u] = (int)((sxv >> kTapShift) & (kInterTab - 1));
                         fyv[u] = (int)((syv >> kTapShift) & (kInterTab - 1));
                     }
-                    uint32_t pk;
-                    if (D16) {
-                        uint32_t a02[4], a13[4];
-                        lds_taps16_d16<ftw>(off, a02, a13);
-                        pk = bilerp_row4p(a02, a13, fxv, fyv);
-                    } else {
-                        int v[4][4];
-                        lds_taps16<ftw>(off, v);
-                        pk = bilerp_row4(v, fxv, fyv);
-                    }
+                    int v[4][4];
+                    lds_taps16<ftw>(off, v);
+                    const uint32_t pk = bilerp_row4(v, fxv, fyv);
                     if (ry0 + lr + 8 * i <= ry1) st_at<uint32_t>(tile, st_lane + 256u * i, (pk & colmask) ^ kRoiFlip);
                 }
                 continue;
@@ -3637,7 +3594,9 @@ size_t roi_small_lds(int tw, int th) { return (size_t)small_layout(tw, th).total
 // MODE (profiling ablations in scripts/roi_microbench.hip; the product uses 0): 1 = tables + sampling only,
 // 2 = + row / window sums, 3 = + bands without the fold, 5 = full with byte-gather taps, 9 = full with per-phase
 // s_memtime stamps (a.stamps)
-template <int MODE, int WPE = 3>
+// PROL: the previous layer's candidate step in the prologue (a.prev_rec set; a separate instantiation: its registers
+// would cost the plain form spills, 11 -> 33 VGPRs at 4 waves, k_roi_small 178 -> 207 us per 43-source pass)
+template <int MODE, int WPE = 3, bool PROL = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_small(RoiArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tw = a.tw, th = a.th, RW = tw + 6, RH = th + 6, W = a.W, H = a.H;
@@ -3675,7 +3634,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const uint8_t* lvl = a.level + (size_t)(id / a.per_source) * a.level_stride;
         CandState st = a.state[id];
         AngleNode nd;
-        if (a.prev_rec) {   // the previous layer's candidate step (same inputs, same result in every thread)
+        if (PROL) {   // the previous layer's candidate step (same inputs, same result in every thread)
             if (st.alive) {
                 const RoiRecord* r = a.prev_rec + (size_t)id * a.n3;
                 float score[3];
@@ -4276,6 +4235,11 @@ void launch_roi_small(const RoiArgs& a, hipStream_t st) {
     const int grid = a.slot_cap < 8192 ? a.slot_cap : 8192;
     // 4 waves per SIMD where 4 workgroups' LDS fit a CU (Src7 layers 5 and 4: 46.8 -> 42.4 and 54.7 -> 47.4 us per
     // 43-source launch despite a 48-byte spill; 5 waves spill 176 bytes and measured slower), else 3
+    if (a.prev_rec) {   // small batches only (the engine's rule): occupancy matters less than spills (3 vs 28 VGPRs)
+        ensure_lds_attr((const void*)k_roi_small<0, 3, true>, lds);
+        hipLaunchKernelGGL((k_roi_small<0, 3, true>), dim3(grid), dim3(256), lds, st, a);
+        return;
+    }
     if (lds * 4 <= kLdsPerCu) {
         ensure_lds_attr((const void*)k_roi_small<0, 4>, lds);
         hipLaunchKernelGGL((k_roi_small<0, 4>), dim3(grid), dim3(256), lds, st, a);

@@ -20,3 +20,5 @@ for oh in 16 32; do
   FPM_PYR2_OH=$oh MB_NSRC=43 MB_SHORT=1 timeout -k 10 240 ./build/roi_mb 10 > gpurun_out/mb${oh}_$TAG.txt 2>&1 || exit $?
   echo "== OH $oh"; grep -E "pyr" gpurun_out/mb${oh}_$TAG.txt
 done
+FPM_TOP_FUSED=1 bash scripts/latency_trace.sh > gpurun_out/lat_topfused_$TAG.txt 2>&1 || exit $?
+head -24 gpurun_out/lat_topfused_$TAG.txt

@@ -286,8 +286,7 @@ int main(int argc, char** argv) {
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<6>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 6w");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 7w p68");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 1>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 7w p68 r03stg");
-            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 0>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 7w p68 no d16");
-            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<8, 68, 0>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 8w p68 d16");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<8, 68, 0>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 8w p68");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 64, 1>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 7w p64 r03stg");
             {   // every warp3 form writes the same ROI bytes as the round-3 form
                 const size_t nb = (size_t)a.slot_cap * a.roi_stride;
@@ -308,7 +307,6 @@ int main(int argc, char** argv) {
                 run_cmp([&] { hipLaunchKernelGGL((k_roi_warp3<7>), dim3(grid3), dim3(256), 0, 0, a); }, "p64");
                 run_cmp([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0>), dim3(grid3), dim3(256), 0, 0, a); }, "p68");
                 run_cmp([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 1>), dim3(grid3), dim3(256), 0, 0, a); }, "p68 r03stg");
-                run_cmp([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 0>), dim3(grid3), dim3(256), 0, 0, a); }, "p68 no d16");
                 run_cmp([&] { launch_roi_warp(a, 0); }, "product");
             }
 
