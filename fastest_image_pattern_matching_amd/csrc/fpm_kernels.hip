@@ -2609,7 +2609,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t box_rsrc(const uint8_t* base) 
 //  * per task, not per ROI: the lane's table offsets, the column mask and the row masks (the three ROIs share them);
 //  * the interior pixel: the tables' 16-fraction-bit scale (kTabShift) puts the integer tap coordinate in the high
 //    half-word, read by SDWA word selects, and the 16 tap reads and their wait are one asm statement.
-template <int WPE, int PITCH = 64, int STG = 0>
+// ABL (profiling ablations, scripts/roi_microbench.hip; the product uses 0): 1 = no footprint staging, 2 = interior
+// taps read but not interpolated (XOR-folded), 3 = interior addressing only (no tap reads), 4 = no ROI stores (a
+// never-true store kept), 5 = no interior rows (staging, tables and border tiles only)
+template <int WPE, int PITCH = 64, int STG = 0, int ABL = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_warp3(RoiArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t ft_all[4 * ROI_FT + 16];
     constexpr int ftw = PITCH;   // footprint row pitch
@@ -2633,6 +2636,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const size_t tab_stride = (size_t)2 * (a.tabw + a.tabh);
     const uint32_t pitch_v = __builtin_amdgcn_readfirstlane(ftw);   // the LDS pitch as an SDWA operand
     auto stage = [&](int wpr, int fth, const uint8_t* gsrc) {
+        if (ABL == 1) return;
         if (STG == 1) {
             stage_footprint32<12, PITCH>(FT, wpr, fth, gsrc, P, lane);
             return;
@@ -2741,10 +2745,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                         fxv[u] = (int)((sxv >> kTapShift) & (kInterTab - 1));
                         fyv[u] = (int)((syv >> kTapShift) & (kInterTab - 1));
                     }
-                    int v[4][4];
-                    lds_taps16<ftw>(off, v);
-                    const uint32_t pk = bilerp_row4(v, fxv, fyv);
-                    if (ry0 + lr + 8 * i <= ry1) st_at<uint32_t>(tile, st_lane + 256u * i, (pk & colmask) ^ kRoiFlip);
+                    if (ABL == 5) continue;
+                    uint32_t pk;
+                    if (ABL == 3) {
+                        pk = off[0] ^ off[1] ^ off[2] ^ off[3] ^ (uint32_t)(fxv[0] + fxv[1] + fxv[2] + fxv[3]) ^
+                             (uint32_t)(fyv[0] + fyv[1] + fyv[2] + fyv[3]);
+                    } else {
+                        int v[4][4];
+                        lds_taps16<ftw>(off, v);
+                        if (ABL == 2) {
+                            pk = 0;
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) pk ^= (uint32_t)(v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3]) << (8 * u);
+                        } else {
+                            pk = bilerp_row4(v, fxv, fyv);
+                        }
+                    }
+                    if (ABL == 4 ? pk == 0x9e3779b9u && c0 < 0 : ry0 + lr + 8 * i <= ry1)
+                        st_at<uint32_t>(tile, st_lane + 256u * i, (pk & colmask) ^ kRoiFlip);
                 }
                 continue;
             }

@@ -287,6 +287,11 @@ int main(int argc, char** argv) {
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 7w p68");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 1>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 7w p68 r03stg");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<8, 68, 0>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 8w p68");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 1>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 abl no staging");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 2>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 abl no lerp");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 3>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 abl addr only");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 4>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 abl no stores");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 5>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 abl no interior");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 64, 1>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 7w p64 r03stg");
             {   // every warp3 form writes the same ROI bytes as the round-3 form
                 const size_t nb = (size_t)a.slot_cap * a.roi_stride;

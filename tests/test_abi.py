@@ -85,6 +85,8 @@ def test_product_library_holds_no_measurement_kernels():
             assert args[0] == "0", k
         if k.startswith("fpm::k_roi_warp<"):
             assert args[1] == "0", k
+        if k.startswith("fpm::k_roi_warp3<"):
+            assert args[3] == "0", k
 
 
 def test_product_switches_are_result_neutral():
