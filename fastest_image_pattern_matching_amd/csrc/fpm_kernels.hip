@@ -2611,8 +2611,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t box_rsrc(const uint8_t* base) 
 //    half-word, read by SDWA word selects, and the 16 tap reads and their wait are one asm statement.
 // ABL (profiling ablations, scripts/roi_microbench.hip; the product uses 0): 1 = no footprint staging, 2 = interior
 // taps read but not interpolated (XOR-folded), 3 = interior addressing only (no tap reads), 4 = no ROI stores (a
-// never-true store kept), 5 = no interior rows (staging, tables and border tiles only)
-template <int WPE, int PITCH = 64, int STG = 0, int ABL = 0>
+// never-true store kept), 5 = no interior rows (staging, tables and border tiles only), 6 = as 5 without staging,
+// 7 = as 6 without the table loads, 8 = as 7 without border tiles (descriptor loads and the task loop only)
+// PFT: the next ROI's tables are requested before this ROI's rows are sampled (16 more VGPRs)
+template <int WPE, int PITCH = 64, int STG = 0, int ABL = 0, bool PFT = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_warp3(RoiArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t ft_all[4 * ROI_FT + 16];
     constexpr int ftw = PITCH;   // footprint row pitch
@@ -2636,7 +2638,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const size_t tab_stride = (size_t)2 * (a.tabw + a.tabh);
     const uint32_t pitch_v = __builtin_amdgcn_readfirstlane(ftw);   // the LDS pitch as an SDWA operand
     auto stage = [&](int wpr, int fth, const uint8_t* gsrc) {
-        if (ABL == 1) return;
+        if (ABL == 1 || ABL >= 6) return;
         if (STG == 1) {
             stage_footprint32<12, PITCH>(FT, wpr, fth, gsrc, P, lane);
             return;
@@ -2695,8 +2697,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                        oY = oX + 4u * a.tabh;
         const int nvalid = RW - c0;
         const uint32_t colmask = nvalid >= 4 ? 0xffffffffu : (1u << (8 * max(nvalid, 0))) - 1u;
-        int4 tA, tB, tX, tY;
+        int4 tA, tB, tX, tY, nA, nB, nX, nY;
+        bool nxt_ok = false;   // (PFT) nA .. nY hold the next non-empty ROI's tables
+        auto load_next = [&](int slot_) {
+            const int32_t* tb = a.tab + (size_t)slot_ * tab_stride;
+            nA = ld_at<int4>(tb, oA);
+            nB = ld_at<int4>(tb, oB);
+            nX = ld_at<int4>(tb, oX);
+            nY = ld_at<int4>(tb, oY);
+        };
         auto load_tabs = [&](int slot_) {
+            if (ABL >= 7) {
+                tA = tB = tX = tY = make_int4(slot_, 0, 0, 0);
+                return;
+            }
             const int32_t* tb = a.tab + (size_t)slot_ * tab_stride;
             tA = ld_at<int4>(tb, oA);
             tB = ld_at<int4>(tb, oB);
@@ -2722,13 +2736,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 if ((flags & kTileAny) && in_lds) stage(wp[j], fh[j], lvl + (size_t)by0 * P + bxa);
                 wave_sync();
             }
-            if (j > 0) load_tabs(slot);
+            if (j > 0 && (flags & kTileAny)) {   // (an empty tile needs no tables)
+                if (PFT && nxt_ok) {
+                    tA = nA; tB = nB; tX = nX; tY = nY;
+                } else {
+                    load_tabs(slot);
+                }
+            }
+            nxt_ok = false;
+            if (PFT && j + 1 < 3 && (fl[j + 1] & kTileAny)) {
+                load_next(slot + 1);
+                nxt_ok = true;
+            }
             const uint32_t adv[4] = {(uint32_t)tA.x, (uint32_t)tA.y, (uint32_t)tA.z, (uint32_t)tA.w};
             const uint32_t bdv[4] = {(uint32_t)tB.x, (uint32_t)tB.y, (uint32_t)tB.z, (uint32_t)tB.w};
             const uint32_t X0r[4] = {(uint32_t)tX.x, (uint32_t)tX.y, (uint32_t)tX.z, (uint32_t)tX.w};
             const uint32_t Y0r[4] = {(uint32_t)tY.x, (uint32_t)tY.y, (uint32_t)tY.z, (uint32_t)tY.w};
             uint8_t* tile = a.roi + (size_t)slot * a.roi_stride + ((size_t)rem << 10);
             if (c0 > cx1) continue;
+            if (!(flags & kTileAny)) {
+                // the tile's footprint lies entirely outside the level: every tap is BORDER_CONSTANT 0, so the tile is
+                // zeros (stored flipped) -- no taps (18 % of the layer-0 tiles of the Src7 bench: ROIs reaching past
+                // the image; they took the per-pixel border path before, round 4)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (ry0 + lr + 8 * i <= ry1) st_at<uint32_t>(tile, st_lane + 256u * i, kRoiFlip);
+                continue;
+            }
+            if (ABL == 8 && !((flags & kTileInterior) && in_lds)) {
+                if (X0r[0] == 0x9e3779b9u) st_at<uint32_t>(tile, st_lane, adv[0]);
+                continue;
+            }
             if ((flags & kTileInterior) && in_lds) {
                 // folded coordinates: (X0 + adv + xo) >> 16 is the tap's LDS byte column (footprint base included),
                 // (Y0 + bdv + yo) >> 16 its footprint row; both lie in [0, 2^15), so the high half-words are exact
@@ -2745,7 +2783,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                         fxv[u] = (int)((sxv >> kTapShift) & (kInterTab - 1));
                         fyv[u] = (int)((syv >> kTapShift) & (kInterTab - 1));
                     }
-                    if (ABL == 5) continue;
+                    if (ABL >= 5) continue;
                     uint32_t pk;
                     if (ABL == 3) {
                         pk = off[0] ^ off[1] ^ off[2] ^ off[3] ^ (uint32_t)(fxv[0] + fxv[1] + fxv[2] + fxv[3]) ^
@@ -2940,16 +2978,21 @@ __device__ __forceinline__ void band_mfma_regs(const fpm_v4i* A, const uint8_t* 
 // item's staging (after the loads of its rows are issued, so waiting for those loads does not wait for these stores)
 // DMA (register-A form, no row prefetch): the item's ROI rows go global -> LDS by LDS-DMA (one global_load_lds_dwordx4
 // per row and wave, the scratch already flipped): no staging registers and no VALU per staged row
-template <int MODE, bool GA, int WPE, int NK = 0, bool PFR = true, int RS = 1, bool SE = false, bool DMA = false>
+// DB (with DMA): two row buffers; the next item's rows are issued into the other buffer once this item's are in LDS,
+// so an item waits for rows requested one item earlier (the LDS holds a second kBandSrc x SBp buffer after the rest)
+template <int MODE, bool GA, int WPE, int NK = 0, bool PFR = true, int RS = 1, bool SE = false, bool DMA = false,
+          bool DB = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_corr(RoiArgs a) {
     static_assert(!DMA || (NK > 0 && !PFR), "LDS-DMA staging replaces the register staging of the register-A form");
+    static_assert(!DB || DMA, "the double buffer is filled by LDS-DMA");
     static_assert(NK == 0 || (GA && MODE != 3), "the register-A form stages no template rows");
     static_assert(!SE || NK > 0, "the staged epilogue is flushed in the register-A form's staging phase");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tw = a.tw, th = a.th, RW = tw + 6;
     const int SBp = a.roi_pitch;
     const int TBp = tmpl_lds_pitch(a.tp8);
-    uint8_t* SB = smem;                                        // kBandSrc rows x SBp, bytes ^ 0x80
+    uint8_t* const SB0 = smem;                                 // kBandSrc rows x SBp, bytes ^ 0x80
+    uint8_t* SB = SB0;
     uint8_t* TB = SB + (size_t)kBandSrc * SBp;                 // kBandRows template rows (i8) x TBp (!GA)
     uint32_t* rall = (uint32_t*)(TB + (GA ? 0 : (size_t)kBandRows * TBp)); // full-row sums of I
     uint32_t* rallq = rall + kBandSrc;                         // full-row sums of I^2
@@ -2957,6 +3000,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     uint32_t* wq = wi + kBandSrc * 7;                          // [row][dx] window sums of I^2
     uint32_t* lts = wq + kBandSrc * 7;                         // the band's template-row sums (16-byte aligned)
     uint32_t* rsb = lts + 2 * kMmaRows;                        // (SE) the band's [rb][49] row results (16-byte aligned)
+    uint8_t* const SB1 = (uint8_t*)(((uintptr_t)(rsb + 2 * kMmaRows * 49) + 64 + 15) & ~(uintptr_t)15);   // (DB)
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int nband = (th + kBandRows - 1) / kBandRows;
     const int rois = roi_count(a), items = rois * nband;
@@ -3012,10 +3056,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         for (int i = tid; i < n16; i += 256) *(uint4*)(dst + 4 * i) = *(const uint4*)(rsb + 4 * i);
         if (tid < (nw & 3)) dst[4 * n16 + tid] = rsb[4 * n16 + tid];
     };
+    // (DMA) item it's ROI rows wv + 4i -> buffer buf: SGPR row address, the lane's 16-byte chunk of it (lanes past the
+    // ROI width idle: the LDS chunks past the ROI are multiplied by the template's zero padding and never summed)
+    auto dma_rows = [&](int it, uint8_t* buf) {
+        const int bd = it / rois, sl = it - bd * rois;
+        const int T0n = bd * kBandRows, nsn = min(kBandRows, th - T0n) + 6;
+        const uint8_t* rsrc = a.roi + (size_t)sl * a.roi_stride;
+        const uint32_t lane_off = ((uint32_t)(lane >> 1) << 10) + 16u * (uint32_t)(lane & 1);
+        const int wvu = __builtin_amdgcn_readfirstlane(wv);
+        const bool in_roi = lane < 2 * txn;
+#pragma unroll
+        for (int i = 0; i < kStageRows; ++i) {
+            const int r = wvu + 4 * i;
+            if (r < nsn && in_roi) {
+                const int R = T0n + r;
+                const uint8_t* gp = rsrc + ((size_t)((R >> 5) * txn) << 10) + (R & 31) * ROI_T + lane_off;
+                const uint32_t ldsa = __builtin_amdgcn_readfirstlane(lds_offset_of(buf + (size_t)r * SBp));
+                uint32_t keep;
+                asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                             "s_mov_b32 m0, %0"
+                             : "=&s"(keep) : "v"(gp), "s"(ldsa) : "memory");
+            }
+        }
+    };
     for (int item = it_lo; item < it_hi; item += it_step) {
         int slot, band;
         if (NK > 0) { band = item / rois; slot = item - band * rois; }
         else { slot = item / nband; band = item - slot * nband; }
+        SB = DB && ((item - it_lo) & 1) ? SB1 : SB0;
         const int T0 = band * kBandRows, rb = min(kBandRows, th - T0), nsrc = rb + 6;
         __syncthreads();   // previous item done with SB / rall / wi
         if (RS == 0 && tid < kBandSrc) { rall[tid] = 0; rallq[tid] = 0; }
@@ -3023,25 +3091,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             // this item's rows (loaded during the previous item) ^ 0x80 into LDS; this wave's A fragments when the
             // band changes (workgroup-uniform); then the next item's row loads
             const bool in_roi = lane < 2 * txn;
-            if (DMA) {
-                // rows wv + 4i of the item: SGPR row address, the lane's 16-byte chunk of it (lanes past the ROI width
-                // idle: the LDS chunks past the ROI are multiplied by the template's zero padding and never summed)
-                const uint8_t* rsrc = a.roi + (size_t)slot * a.roi_stride;
-                const uint32_t lane_off = ((uint32_t)(lane >> 1) << 10) + 16u * (uint32_t)(lane & 1);
-                const int wvu = __builtin_amdgcn_readfirstlane(wv);
-#pragma unroll
-                for (int i = 0; i < kStageRows; ++i) {
-                    const int r = wvu + 4 * i;
-                    if (r < nsrc && in_roi) {
-                        const int R = T0 + r;
-                        const uint8_t* g = rsrc + ((size_t)((R >> 5) * txn) << 10) + (R & 31) * ROI_T + lane_off;
-                        const uint32_t ldsa = __builtin_amdgcn_readfirstlane(lds_offset_of(SB + (size_t)r * SBp));
-                        uint32_t keep;
-                        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
-                                     "s_mov_b32 m0, %0"
-                                     : "=&s"(keep) : "v"(g), "s"(ldsa) : "memory");
-                    }
-                }
+            if (DB) {
+                // this item's rows were issued during the previous item (the first item's now); wait, then start the
+                // previous item's row-result stores
+                if (item == it_lo) dma_rows(item, SB);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                flush();
+            } else if (DMA) {
+                dma_rows(item, SB);
                 flush();
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             } else {
@@ -3091,6 +3148,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             }
         }
         __syncthreads();
+        if (DB && item + 1 < it_hi) dma_rows(item + 1, SB == SB0 ? SB1 : SB0);   // every wave is past the other buffer
         if (RS >= 1 && MODE != 7 && tid < 4 * nsrc) {
             // row r's statistics by the quad of lanes 4r .. 4r + 3 (whole quads: DPP within the quad): exact full-row
             // sums of I and I^2 over the row's words (pixels past RW are zero), then each lane subtracts the window's

@@ -267,6 +267,18 @@ int main(int argc, char** argv) {
         printf("%-20s %8.1f us\n", name, ms * 1000.f / reps);
     };
     timeit([&] { launch_roi_tables(a, 0); }, "prod tables");
+    {   // tile classes of this geometry: interior + in LDS (the fast path), in LDS with border taps, global taps
+        std::vector<int4> td((size_t)C * n3 * a.tdesc_stride);
+        CK(hipMemcpy(td.data(), a.tdesc, td.size() * sizeof(int4), hipMemcpyDeviceToHost));
+        long fast = 0, lds_border = 0, glob = 0, empty = 0;
+        for (const int4& d : td) {
+            if (!(d.w & kTileAny)) ++empty;
+            else if ((d.w & kTileLds) && (d.w & kTileInterior)) ++fast;
+            else if (d.w & kTileLds) ++lds_border;
+            else ++glob;
+        }
+        printf("tiles: %ld interior+LDS, %ld LDS border, %ld global taps, %ld empty\n", fast, lds_border, glob, empty);
+    }
     timeit([&] { launch_roi_warp(a, 0); }, "prod warp");
     if (!envi("MB_CORR", 0)) {   // MB_CORR=1: the correlation section only (the ROIs from the product warp above)
         const long tiles = (long)a.slot_cap * ((TH + 6 + 31) / 32) * ((TW + 6 + 31) / 32);
@@ -292,6 +304,11 @@ int main(int argc, char** argv) {
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 3>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 abl addr only");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 4>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 abl no stores");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 5>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 abl no interior");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 0, true>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 7w pft");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<6, 68, 0, 0, true>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 6w pft");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 6>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 abl -stage");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 7>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 abl -tables");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 8>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 abl -border");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 64, 1>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 7w p64 r03stg");
             {   // every warp3 form writes the same ROI bytes as the round-3 form
                 const size_t nb = (size_t)a.slot_cap * a.roi_stride;
@@ -312,6 +329,7 @@ int main(int argc, char** argv) {
                 run_cmp([&] { hipLaunchKernelGGL((k_roi_warp3<7>), dim3(grid3), dim3(256), 0, 0, a); }, "p64");
                 run_cmp([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0>), dim3(grid3), dim3(256), 0, 0, a); }, "p68");
                 run_cmp([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 1>), dim3(grid3), dim3(256), 0, 0, a); }, "p68 r03stg");
+                run_cmp([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 0, true>), dim3(grid3), dim3(256), 0, 0, a); }, "p68 pft");
                 run_cmp([&] { launch_roi_warp(a, 0); }, "product");
             }
 
@@ -340,6 +358,14 @@ int main(int argc, char** argv) {
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 12, false, 1, true, true>), dim3(grid), dim3(256), lds, 0, a); }, "corrA SE DMA 3w");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 4, 12, false, 1, true, true>), dim3((int)std::min<long>(items, 1024)), dim3(256), lds, 0, a); }, "corrA SE DMA 4w");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 4, 12, false, 1, false, true>), dim3((int)std::min<long>(items, 1024)), dim3(256), lds, 0, a); }, "corrA DMA 4w");
+        {
+            const size_t lds_db = lds + 16 + (size_t)38 * a.roi_pitch;
+            hipFuncSetAttribute((const void*)k_roi_corr<0, true, 2, 12, false, 1, true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_db);
+            hipFuncSetAttribute((const void*)k_roi_corr<0, true, 3, 12, false, 1, true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_db);
+            printf("corr DB lds %zu\n", lds_db);
+            timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 2, 12, false, 1, true, true, true>), dim3((int)std::min<long>(items, 512)), dim3(256), lds_db, 0, a); }, "corrA SE DMA DB 2w");
+            timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 12, false, 1, true, true, true>), dim3((int)std::min<long>(items, 512)), dim3(256), lds_db, 0, a); }, "corrA SE DMA DB 3wr");
+        }
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<2, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA no mfma+epi");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<4, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA no edges");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<5, true, 3, 12, false>), dim3(grid), dim3(256), lds, 0, a); }, "corrA no stores");
@@ -354,6 +380,12 @@ int main(int argc, char** argv) {
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 8, false, 1, true>), dim3((int)std::min<long>(items, 768)), dim3(256), lds, 0, a); }, "corrA8 SE 3 waves");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 4, 8, false, 1, true>), dim3((int)std::min<long>(items, 1024)), dim3(256), lds, 0, a); }, "corrA8 SE 4 waves");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 4, 8, false, 1, true, true>), dim3((int)std::min<long>(items, 1024)), dim3(256), lds, 0, a); }, "corrA8 SE DMA 4w");
+        {
+            const size_t lds_db = lds + 16 + (size_t)38 * a.roi_pitch;
+            hipFuncSetAttribute((const void*)k_roi_corr<0, true, 4, 8, false, 1, true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_db);
+            printf("corr8 DB lds %zu\n", lds_db);
+            timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 4, 8, false, 1, true, true, true>), dim3((int)std::min<long>(items, 1024)), dim3(256), lds_db, 0, a); }, "corrA8 SE DMA DB 4w");
+        }
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 8, false, 0>), dim3((int)std::min<long>(items, 768)), dim3(256), lds, 0, a); }, "corrA8 RS0 3 waves");
     }
     timeit([&] { launch_roi_eval(a, 0); }, "prod eval");
@@ -378,6 +410,16 @@ int main(int argc, char** argv) {
             else if (TW > 256 && TW <= 512)
                 hipLaunchKernelGGL((k_roi_corr<0, true, 4, 8, false, 1, true, true>), dim3((int)std::min<long>(items, 1024)), dim3(256), lds1, 0, a);
             printf("host check of the DMA form\n");
+        }
+        if (envi("MB_DB_CHECK", 0)) {   // the host check below then checks the double-buffered LDS-DMA form
+            hipMemset(a.rowsum, 0xff, (size_t)C * n3 * ((TH * 49 + 3) & ~3) * 4);
+            const long items = (long)a.slot_cap * ((TH + 31) / 32);
+            const size_t lds_db = lds1 + 16 + (size_t)38 * a.roi_pitch;
+            if (TW > 512 && TW <= 768)
+                hipLaunchKernelGGL((k_roi_corr<0, true, 2, 12, false, 1, true, true, true>), dim3((int)std::min<long>(items, 512)), dim3(256), lds_db, 0, a);
+            else if (TW > 256 && TW <= 512)
+                hipLaunchKernelGGL((k_roi_corr<0, true, 4, 8, false, 1, true, true, true>), dim3((int)std::min<long>(items, 1024)), dim3(256), lds_db, 0, a);
+            printf("host check of the DB form\n");
         }
         if (envi("MB_SE_CHECK", 0)) {   // the host check below then checks the LDS-staged epilogue form
             hipMemset(a.rowsum, 0xff, (size_t)C * n3 * ((TH * 49 + 3) & ~3) * 4);
