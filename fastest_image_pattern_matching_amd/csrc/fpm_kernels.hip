@@ -1151,8 +1151,7 @@ __device__ void cand_init_job(const CandInitArgs& c, int mode, int job, int cnt,
     }
 }
 
-constexpr int kNmsChunkMax = 1024;   // plain path: per-thread runs up to this length (maps up to 256 K pixels)
-constexpr int kNmsLdsMapMax = 36 * 1024;   // plain path: maps up to this many pixels are copied into LDS (144 KB)
+constexpr int kNmsPlainBlk = 4096;   // plain path: 64-pixel block maxima kept in LDS (maps up to 256 K pixels)
 // ci_mode 0: peaks only; 1-3: also the job's candidate slots (cand_init_job; plain path, cap <= kNmsInitCap)
 __global__ __launch_bounds__(256) void k_nms(NmsArgs a, CandInitArgs ci, int ci_mode) {
     __shared__ float sv[4];
@@ -1161,7 +1160,8 @@ __global__ __launch_bounds__(256) void k_nms(NmsArgs a, CandInitArgs ci, int ci_
     __shared__ int aff[256];
     __shared__ Peak spk[kNmsInitCap];
     __shared__ int sbase;
-    extern __shared__ __attribute__((aligned(16))) float lmap[];
+    __shared__ float pbv[kNmsPlainBlk];
+    __shared__ int pbi[kNmsPlainBlk];
     const NmsJob& j = a.jobs[blockIdx.x];
     if (a.cand && a.cand_cnt[blockIdx.x] < 0) return;   // taken by k_nms_greedy
     float* m = j.map;
@@ -1181,63 +1181,46 @@ __global__ __launch_bounds__(256) void k_nms(NmsArgs a, CandInitArgs ci, int ci_
     }
     float* bm = j.bmax;
     int* bl = j.bloc;
-    // plain path on maps up to 256 x kNmsChunkMax pixels: thread tid owns the contiguous run [c0, c1) of the map and
-    // keeps its first maximum (tv, ti); after a painted rectangle only the threads whose run it touches re-scan, and
-    // the workgroup argmax (max value, lowest index) of the 256 run maxima is the map's first maximum -- the same
-    // answer as a full-map scan (round 4: the README Test4 search, 43 peaks on a 187 x 143 map, spent 545 us in
-    // full scans)
-    const int clen = ((n + 255) / 256 + 3) & ~3;   // a multiple of 4: runs start 16-byte aligned in an aligned map
-    const bool chunked = !blocks && clen <= kNmsChunkMax;
-    if (chunked && n <= a.lds_map) {
-        // the map into LDS (painted and re-scanned there; the HBM copy stays unpainted -- nothing reads it after the
-        // peaks, as in the fused top layer)
-        for (int k = tid; k < n; k += 256) lmap[k] = m[k];
-        __syncthreads();
-        m = lmap;
-    }
-    const int c0 = min(n, tid * clen), c1 = min(n, c0 + clen);
-    float tv = -INFINITY;
-    int ti = INT_MAX;
+    // plain path on maps of up to kNmsPlainBlk blocks of 64 pixels: the first maximum of every block in LDS; after a
+    // painted rectangle only the blocks it touches are re-scanned, and the workgroup argmax of the block maxima (largest
+    // value, lowest index) is the map's first maximum -- the same answer as a full-map scan (round 4: the README Test4
+    // search, 43 peak slots on a 373 x 284 map, spent 545 us in full scans)
+    const int nb64 = (n + 63) >> 6;
+    const bool chunked = !blocks && nb64 <= kNmsPlainBlk;
     const bool m16 = ((uintptr_t)m & 15) == 0;
-    auto scan_run = [&]() {   // 8 x 16 bytes (or 16 floats) in flight per round trip, compared in index order
-        tv = -INFINITY;
-        ti = INT_MAX;
-        if (m16) {
-            for (int k0 = c0; k0 < c1; k0 += 32) {
-                float4 x[8];
+    auto scan_blk = [&](int b) {   // first maximum of block b: its 16 loads in flight, compared in index order
+        const int k0 = b << 6, k1 = min(n, k0 + 64);
+        float tv = -INFINITY;
+        int ti = INT_MAX;
+        if (m16 && k1 - k0 == 64) {
+            float4 x[16];
 #pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    x[u] = k0 + 4 * u + 3 < c1 ? *(const float4*)(m + k0 + 4 * u)
-                                               : make_float4(k0 + 4 * u < c1 ? m[k0 + 4 * u] : -INFINITY,
-                                                             k0 + 4 * u + 1 < c1 ? m[k0 + 4 * u + 1] : -INFINITY,
-                                                             k0 + 4 * u + 2 < c1 ? m[k0 + 4 * u + 2] : -INFINITY,
-                                                             -INFINITY);
+            for (int u = 0; u < 16; ++u) x[u] = *(const float4*)(m + k0 + 4 * u);
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    if (x[u].x > tv) { tv = x[u].x; ti = k0 + 4 * u; }
-                    if (x[u].y > tv) { tv = x[u].y; ti = k0 + 4 * u + 1; }
-                    if (x[u].z > tv) { tv = x[u].z; ti = k0 + 4 * u + 2; }
-                    if (x[u].w > tv) { tv = x[u].w; ti = k0 + 4 * u + 3; }
-                }
+            for (int u = 0; u < 16; ++u) {
+                if (x[u].x > tv) { tv = x[u].x; ti = k0 + 4 * u; }
+                if (x[u].y > tv) { tv = x[u].y; ti = k0 + 4 * u + 1; }
+                if (x[u].z > tv) { tv = x[u].z; ti = k0 + 4 * u + 2; }
+                if (x[u].w > tv) { tv = x[u].w; ti = k0 + 4 * u + 3; }
             }
-            return;
+        } else {
+            for (int k = k0; k < k1; ++k) { const float x = m[k]; if (x > tv) { tv = x; ti = k; } }
         }
-        for (int k0 = c0; k0 < c1; k0 += 16) {
-            float x[16];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) x[u] = k0 + u < c1 ? m[k0 + u] : -INFINITY;
-#pragma unroll
-            for (int u = 0; u < 16; ++u)
-                if (x[u] > tv) { tv = x[u]; ti = k0 + u; }
-        }
+        pbv[b] = tv;
+        pbi[b] = ti;
+    };
+    auto blocks_argmax = [&]() {
+        v = -INFINITY;
+        i = INT_MAX;
+        for (int b = tid; b < nb64; b += 256) better(v, i, pbv[b], pbi[b]);
+        wg_argmax(v, i, sv, si);
     };
     if (blocks) {
         block_argmax(bm, bl, g.nb, last, sv, si, v, i);
     } else if (chunked) {
-        scan_run();
-        v = tv;
-        i = ti;
-        wg_argmax(v, i, sv, si);
+        for (int b = tid; b < nb64; b += 256) scan_blk(b);
+        __syncthreads();
+        blocks_argmax();
     } else {
         for (int k = tid; k < n; k += 256) { const float x = m[k]; if (x > v) { v = x; i = k; } }
         wg_argmax(v, i, sv, si);
@@ -1304,21 +1287,22 @@ __global__ __launch_bounds__(256) void k_nms(NmsArgs a, CandInitArgs ci, int ci_
             __syncthreads();
             block_argmax(bm, bl, g.nb, last, sv, si, v, i);
         } else if (chunked) {
-            // does the painted rectangle (rows y1 .. y2, columns x1 .. x2, as painted above) touch this run?
-            bool touched = false;
-            if (rw > 0 && rh > 0 && c0 < c1) {
+            // the blocks the painted rectangle (rows y1 .. y2, columns x1 .. x2, as painted above) touches: row y's
+            // segment covers blocks (y mw + x1) >> 6 .. (y mw + x2) >> 6, at most per_row of them (a block two rows share
+            // is re-scanned twice, to the same values)
+            if (rw > 0 && rh > 0) {
                 const int x1 = sx > 0 ? sx : 0, y1 = sy > 0 ? sy : 0;
                 const int x2 = min(sx + rw - 1, mw - 1), y2 = min(sy + rh - 1, mh - 1);
                 if (x1 <= x2 && y1 <= y2) {
-                    const int ya = max(c0 / mw, y1), yb = min((c1 - 1) / mw, y2);
-                    for (int y = ya; y <= yb && !touched; ++y)
-                        touched = max(c0, y * mw + x1) <= min(c1 - 1, y * mw + x2);
+                    const int per_row = ((x2 - x1) >> 6) + 2;
+                    for (int q = tid; q < (y2 - y1 + 1) * per_row; q += 256) {
+                        const int y = y1 + q / per_row, b = ((y * mw + x1) >> 6) + q % per_row;
+                        if (b <= ((y * mw + x2) >> 6)) scan_blk(b);
+                    }
                 }
             }
-            if (touched) scan_run();
-            v = tv;
-            i = ti;
-            wg_argmax(v, i, sv, si);
+            __syncthreads();
+            blocks_argmax();
         } else {
             v = -INFINITY;
             i = INT_MAX;
@@ -1746,13 +1730,9 @@ void launch_nms(const NmsArgs& a0, int njobs, int max_blocks, int max_map_dim, i
     if (njobs <= 0) return;
     NmsArgs a = a0;
     CandInitArgs cz{};
+    (void)max_map_pixels;
     a.lds_map = 0;
-    size_t lmap = 0;
-    if (!a.by_block && max_map_pixels > 0 && max_map_pixels <= kNmsLdsMapMax) {   // plain path: the map in LDS
-        a.lds_map = max_map_pixels;
-        lmap = sizeof(float) * (size_t)max_map_pixels;
-        ensure_lds_attr((const void*)k_nms, lmap);
-    }
+    const size_t lmap = 0;
     if (!a.by_block && ci && a.cap <= kNmsInitCap) {   // plain path with the candidate init fused
         hipLaunchKernelGGL(k_nms, dim3(njobs), dim3(256), lmap, st, a, *ci, ci->refine == 0 ? 1 : (ci->refine == 2 ? 3 : 2));
         return;
