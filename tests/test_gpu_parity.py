@@ -207,6 +207,22 @@ def test_top_fused_lds_threshold(gpu_matcher_factory, templates, monkeypatch):
     assert forms == sorted(forms, reverse=True), fused   # one threshold
 
 
+@pytest.mark.parametrize("size", [(500, 400), (1000, 900)])
+def test_plain_peak_loop_map_sizes(hip, size):
+    """The plain getNextMaxLoc loop (MaxPos 10: no s_BlockMax) on one large top map: a 20x20 template is searched at
+    level 0 (MinReduceArea 1024: no pyramid), so the maps are 481 x 381 (183 K pixels: the 64-pixel block maxima in LDS, a partial last block) and
+    981 x 881 (864 K pixels > 4096 blocks: the full-map scan form); both equal the oracle."""
+    w, h = size
+    t = synth.box_blur(synth.noise(20, 20, 128, 60, 5), 3)
+    s = synth.box_blur(synth.noise(w, h, 128, 40, w), 3)
+    for k in range(6):
+        synth.paste_rotated(s, t, 40 + (w - 80) * k / 5, 40 + (h - 80) * k / 5, 0.0)
+    gpu, orc, ostats, gstats = _run_both(hip, s, t, max_pos=10, tolerance_angle=0.0, score=0.3, min_reduce_area=1024)
+    assert gstats == ostats, (gstats, ostats)
+    assert_same_results(gpu, orc, f"plain_map_{w}x{h}")
+    assert len(orc) == 15
+
+
 @pytest.mark.parametrize("max_pos", [100, 150])
 def test_plain_peaks_many(hip, templates, max_pos):
     """Plain getNextMaxLoc path (top map / template area <= 500) with ~80 peaks per map: MaxPos 100 (cap 105) runs the
