@@ -2527,6 +2527,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 if (ry0 + lr + 8 * i <= ry1) st_at<uint32_t>(tile, st_lane + 256u * i, (uint32_t)(X0r[i] ^ Y0r[i] ^ adv[0] ^ bdv[3]));
             continue;
         }
+        if (ABL == 0 && !(flags & kTileAny)) {   // footprint outside the level: zeros, stored flipped (as k_roi_warp3)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (ry0 + lr + 8 * i <= ry1) st_at<uint32_t>(tile, st_lane + 256u * i, kRoiFlip);
+            continue;
+        }
         if ((flags & kTileInterior) && in_lds && ABL == 4) {
             const int obase = by0 * ftw + bxa;
             const int nvalid = RW - c0;
