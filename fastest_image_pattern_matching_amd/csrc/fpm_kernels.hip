@@ -4275,10 +4275,8 @@ void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
     // a candidate's three angle ROIs from one staged union footprint (k_roi_warp3; Src7 kernel pass at 43 sources:
     // layer 0 395 -> 329 us, layer 1 114 -> 99, bench 28.07k -> 29.62k searches/s, profiles/r03_r); FPM_WARP3=0 keeps
     // one ROI per task (measurement)
-    static const int warp3 = [] {
-        const char* e = getenv("FPM_WARP3");
-        return e ? atoi(e) : 1;
-    }();
+    const char* w3e = getenv("FPM_WARP3");   // read when the search is recorded (once per plan)
+    const int warp3 = w3e ? atoi(w3e) : 1;
     if (warp3 && a.n3 == 3 && a.slot_base % 3 == 0 && a.slot_cap % 3 == 0) {
         const long want3 = (tiles / 3 + 3) / 4;
         // 7 waves per SIMD with the first ROI's tables requested before the staging (8 would spill them): microbenchmark

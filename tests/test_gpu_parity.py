@@ -277,6 +277,23 @@ def test_step_prologue_forms(gpu_matcher_factory, templates, monkeypatch, prolog
     assert_same_results(gpu, orc, f"src7 prologue={prologue} score 0.3")
 
 
+@pytest.mark.parametrize("warp3", ["0", "1"])
+def test_src7_sampler_forms(gpu_matcher_factory, templates, monkeypatch, warp3):
+    """The ROI sampler as one task per tile position of a candidate's three angle ROIs (k_roi_warp3, default) and as one
+    task per ROI tile (k_roi_warp, FPM_WARP3=0), both with the empty-footprint tile path (a source whose candidates'
+    ROIs reach past the image): a batch of two Src7 sources equals the oracle."""
+    monkeypatch.setenv("FPM_WARP3", warp3)
+    t = templates["Dst7"]
+    srcs = [synth.src7_scene(t, seed=51 + i)[0] for i in range(2)]
+    m = gpu_matcher_factory(max_pos=6, tolerance_angle=180.0, score=0.5)
+    assert m.learnPattern(t)
+    m.stage(srcs)
+    got = [[r.as_tuple() for r in rr] for rr in m.match_staged()]
+    o = oracle.OracleMatcher().set(max_pos=6, tolerance_angle=180.0, score=0.5)
+    o.learnPattern(t)
+    assert got == [o.match(s) for s in srcs]
+
+
 @pytest.mark.parametrize("pyr2", ["0", "1"])
 def test_src7_batch_pyramid_forms(gpu_matcher_factory, templates, monkeypatch, pyr2):
     """The search pyramid as one launch per level (FPM_PYR2=0) and as two levels per launch at every pair
