@@ -1,6 +1,7 @@
 // fpm_kernels.hip — MI355X (gfx950) kernels of the NCC template-matching hot path.
 //
-//   K1  k_pyr_down    cv::pyrDown                          (TemplateMatcher.cpp:55, :124)
+//   K1  k_pyr_down_s  cv::pyrDown, one level per launch    (TemplateMatcher.cpp:55, :124)
+//       k_pyr_down2   two levels per launch (small inputs)
 //   K2  k_warp        cv::warpAffine INTER_LINEAR          (TemplateMatcher.cpp:175, :1089)
 //   K3+K4 k_ncc_map   matchTemplate(TM_CCORR) + CCOEFF_Denominator   (:177 -> :514, :523, :527-598)
 //   K5  k_nms         minMaxLoc + getNextMaxLoc / s_BlockMax (:179-210, :1196-1221, DataStructures.h:118-246)
@@ -8,7 +9,9 @@
 //   K6-K8 refinement  getRotatedROI + IM_Conv_SIMD fold + CCOEFF_Denominator + minMaxLoc + 3x3
 //                     (:309-328, :461-512, :527-598): k_roi_tables / k_roi_warp / k_roi_corr (i8 MFMA) / k_roi_eval
 //                     for large templates, k_roi_small (the ROI sampled into LDS, never stored) for small ones
-//       k_cand_step   best-of-3 / early break / back-mapping (:331-366) after k_roi_small
+//       k_cand_step   best-of-3 / early break / back-mapping (:331-366) after k_roi_small (small batches: after
+//                     the last of consecutive small layers, the earlier steps in k_roi_small's prologue)
+//       k_overlap_pairs filterWithRotatedRect's pair tests (:1133-1194), decisions replayed on the host
 //
 // Numerics contract: built with -ffp-contract=off, no fast-math; integer sums are exact; the per-row
 // int32 -> f32 fold is sequential in template-row order; the normalisation is IEEE f64 in the reference's
@@ -2680,8 +2683,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t box_rsrc(const uint8_t* base) 
 // taps read but not interpolated (XOR-folded), 3 = interior addressing only (no tap reads), 4 = no ROI stores (a
 // never-true store kept), 5 = no interior rows (staging, tables and border tiles only), 6 = as 5 without staging,
 // 7 = as 6 without the table loads, 8 = as 7 without border tiles (descriptor loads and the task loop only)
-// PFT: the next ROI's tables are requested before this ROI's rows are sampled (16 more VGPRs)
-template <int WPE, int PITCH = 64, int STG = 0, int ABL = 0, bool PFT = false>
+// PFT: the next ROI's tables are requested before this ROI's rows are sampled (16 more VGPRs); SLD: descriptors by
+// scalar loads
+template <int WPE, int PITCH = 64, int STG = 0, int ABL = 0, bool PFT = false, bool SLD = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_warp3(RoiArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t ft_all[4 * ROI_FT + 16];
     constexpr int ftw = PITCH;   // footprint row pitch
@@ -2738,7 +2742,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         int bx[3], by[3], wp[3], fh[3], fl[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            const int4 d = a.tdesc[(size_t)(3 * cand + j) * a.tdesc_stride + rem];
+            // the descriptor through the scalar cache (a uniform address in the constant address space: one
+            // s_load_dwordx4, no vector load and no readfirstlane; k_roi_tables wrote it in an earlier launch)
+            int4 d;
+            if (SLD) {
+                typedef int sv4 __attribute__((ext_vector_type(4)));
+                const sv4 q = *(const __attribute__((address_space(4))) sv4*)(size_t)(a.tdesc + (size_t)(3 * cand + j) * a.tdesc_stride + rem);
+                d = make_int4(q.x, q.y, q.z, q.w);
+            } else {
+                d = a.tdesc[(size_t)(3 * cand + j) * a.tdesc_stride + rem];
+            }
             bx[j] = __builtin_amdgcn_readfirstlane(d.x);
             by[j] = __builtin_amdgcn_readfirstlane(d.y);
             const int dz = __builtin_amdgcn_readfirstlane(d.z);

@@ -304,6 +304,7 @@ int main(int argc, char** argv) {
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 3>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 abl addr only");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 4>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 abl no stores");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 5>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 abl no interior");
+            timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 0, false, true>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 7w sld");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 0, true>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 7w pft");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<6, 68, 0, 0, true>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 6w pft");
             timeit([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 6>), dim3(grid3), dim3(256), 0, 0, a); }, "warp3 abl -stage");
@@ -330,6 +331,7 @@ int main(int argc, char** argv) {
                 run_cmp([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0>), dim3(grid3), dim3(256), 0, 0, a); }, "p68");
                 run_cmp([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 1>), dim3(grid3), dim3(256), 0, 0, a); }, "p68 r03stg");
                 run_cmp([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 0, true>), dim3(grid3), dim3(256), 0, 0, a); }, "p68 pft");
+                run_cmp([&] { hipLaunchKernelGGL((k_roi_warp3<7, 68, 0, 0, false, true>), dim3(grid3), dim3(256), 0, 0, a); }, "p68 sld");
                 run_cmp([&] { launch_roi_warp(a, 0); }, "product");
             }
 
