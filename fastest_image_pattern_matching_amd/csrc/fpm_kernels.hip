@@ -1155,6 +1155,7 @@ __device__ void cand_init_job(const CandInitArgs& c, int mode, int job, int cnt,
 }
 
 constexpr int kNmsPlainBlk = 4096;   // plain path: 64-pixel block maxima kept in LDS (maps up to 256 K pixels)
+constexpr long kNmsBlkMinWork = 1 << 16;   // ... used when peak slots x map pixels reach this
 // ci_mode 0: peaks only; 1-3: also the job's candidate slots (cand_init_job; plain path, cap <= kNmsInitCap)
 __global__ __launch_bounds__(256) void k_nms(NmsArgs a, CandInitArgs ci, int ci_mode) {
     __shared__ float sv[4];
@@ -1189,7 +1190,9 @@ __global__ __launch_bounds__(256) void k_nms(NmsArgs a, CandInitArgs ci, int ci_
     // value, lowest index) is the map's first maximum -- the same answer as a full-map scan (round 4: the README Test4
     // search, 43 peak slots on a 373 x 284 map, spent 545 us in full scans)
     const int nb64 = (n + 63) >> 6;
-    const bool chunked = !blocks && nb64 <= kNmsPlainBlk;
+    // (small loops keep the full-map scan: a lone Src7 search's 41 maps of ~2 K pixels and 8 peak slots ran 10.8 us
+    // that way, 15.0 us with the block maxima's extra barriers, profiles/r04_end)
+    const bool chunked = !blocks && nb64 <= kNmsPlainBlk && (long)a.cap * n >= kNmsBlkMinWork;
     const bool m16 = ((uintptr_t)m & 15) == 0;
     auto scan_blk = [&](int b) {   // first maximum of block b: its 16 loads in flight, compared in index order
         const int k0 = b << 6, k1 = min(n, k0 + 64);
