@@ -4459,18 +4459,25 @@ __global__ __launch_bounds__(256) void k_overlap_pairs(const OvRect* __restrict_
         const float4 bi = box[i];
         int nc = 0;   // wave-uniform
         bool over = false;
-        for (int j0 = i + 1; j0 < n; j0 += 64) {
-            const int j = j0 + lane;
-            bool ov = false;
-            if (j < n) {
-                const float4 bj = box[j];
-                ov = !(bj.x > bi.z || bj.z < bi.x || bj.y > bi.w || bj.w < bi.y);
+        // four 64-rectangle chunks' boxes in flight per round (the sweep of the first rectangles is the kernel's
+        // critical path: ~n / 64 dependent load round trips otherwise), then the chunks in ascending order
+        for (int j0 = i + 1; j0 < n && !over; j0 += 256) {
+            float4 bj[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int j = j0 + 64 * u + lane;
+                bj[u] = j < n ? box[j] : make_float4(INFINITY, -INFINITY, INFINITY, -INFINITY);
             }
-            const uint64_t m = __ballot(ov);
-            const int c = __popcll(m);
-            if (nc + c > kOverlapMaxCand) { over = true; break; }
-            if (ov) cand[wv][nc + __popcll(m & below)] = j;
-            nc += c;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int j = j0 + 64 * u + lane;
+                const bool ov = j < n && !(bj[u].x > bi.z || bj[u].z < bi.x || bj[u].y > bi.w || bj[u].w < bi.y);
+                const uint64_t m = __ballot(ov);
+                const int c = __popcll(m);
+                if (nc + c > kOverlapMaxCand) { over = true; break; }
+                if (ov) cand[wv][nc + __popcll(m & below)] = j;
+                nc += c;
+            }
         }
         if (over) {
             if (lane == 0) atomicOr(&meta[1], 1);
