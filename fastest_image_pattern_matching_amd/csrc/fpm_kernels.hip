@@ -257,8 +257,7 @@ __global__ __launch_bounds__(256) void k_pyr_down(const uint8_t* __restrict__ sr
 typedef unsigned short fpm_u16x2 __attribute__((ext_vector_type(2)));
 
 // OH: output rows per chunk (window 2 OH + 4 input rows; 16-byte loads per thread for it: 5 at OH 32, 3 at OH 16)
-// NT (measurement): the source rows by nontemporal loads
-template <int OH, bool NT = false>
+template <int OH>
 __global__ __launch_bounds__(256) void k_pyr_down_s(const uint8_t* __restrict__ src0, int sw, int sh, int sp,
                                                     size_t s_img, uint8_t* __restrict__ dst0, int dw, int dh,
                                                     int dp, size_t d_img, int nimg, int32_t* zero, int nzero) {
@@ -304,16 +303,7 @@ __global__ __launch_bounds__(256) void k_pyr_down_s(const uint8_t* __restrict__ 
                 const int r = i / Q, c = i - r * Q;
                 const int x = ix0 + 16 * c;
                 v[k] = make_uint4(0, 0, 0, 0);
-                if (r < nrows && x >= 0 && x + 16 <= sp) {
-                    const uint4* gp = (const uint4*)(src + (size_t)srow(iy + r) * sp + x);
-                    if (NT) {
-                        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-                        const u32x4 q = __builtin_nontemporal_load((const u32x4*)gp);
-                        v[k] = make_uint4(q.x, q.y, q.z, q.w);
-                    } else {
-                        v[k] = *gp;
-                    }
-                }
+                if (r < nrows && x >= 0 && x + 16 <= sp) v[k] = *(const uint4*)(src + (size_t)srow(iy + r) * sp + x);
             }
         };
         auto commit = [&](int roff, int nrows) {

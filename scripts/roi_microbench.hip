@@ -563,12 +563,6 @@ int main(int argc, char** argv) {
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));
         const double us = ms * 1000.0 / reps, bytes = (double)nsrc * ((double)W * H + (double)dw * dh);
         printf("pyr_down L0->L1 x8  %8.1f us  %.0f GB/s algorithmic\n", us, bytes / us / 1e3);
-        {
-            const int units = ((dw + PD_OW - 1) / PD_OW) * ((dh + 31) / 32) * nsrc;
-            const int g = units < kPyrWGs ? units : kPyrWGs;
-            timeit([&] { hipLaunchKernelGGL((k_pyr_down_s<32, true>), dim3(g), dim3(256), 0, 0, d_img, W, H, P, a.level_stride, d_out, dw, dh, dp, (size_t)dp * (dh + 1), nsrc, (int32_t*)nullptr, 0); }, "pyr L0->L1 nt loads");
-            timeit([&] { hipLaunchKernelGGL((k_pyr_down_s<32, false>), dim3(g), dim3(256), 0, 0, d_img, W, H, P, a.level_stride, d_out, dw, dh, dp, (size_t)dp * (dh + 1), nsrc, (int32_t*)nullptr, 0); }, "pyr L0->L1 plain");
-        }
         dim3 grid((dw + 127) / 128, (dh + 31) / 32, nsrc);
         timeit([&] { hipLaunchKernelGGL(k_pyr_down<1>, grid, dim3(256), 0, 0, d_img, W, H, P, a.level_stride, d_out, dw, dh, dp, (size_t)dp * (dh + 1)); }, "pyr loads only");
         timeit([&] { hipLaunchKernelGGL(k_pyr_down<2>, grid, dim3(256), 0, 0, d_img, W, H, P, a.level_stride, d_out, dw, dh, dp, (size_t)dp * (dh + 1)); }, "pyr +lds tile");
