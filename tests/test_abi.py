@@ -86,7 +86,9 @@ def test_product_library_holds_no_measurement_kernels():
         if k.startswith("fpm::k_roi_warp<"):
             assert args[1] == "0", k
         if k.startswith("fpm::k_roi_warp3<"):
-            assert args[3] == "0", k
+            assert args[3] == "0" and args[4:] == ["false", "false"], k   # no ablation, no measurement-only form
+        if k.startswith("fpm::k_roi_corr<"):
+            assert args[-1] == "false", k                                  # no double-buffered measurement form
 
 
 def test_product_switches_are_result_neutral():
