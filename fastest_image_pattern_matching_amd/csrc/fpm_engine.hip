@@ -750,9 +750,7 @@ int enqueue_search(fpm_ctx* ctx) {
         for (int a = 0; a < P.nang; ++a) mdim = std::max(mdim, std::max(P.map_w[a], P.map_h[a]));
         // plain path: k_nms also initialises the candidates (the live counter was zeroed by k_warp)
         cand_fused = !P.by_block && P.cap <= kNmsInitCap && (size_t)J * P.cap == (size_t)P.C;
-        int mpix = 0;
-        for (int a = 0; a < P.nang; ++a) mpix = std::max(mpix, P.map_w[a] * P.map_h[a]);
-        launch_nms(na, J, P.max_nblk, mdim, P.max_cells, st, P.max_nitems, cand_fused ? &ca : nullptr, mpix);
+        launch_nms(na, J, P.max_nblk, mdim, P.max_cells, st, P.max_nitems, cand_fused ? &ca : nullptr);
     }
     if (!cand_fused) {
         ProfScope ps(ctx, FPM_K_CAND_INIT, 0);

@@ -54,7 +54,6 @@ struct NmsArgs {
     int32_t by_block;
     int32_t mfc;             // MFC s_BlockMax semantics (fpm_params.semantics, MatchToolDlg.h:93-210)
     int32_t lds_blocks;      // block-maxima capacity in LDS (set by launch_nms; 0 = global scratch)
-    int32_t lds_map;         // plain path: map pixels held in dynamic LDS (set by launch_nms; 0 = the map in HBM)
     int32_t* cand;           // s_BlockMax mode: indices of the map pixels >= thr, [job][cand_cap] (k_nms_blocks)
     int32_t* cand_cnt;       // [job], zeroed before the launch
     int32_t cand_cap;        // kNmsCandCap
@@ -190,9 +189,8 @@ constexpr int kNmsCandCap = 8192;   // s_BlockMax candidates (pixels >= the top-
 // ci (plain getNextMaxLoc path only, cap <= kNmsInitCap): k_nms also does k_cand_init's work for its job's
 // candidate slots (one launch fewer); the live counter must have been zeroed by an earlier launch
 constexpr int kNmsInitCap = 128;
-// max_map_pixels: the largest map (plain path: held in LDS when it fits, kNmsLdsMapMax)
 void launch_nms(const NmsArgs& a, int njobs, int max_blocks, int max_map_dim, int max_cells, hipStream_t st,
-                int max_items = 0, const CandInitArgs* ci = nullptr, int max_map_pixels = 0);
+                int max_items = 0, const CandInitArgs* ci = nullptr);
 int nms_block_items(int mw, int mh, int tw, int th, int mfc);
 void launch_cand_init(const CandInitArgs& a, hipStream_t st);
 // K2-K5 fused for small canvases (plain peak path): LDS bytes of one (source, angle) job, and the launch (one

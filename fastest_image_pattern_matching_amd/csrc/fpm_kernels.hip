@@ -1732,15 +1732,12 @@ constexpr int kNmsLdsBlocksMax = 12 * 1024;   // block maxima kept in LDS up to 
 constexpr int kNmsLdsBytes = 160 * 1024 - 4096;   // k_nms_fast dynamic LDS budget (statics take the rest)
 
 void launch_nms(const NmsArgs& a0, int njobs, int max_blocks, int max_map_dim, int max_cells, hipStream_t st,
-                int max_items, const CandInitArgs* ci, int max_map_pixels) {
+                int max_items, const CandInitArgs* ci) {
     if (njobs <= 0) return;
     NmsArgs a = a0;
     CandInitArgs cz{};
-    (void)max_map_pixels;
-    a.lds_map = 0;
-    const size_t lmap = 0;
     if (!a.by_block && ci && a.cap <= kNmsInitCap) {   // plain path with the candidate init fused
-        hipLaunchKernelGGL(k_nms, dim3(njobs), dim3(256), lmap, st, a, *ci, ci->refine == 0 ? 1 : (ci->refine == 2 ? 3 : 2));
+        hipLaunchKernelGGL(k_nms, dim3(njobs), dim3(256), 0, st, a, *ci, ci->refine == 0 ? 1 : (ci->refine == 2 ? 3 : 2));
         return;
     }
     if (a.by_block && max_blocks > 0) {
@@ -1779,7 +1776,7 @@ void launch_nms(const NmsArgs& a0, int njobs, int max_blocks, int max_map_dim, i
         }
     }
     a.lds_blocks = 0;
-    hipLaunchKernelGGL(k_nms, dim3(njobs), dim3(256), lmap, st, a, cz, 0);
+    hipLaunchKernelGGL(k_nms, dim3(njobs), dim3(256), 0, st, a, cz, 0);
 }
 
 // ============================================================================================== init
