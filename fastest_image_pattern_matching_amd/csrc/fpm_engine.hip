@@ -830,10 +830,6 @@ int enqueue_search(fpm_ctx* ctx) {
         }
         const int total_rois = P.C * P.n3;
         const bool small = roi_small_fits(tl.w, tl.h);   // one-kernel refinement of the ROI in LDS
-        // FPM_REF_ROUNDS=k (measurement): layer 0 of a batch whose scratch holds every ROI as k device-sized parts
-        const char* rr_env = getenv("FPM_REF_ROUNDS");
-        const int parts = !small && l == 0 && total_rois <= P.slot_cap && rr_env && atoi(rr_env) > 1
-                              ? std::min(atoi(rr_env), 16) : 1;
         for (int base = 0; base < total_rois; base += P.slot_cap) {
             ra.slot_base = base;
             ra.slot_cap = std::min(P.slot_cap, total_rois - base);
@@ -842,25 +838,21 @@ int enqueue_search(fpm_ctx* ctx) {
                 launch_roi_small(ra, st);
                 continue;
             }
-            for (int part = 0; part < parts; ++part) {
-                ra.round_i = part;
-                ra.round_n = parts;
-                {
-                    ProfScope ps(ctx, FPM_K_ROI_TABLES, 0);
-                    launch_roi_tables(ra, st);
-                }
-                {
-                    ProfScope ps(ctx, FPM_K_ROI_WARP, 0);
-                    launch_roi_warp(ra, st);
-                }
-                {
-                    ProfScope ps(ctx, FPM_K_ROI_CORR, 0);
-                    launch_roi_corr(ra, st);
-                }
-                {
-                    ProfScope ps(ctx, FPM_K_ROI_EVAL, 0);
-                    launch_roi_eval(ra, st);
-                }
+            {
+                ProfScope ps(ctx, FPM_K_ROI_TABLES, 0);
+                launch_roi_tables(ra, st);
+            }
+            {
+                ProfScope ps(ctx, FPM_K_ROI_WARP, 0);
+                launch_roi_warp(ra, st);
+            }
+            {
+                ProfScope ps(ctx, FPM_K_ROI_CORR, 0);
+                launch_roi_corr(ra, st);
+            }
+            {
+                ProfScope ps(ctx, FPM_K_ROI_EVAL, 0);
+                launch_roi_eval(ra, st);
             }
         }
         if (in_run && l > run_end) {   // the step runs in the next layer's prologue

@@ -110,7 +110,6 @@ struct RoiArgs {
     int32_t per_source;      // candidates per source (nang * cap)
     int32_t slot_base;       // this round covers live ROIs [slot_base, slot_base + slot_cap)
     int32_t slot_cap;
-    int32_t round_i, round_n;   // round_n > 1: this launch covers part round_i of round_n of the live ROIs (roi_base)
     double mean, norm, inv_area;
     const int32_t* live;
     const int32_t* live_count;

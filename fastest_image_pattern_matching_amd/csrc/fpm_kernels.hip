@@ -2228,14 +2228,7 @@ __device__ __forceinline__ int ft_tap_general(const uint8_t* FT, int ftw, int bx
 }
 
 // this launch's live ROIs [slot_base, slot_base + count) (the host's rounds of whole candidates)
-// (round_n > 1: part round_i of round_n equal whole-candidate parts of the live ROIs, sized on the device)
-__device__ __forceinline__ int roi_part(const RoiArgs& a) {
-    const int total = *a.live_count * a.n3;
-    return (total + a.round_n * a.n3 - 1) / (a.round_n * a.n3) * a.n3;
-}
-__device__ __forceinline__ int roi_base(const RoiArgs& a) {
-    return a.round_n > 1 ? a.round_i * roi_part(a) : a.slot_base;
-}
+__device__ __forceinline__ int roi_base(const RoiArgs& a) { return a.slot_base; }
 __device__ __forceinline__ void roi_slot(const RoiArgs& a, int slot, int& id, int& jj) {
     const int ri = roi_base(a) + slot;
     const int li = ri / a.n3;
@@ -2245,8 +2238,7 @@ __device__ __forceinline__ void roi_slot(const RoiArgs& a, int slot, int& id, in
 
 __device__ __forceinline__ int roi_count(const RoiArgs& a) {
     int rois = *a.live_count * a.n3 - roi_base(a);
-    const int cap = a.round_n > 1 ? min(a.slot_cap, roi_part(a)) : a.slot_cap;
-    return rois < 0 ? 0 : (rois > cap ? cap : rois);
+    return rois < 0 ? 0 : (rois > a.slot_cap ? a.slot_cap : rois);
 }
 
 __device__ __forceinline__ void wave_sync() {
@@ -4302,8 +4294,7 @@ void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
         const long want3 = (tiles / 3 + 3) / 4;
         // 7 waves per SIMD with the first ROI's tables requested before the staging (8 would spill them): microbenchmark
         // 405.5 / 406.3 -> 400.6 / 402.0 us (round 3)
-        const long gcap = a.round_n > 1 ? 16384 / a.round_n : 16384;   // a part: its share of the grid
-        hipLaunchKernelGGL((k_roi_warp3<7, kFtPitch, 0>), dim3((int)(want3 < gcap ? want3 : gcap)), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((k_roi_warp3<7, kFtPitch, 0>), dim3((int)(want3 < 16384 ? want3 : 16384)), dim3(256), 0, st, a);
         return;
     }
     hipLaunchKernelGGL((k_roi_warp<kWarpFootBatch, 0, kWarpWaves>), dim3(grid), dim3(256), 0, st, a);

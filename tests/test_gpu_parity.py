@@ -294,22 +294,6 @@ def test_src7_sampler_forms(gpu_matcher_factory, templates, monkeypatch, warp3):
     assert got == [o.match(s) for s in srcs]
 
 
-@pytest.mark.parametrize("parts", [2, 5])
-def test_layer0_parts(gpu_matcher_factory, templates, monkeypatch, parts):
-    """Layer 0 of a batch run as device-sized parts (FPM_REF_ROUNDS: each part a whole-candidate slice of the live
-    list, sized from the live count on the device): the batched Src7 search is unchanged."""
-    monkeypatch.setenv("FPM_REF_ROUNDS", str(parts))
-    t = templates["Dst7"]
-    srcs = [synth.src7_scene(t, seed=41 + i)[0] for i in range(3)]
-    m = gpu_matcher_factory(max_pos=3, tolerance_angle=180.0, score=0.7)
-    assert m.learnPattern(t)
-    m.stage(srcs)
-    got = [[r.as_tuple() for r in rr] for rr in m.match_staged()]
-    o = oracle.OracleMatcher().set(max_pos=3, tolerance_angle=180.0, score=0.7)
-    o.learnPattern(t)
-    assert got == [o.match(s) for s in srcs]
-
-
 @pytest.mark.parametrize("pyr2", ["0", "1"])
 def test_src7_batch_pyramid_forms(gpu_matcher_factory, templates, monkeypatch, pyr2):
     """The search pyramid as one launch per level (FPM_PYR2=0) and as two levels per launch at every pair
