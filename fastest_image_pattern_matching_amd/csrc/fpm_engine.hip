@@ -778,6 +778,12 @@ int enqueue_search(fpm_ctx* ctx) {
     int cur_list = 0;   // live[cur_list]: the list the layer's ROIs come from; its count is livecnt[list_cnt]
     int list_cnt = 0;
     int run_k = 0;      // layers of the run done
+    // the next layer's warp tables written by the step of this layer (RoiArgs::nt_tab): where that layer takes tables
+    // (not small, not equal1) and every layer runs as one round; FPM_STEP_TABLES=0 keeps the k_roi_tables launches
+    // (result-neutral: the same pure functions of the stepped state)
+    const char* stab_env = getenv("FPM_STEP_TABLES");
+    const bool step_tables = (stab_env ? atoi(stab_env) != 0 : true) && (size_t)P.C * P.n3 <= (size_t)P.slot_cap;
+    bool tables_done = false;   // this layer's tables were written by the previous layer's step
     for (int l = L - 1; l >= 0; --l) {
         const int d = L - 1 - l;
         const SrcLevel& lv = ctx->src[l];
@@ -828,6 +834,15 @@ int enqueue_search(fpm_ctx* ctx) {
                 ra.live_out_count = livecnt + d;   // the survivors entering this layer (counted, not listed)
             }
         }
+        if (step_tables && l >= 1 && ra.step && !roi_small_fits(ctx->tmpl[l - 1].w, ctx->tmpl[l - 1].h) &&
+            !ctx->tmpl[l - 1].equal1) {
+            const TmplLevel& nt = ctx->tmpl[l - 1];
+            ra.nt_tab = P.d_tab.as<int32_t>();
+            ra.nt_nodes = P.d_nodes.as<AngleNode>() + P.node_off[d + 1];
+            ra.nt_tabw = roi_pitch_for(nt.w); ra.nt_tabh = roi_tab_rows(nt.h);
+            ra.nt_tw = nt.w; ra.nt_th = nt.h;
+            ra.nt_W = ctx->src[l - 1].w; ra.nt_H = ctx->src[l - 1].h;
+        }
         const int total_rois = P.C * P.n3;
         const bool small = roi_small_fits(tl.w, tl.h);   // one-kernel refinement of the ROI in LDS
         for (int base = 0; base < total_rois; base += P.slot_cap) {
@@ -838,7 +853,7 @@ int enqueue_search(fpm_ctx* ctx) {
                 launch_roi_small(ra, st);
                 continue;
             }
-            {
+            if (!tables_done) {
                 ProfScope ps(ctx, FPM_K_ROI_TABLES, 0);
                 launch_roi_tables(ra, st);
             }
@@ -855,7 +870,9 @@ int enqueue_search(fpm_ctx* ctx) {
                 launch_roi_eval(ra, st);
             }
         }
+        tables_done = ra.nt_tab != nullptr;
         if (in_run && l > run_end) {   // the step runs in the next layer's prologue
+            tables_done = false;
             ++run_k;
             continue;
         }

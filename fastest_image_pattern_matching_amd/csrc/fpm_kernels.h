@@ -143,6 +143,12 @@ struct RoiArgs {
     double prev_thr;             // vecLayerScore of the previous layer
     int32_t prev_W, prev_H;      // the previous layer's level size
     CandState* state_out;
+    // nt_tab != nullptr: the step (k_roi_eval, k_cand_step -> k_cand_step_tab) also writes the next layer's warp tables
+    // and tile descriptors for each survivor at its next-list position, so that layer launches no k_roi_tables (the
+    // next layer takes tables and runs as one round; tdesc / tdesc_stride / per_source are shared with it)
+    int32_t* nt_tab;
+    const AngleNode* nt_nodes;   // the next layer's nodes
+    int32_t nt_tabw, nt_tabh, nt_tw, nt_th, nt_W, nt_H;
     uint64_t* stamps;        // profiling ablations only (scripts/roi_microbench.hip): per-phase s_memtime stamps
 };
 

@@ -2343,65 +2343,68 @@ __device__ __forceinline__ void stage_block4(uint8_t* dst, int dp, const uint8_t
 constexpr int kTileAny = 1, kTileLds = 2, kTileInterior = 4, kTileSrcShift = 8;
 int roi_tiles_for(int tw, int th) { return ((tw + 6 + ROI_T - 1) / ROI_T) * ((th + 6 + ROI_T - 1) / ROI_T); }
 
-__global__ __launch_bounds__(256) void k_roi_tables(RoiArgs a) {
-    extern __shared__ int32_t tl[];   // ad[tabw] bd[tabw] x0[tabh] y0[tabh]
-    const int rois = roi_count(a);
-    const int RW = a.tw + 6, RH = a.th + 6, W = a.W, H = a.H;
+// The tables and descriptors of one ROI (slot) from its candidate's ptLT and angle node, by threads t0, t0 + nt, ...
+// of the caller.  The descriptors' corner samples recompute the same fixed-point rows and columns (pure functions of
+// M), so the threads need no LDS copy of the tables and no barrier.  Used by k_roi_tables and, for the next layer's
+// survivors, by the steps in k_roi_eval / k_cand_step_tab (RoiArgs::nt_tab).
+__device__ void roi_tables_fill(int32_t* tab, int4* tdesc, int tdesc_stride, int tabw, int tabh, int tw, int th,
+                                int W, int H, int slot, F2 lt, const AngleNode& nd, int src_bits, int t0, int nt) {
+    const int RW = tw + 6, RH = th + 6;
     const int txn = (RW + ROI_T - 1) / ROI_T, tyn = (RH + ROI_T - 1) / ROI_T;
-    int32_t* lad = tl;
-    int32_t* lbd = lad + a.tabw;
-    int32_t* lx0 = lbd + a.tabw;
-    int32_t* ly0 = lx0 + a.tabh;
+    double M[6];
+    roi_matrix(W, H, f2(lt.x * 2, lt.y * 2), nd.c, nd.s, M);
+    int32_t* t = tab + (size_t)slot * 2 * (tabw + tabh);
+    for (int x = t0; x < tabw; x += nt) {
+        const int ad = rint_i(M[0] * x * kAbScale), bd = rint_i(M[3] * x * kAbScale);
+        t[x] = ad * (1 << kTabShift); t[tabw + x] = bd * (1 << kTabShift);
+    }
+    for (int y = t0; y < tabh; y += nt) {
+        // rows past the ROI (the last tile block's padding) repeat its last row: k_roi_warp reads them unclamped
+        const int yc = min(y, RH - 1);
+        const int x0 = rint_i((M[1] * yc + M[2]) * kAbScale) + kRoundDelta;
+        const int y0 = rint_i((M[4] * yc + M[5]) * kAbScale) + kRoundDelta;
+        const int q = roi_tab_row_pos(y);
+        t[2 * tabw + q] = x0 * (1 << kTabShift); t[2 * tabw + tabh + q] = y0 * (1 << kTabShift);
+    }
+    for (int i = t0; i < txn * tyn; i += nt) {
+        const int ty = i / txn, tx = i - ty * txn;
+        const int cx0 = tx * ROI_T, cx1 = min(cx0 + ROI_T, RW) - 1;
+        const int ry0 = ty * ROI_T, ry1 = min(ry0 + ROI_T, RH) - 1;
+        int bx0 = INT_MAX, bx1 = INT_MIN, by0 = INT_MAX, by1 = INT_MIN;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int c = (k & 1) ? cx1 : cx0, r = (k & 2) ? ry1 : ry0;
+            const int ad = rint_i(M[0] * c * kAbScale), bd = rint_i(M[3] * c * kAbScale);
+            const int x0 = rint_i((M[1] * r + M[2]) * kAbScale) + kRoundDelta;
+            const int y0 = rint_i((M[4] * r + M[5]) * kAbScale) + kRoundDelta;
+            const int X = (x0 + ad) >> (kAbBits - kInterBits);
+            const int Y = (y0 + bd) >> (kAbBits - kInterBits);
+            bx0 = min(bx0, X >> kInterBits); bx1 = max(bx1, X >> kInterBits);
+            by0 = min(by0, Y >> kInterBits); by1 = max(by1, Y >> kInterBits);
+        }
+        const bool interior = bx0 - 1 >= 0 && bx1 + 1 <= W - 2 && by0 - 1 >= 0 && by1 + 1 <= H - 2;
+        bx0 = max(bx0 - 1, 0); by0 = max(by0 - 1, 0);
+        bx1 = min(bx1 + 2, W - 1); by1 = min(by1 + 2, H - 1);
+        const bool any = bx0 <= bx1 && by0 <= by1;
+        const int bxa = bx0 & ~3;
+        const int wpr = any ? (bx1 - bxa + 4) >> 2 : 0;   // dwords per footprint row
+        const int fth = any ? by1 - by0 + 1 : 0;
+        const bool in_lds = wpr <= 16 && kFtPitch * fth <= ROI_FT;
+        tdesc[(size_t)slot * tdesc_stride + i] =
+            make_int4(bxa, by0, wpr | (fth << 16),
+                      (any ? kTileAny : 0) | (in_lds ? kTileLds : 0) | (interior ? kTileInterior : 0) | src_bits);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_roi_tables(RoiArgs a) {
+    const int rois = roi_count(a);
     for (int slot = blockIdx.x; slot < rois; slot += gridDim.x) {
         int id, jj;
         roi_slot(a, slot, id, jj);
         const CandState st = a.state[id];
         const AngleNode nd = a.nodes[st.node * a.n3 + jj];
-        const int src_bits = (id / a.per_source) << kTileSrcShift;
-        double M[6];
-        roi_matrix(a.W, a.H, f2(st.lt.x * 2, st.lt.y * 2), nd.c, nd.s, M);
-        int32_t* t = a.tab + (size_t)slot * 2 * (a.tabw + a.tabh);
-        __syncthreads();   // previous slot's descriptors are done with the LDS tables
-        for (int x = threadIdx.x; x < a.tabw; x += 256) {
-            const int ad = rint_i(M[0] * x * kAbScale), bd = rint_i(M[3] * x * kAbScale);
-            t[x] = ad * (1 << kTabShift); t[a.tabw + x] = bd * (1 << kTabShift);
-            lad[x] = ad; lbd[x] = bd;
-        }
-        for (int y = threadIdx.x; y < a.tabh; y += 256) {
-            // rows past the ROI (the last tile block's padding) repeat its last row: k_roi_warp reads them unclamped
-            const int yc = min(y, RH - 1);
-            const int x0 = rint_i((M[1] * yc + M[2]) * kAbScale) + kRoundDelta;
-            const int y0 = rint_i((M[4] * yc + M[5]) * kAbScale) + kRoundDelta;
-            const int q = roi_tab_row_pos(y);
-            t[2 * a.tabw + q] = x0 * (1 << kTabShift); t[2 * a.tabw + a.tabh + q] = y0 * (1 << kTabShift);
-            lx0[y] = x0; ly0[y] = y0;
-        }
-        __syncthreads();
-        for (int i = threadIdx.x; i < txn * tyn; i += 256) {
-            const int ty = i / txn, tx = i - ty * txn;
-            const int cx0 = tx * ROI_T, cx1 = min(cx0 + ROI_T, RW) - 1;
-            const int ry0 = ty * ROI_T, ry1 = min(ry0 + ROI_T, RH) - 1;
-            int bx0 = INT_MAX, bx1 = INT_MIN, by0 = INT_MAX, by1 = INT_MIN;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int c = (k & 1) ? cx1 : cx0, r = (k & 2) ? ry1 : ry0;
-                const int X = (lx0[r] + lad[c]) >> (kAbBits - kInterBits);
-                const int Y = (ly0[r] + lbd[c]) >> (kAbBits - kInterBits);
-                bx0 = min(bx0, X >> kInterBits); bx1 = max(bx1, X >> kInterBits);
-                by0 = min(by0, Y >> kInterBits); by1 = max(by1, Y >> kInterBits);
-            }
-            const bool interior = bx0 - 1 >= 0 && bx1 + 1 <= W - 2 && by0 - 1 >= 0 && by1 + 1 <= H - 2;
-            bx0 = max(bx0 - 1, 0); by0 = max(by0 - 1, 0);
-            bx1 = min(bx1 + 2, W - 1); by1 = min(by1 + 2, H - 1);
-            const bool any = bx0 <= bx1 && by0 <= by1;
-            const int bxa = bx0 & ~3;
-            const int wpr = any ? (bx1 - bxa + 4) >> 2 : 0;   // dwords per footprint row
-            const int fth = any ? by1 - by0 + 1 : 0;
-            const bool in_lds = wpr <= 16 && kFtPitch * fth <= ROI_FT;
-            a.tdesc[(size_t)slot * a.tdesc_stride + i] =
-                make_int4(bxa, by0, wpr | (fth << 16),
-                          (any ? kTileAny : 0) | (in_lds ? kTileLds : 0) | (interior ? kTileInterior : 0) | src_bits);
-        }
+        roi_tables_fill(a.tab, a.tdesc, a.tdesc_stride, a.tabw, a.tabh, a.tw, a.th, a.W, a.H, slot, st.lt, nd,
+                        (id / a.per_source) << kTileSrcShift, threadIdx.x, 256);
     }
 }
 
@@ -4105,16 +4108,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 
 // candidate step of :329-366 from the scores and 7x7 argmax positions of a candidate's n3 records: best of the
 // angles, early break below vecLayerScore, back-mapping of ptLT, append to the next live list
-__device__ void cand_step_one(const RoiArgs& a, int id, const float* score, const int* mx, const int* my) {
+// returns the survivor's position in the next live list (-1: dead) and its stepped state in *so
+__device__ int cand_step_one(const RoiArgs& a, int id, const float* score, const int* mx, const int* my,
+                             CandState* so = nullptr) {
     CandState* out = a.state_out ? a.state_out : a.state;
     CandState s = a.state[id];
     if (!s.alive) {   // a hole of a prologue-stepped run (k_roi_small prev_rec): dead before this layer
         out[id] = s;
-        return;
+        return -1;
     }
     s = cand_step_state(s, a.n3, a.nodes, a.thr, a.W, a.H, a.mark_reached0, score, mx, my);
     out[id] = s;
-    if (s.alive) a.live_out[atomicAdd(a.live_out_count, 1)] = id;
+    if (so) *so = s;
+    if (!s.alive) return -1;
+    const int p = atomicAdd(a.live_out_count, 1);
+    a.live_out[p] = id;
+    return p;
+}
+
+// the next layer's tables of a survivor at live position p (RoiArgs::nt_tab; wave j <-> refinement angle j)
+__device__ __forceinline__ void cand_next_tables(const RoiArgs& a, int id, int p, const CandState& s, int j, int lane) {
+    const AngleNode nd = a.nt_nodes[s.node * a.n3 + j];
+    roi_tables_fill(a.nt_tab, a.tdesc, a.tdesc_stride, a.nt_tabw, a.nt_tabh, a.nt_tw, a.nt_th, a.nt_W, a.nt_H,
+                    p * a.n3 + j, s.lt, nd, (id / a.per_source) << kTileSrcShift, lane, 64);
 }
 
 // the candidate step as its own launch over the live list (after k_roi_small's equal1 records)
@@ -4127,6 +4143,30 @@ __global__ __launch_bounds__(256) void k_cand_step(RoiArgs a) {
         int mx[3], my[3];
         for (int k = 0; k < a.n3; ++k) { score[k] = r[k].score; mx[k] = r[k].mx; my[k] = r[k].my; }
         cand_step_one(a, id, score, mx, my);
+    }
+}
+
+// the candidate step with the next layer's tables (RoiArgs::nt_tab): one workgroup per live candidate, thread 0
+// steps, wave j writes the tables of the survivor's angle j (saves the next layer's k_roi_tables launch)
+__global__ __launch_bounds__(192) void k_cand_step_tab(RoiArgs a) {
+    __shared__ int pos;
+    __shared__ CandState ns;
+    const int n = *a.live_count;
+    const int lane = threadIdx.x & 63, j = threadIdx.x >> 6;
+    for (int li = blockIdx.x; li < n; li += gridDim.x) {
+        const int id = a.live[li];
+        __syncthreads();   // previous candidate's pos / ns consumed
+        if (threadIdx.x == 0) {
+            const RoiRecord* r = a.rec + (size_t)id * a.n3;
+            float score[3];
+            int mx[3], my[3];
+            for (int k = 0; k < a.n3; ++k) { score[k] = r[k].score; mx[k] = r[k].mx; my[k] = r[k].my; }
+            CandState s;
+            pos = cand_step_one(a, id, score, mx, my, &s);
+            ns = s;
+        }
+        __syncthreads();
+        if (pos >= 0 && j < a.n3) cand_next_tables(a, id, pos, ns, j, lane);
     }
 }
 
@@ -4245,6 +4285,8 @@ __global__ __launch_bounds__(192) void k_roi_eval(RoiArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t blk_all[3][2 * kEvalBuf];
     __shared__ float sc_all[3][64];
     __shared__ RoiRecord recs[3];
+    __shared__ int pos;
+    __shared__ CandState ns;
     const int lane = threadIdx.x & 63, j = threadIdx.x >> 6;   // wave j <-> refinement angle j
     const int rois = roi_count(a);
     const int base = roi_base(a);
@@ -4260,17 +4302,20 @@ __global__ __launch_bounds__(192) void k_roi_eval(RoiArgs a) {
             float score[3];
             int mx[3], my[3];
             for (int k = 0; k < a.n3; ++k) { score[k] = recs[k].score; mx[k] = recs[k].mx; my[k] = recs[k].my; }
-            cand_step_one(a, id, score, mx, my);
+            CandState s;
+            pos = cand_step_one(a, id, score, mx, my, &s);
+            ns = s;
         }
+        if (!a.nt_tab) continue;
+        __syncthreads();
+        if (pos >= 0) cand_next_tables(a, id, pos, ns, j, lane);   // the next layer's tables (no k_roi_tables)
     }
 }
 
 void launch_roi_tables(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0 || a.equal1) return;
     const int grid = a.slot_cap < 4096 ? a.slot_cap : 4096;
-    const size_t lds = sizeof(int32_t) * 2 * (a.tabw + a.tabh);
-    ensure_lds_attr((const void*)k_roi_tables, lds);
-    hipLaunchKernelGGL(k_roi_tables, dim3(grid), dim3(256), lds, st, a);
+    hipLaunchKernelGGL(k_roi_tables, dim3(grid), dim3(256), 0, st, a);
 }
 
 // footprint rows in flight per lane and waves per SIMD: each staging round trip is one memory latency per wave, so
@@ -4405,6 +4450,11 @@ void launch_roi_small(const RoiArgs& a, hipStream_t st) {
 
 void launch_cand_step(const RoiArgs& a, int max_items, hipStream_t st) {
     if (max_items <= 0 || !a.step) return;
+    if (a.nt_tab) {
+        const int grid = max_items < 2048 ? max_items : 2048;
+        hipLaunchKernelGGL(k_cand_step_tab, dim3(grid), dim3(192), 0, st, a);
+        return;
+    }
     int grid = (max_items + 255) / 256;
     if (grid > 1024) grid = 1024;
     hipLaunchKernelGGL(k_cand_step, dim3(grid), dim3(256), 0, st, a);

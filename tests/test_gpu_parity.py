@@ -294,6 +294,23 @@ def test_src7_sampler_forms(gpu_matcher_factory, templates, monkeypatch, warp3):
     assert got == [o.match(s) for s in srcs]
 
 
+@pytest.mark.parametrize("step_tables", ["0", "1"])
+@pytest.mark.parametrize("nsrc", [1, 3])
+def test_step_tables_forms(gpu_matcher_factory, templates, monkeypatch, step_tables, nsrc):
+    """The next layer's warp tables written by the step (k_roi_eval / k_cand_step_tab, FPM_STEP_TABLES=1, the
+    default) or by a k_roi_tables launch per layer (=0): the Src7 searches equal the oracle's either way."""
+    monkeypatch.setenv("FPM_STEP_TABLES", step_tables)
+    t = templates["Dst7"]
+    srcs = [synth.src7_scene(t, seed=71 + i)[0] for i in range(nsrc)]
+    m = gpu_matcher_factory(max_pos=3, tolerance_angle=180.0, score=0.7)
+    assert m.learnPattern(t)
+    m.stage(srcs)
+    got = [[r.as_tuple() for r in rr] for rr in m.match_staged()]
+    o = oracle.OracleMatcher().set(max_pos=3, tolerance_angle=180.0, score=0.7)
+    o.learnPattern(t)
+    assert got == [o.match(s) for s in srcs]
+
+
 @pytest.mark.parametrize("pyr2", ["0", "1"])
 def test_src7_batch_pyramid_forms(gpu_matcher_factory, templates, monkeypatch, pyr2):
     """The search pyramid as one launch per level (FPM_PYR2=0) and as two levels per launch at every pair
