@@ -3699,7 +3699,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 __device__ __forceinline__ CandState cand_step_state(CandState s, int n3, const AngleNode* nodes, double thr, int W,
                                                      int H, int mark_reached0, const float* score, const int* mx,
                                                      const int* my, const AngleNode* next_nodes = nullptr,
-                                                     int jj = 0, AngleNode* next_nd = nullptr) {
+                                                     int jj = 0, AngleNode* next_nd = nullptr, int nnext = 1) {
     int imax = 0;
     double big = -1;
     for (int k = 0; k < n3; ++k)
@@ -3710,7 +3710,8 @@ __device__ __forceinline__ CandState cand_step_state(CandState s, int n3, const 
     }
     const int child = s.node * n3 + imax;
     const AngleNode nd = nodes[child];
-    if (next_nodes) *next_nd = next_nodes[child * n3 + jj];
+    if (next_nodes)
+        for (int k = 0; k < nnext; ++k) next_nd[k] = next_nodes[child * n3 + jj + k];
     const F2 sc = f2((W - 1) / 2.0f, (H - 1) / 2.0f);
     const F2 r0 = rotate_pt(f2(s.lt.x * 2, s.lt.y * 2), sc, nd.c, nd.s);   // :350-353
     const F2 pad = f2(r0.x - 3, r0.y - 3);
@@ -4109,15 +4110,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // candidate step of :329-366 from the scores and 7x7 argmax positions of a candidate's n3 records: best of the
 // angles, early break below vecLayerScore, back-mapping of ptLT, append to the next live list
 // returns the survivor's position in the next live list (-1: dead) and its stepped state in *so
+// nn != nullptr (with a.nt_tab): also the survivor's n3 next-layer nodes, loaded beside its own child node
 __device__ int cand_step_one(const RoiArgs& a, int id, const float* score, const int* mx, const int* my,
-                             CandState* so = nullptr) {
+                             CandState* so = nullptr, AngleNode* nn = nullptr) {
     CandState* out = a.state_out ? a.state_out : a.state;
     CandState s = a.state[id];
     if (!s.alive) {   // a hole of a prologue-stepped run (k_roi_small prev_rec): dead before this layer
         out[id] = s;
         return -1;
     }
-    s = cand_step_state(s, a.n3, a.nodes, a.thr, a.W, a.H, a.mark_reached0, score, mx, my);
+    s = cand_step_state(s, a.n3, a.nodes, a.thr, a.W, a.H, a.mark_reached0, score, mx, my, nn ? a.nt_nodes : nullptr,
+                        0, nn, a.n3);
     out[id] = s;
     if (so) *so = s;
     if (!s.alive) return -1;
@@ -4127,8 +4130,8 @@ __device__ int cand_step_one(const RoiArgs& a, int id, const float* score, const
 }
 
 // the next layer's tables of a survivor at live position p (RoiArgs::nt_tab; wave j <-> refinement angle j)
-__device__ __forceinline__ void cand_next_tables(const RoiArgs& a, int id, int p, const CandState& s, int j, int lane) {
-    const AngleNode nd = a.nt_nodes[s.node * a.n3 + j];
+__device__ __forceinline__ void cand_next_tables(const RoiArgs& a, int id, int p, const CandState& s,
+                                                 const AngleNode& nd, int j, int lane) {
     roi_tables_fill(a.nt_tab, a.tdesc, a.tdesc_stride, a.nt_tabw, a.nt_tabh, a.nt_tw, a.nt_th, a.nt_W, a.nt_H,
                     p * a.n3 + j, s.lt, nd, (id / a.per_source) << kTileSrcShift, lane, 64);
 }
@@ -4151,6 +4154,7 @@ __global__ __launch_bounds__(256) void k_cand_step(RoiArgs a) {
 __global__ __launch_bounds__(192) void k_cand_step_tab(RoiArgs a) {
     __shared__ int pos;
     __shared__ CandState ns;
+    __shared__ AngleNode nn[3];
     const int n = *a.live_count;
     const int lane = threadIdx.x & 63, j = threadIdx.x >> 6;
     for (int li = blockIdx.x; li < n; li += gridDim.x) {
@@ -4162,11 +4166,11 @@ __global__ __launch_bounds__(192) void k_cand_step_tab(RoiArgs a) {
             int mx[3], my[3];
             for (int k = 0; k < a.n3; ++k) { score[k] = r[k].score; mx[k] = r[k].mx; my[k] = r[k].my; }
             CandState s;
-            pos = cand_step_one(a, id, score, mx, my, &s);
+            pos = cand_step_one(a, id, score, mx, my, &s, a.nt_tab ? nn : nullptr);
             ns = s;
         }
         __syncthreads();
-        if (pos >= 0 && j < a.n3) cand_next_tables(a, id, pos, ns, j, lane);
+        if (pos >= 0 && j < a.n3) cand_next_tables(a, id, pos, ns, nn[j], j, lane);
     }
 }
 
@@ -4287,6 +4291,7 @@ __global__ __launch_bounds__(192) void k_roi_eval(RoiArgs a) {
     __shared__ RoiRecord recs[3];
     __shared__ int pos;
     __shared__ CandState ns;
+    __shared__ AngleNode nn[3];
     const int lane = threadIdx.x & 63, j = threadIdx.x >> 6;   // wave j <-> refinement angle j
     const int rois = roi_count(a);
     const int base = roi_base(a);
@@ -4303,12 +4308,12 @@ __global__ __launch_bounds__(192) void k_roi_eval(RoiArgs a) {
             int mx[3], my[3];
             for (int k = 0; k < a.n3; ++k) { score[k] = recs[k].score; mx[k] = recs[k].mx; my[k] = recs[k].my; }
             CandState s;
-            pos = cand_step_one(a, id, score, mx, my, &s);
+            pos = cand_step_one(a, id, score, mx, my, &s, a.nt_tab ? nn : nullptr);
             ns = s;
         }
         if (!a.nt_tab) continue;
         __syncthreads();
-        if (pos >= 0) cand_next_tables(a, id, pos, ns, j, lane);   // the next layer's tables (no k_roi_tables)
+        if (pos >= 0) cand_next_tables(a, id, pos, ns, nn[j], j, lane);   // the next layer's tables (no k_roi_tables)
     }
 }
 
