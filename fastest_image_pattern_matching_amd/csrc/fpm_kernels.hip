@@ -10,8 +10,7 @@
 //                     (:309-328, :461-512, :527-598): k_roi_tables / k_roi_warp / k_roi_corr (i8 MFMA) / k_roi_eval
 //                     for large templates, k_roi_small (the ROI sampled into LDS, never stored) for small ones
 //       k_cand_step   best-of-3 / early break / back-mapping (:331-366) after k_roi_small (small batches: after
-//                     the last of consecutive small layers, the earlier steps in k_roi_small's prologue);
-//                     k_cand_step_tab / k_roi_eval also write the next layer's k_roi_tables output (RoiArgs::nt_tab)
+//                     the last of consecutive small layers, the earlier steps in k_roi_small's prologue)
 //       k_overlap_pairs filterWithRotatedRect's pair tests (:1133-1194), decisions replayed on the host
 //
 // Numerics contract: built with -ffp-contract=off, no fast-math; integer sums are exact; the per-row
@@ -2348,11 +2347,8 @@ int roi_tiles_for(int tw, int th) { return ((tw + 6 + ROI_T - 1) / ROI_T) * ((th
 // of the caller.  The descriptors' corner samples recompute the same fixed-point rows and columns (pure functions of
 // M), so the threads need no LDS copy of the tables and no barrier.  Used by k_roi_tables and, for the next layer's
 // survivors, by the steps in k_roi_eval / k_cand_step_tab (RoiArgs::nt_tab).
-// cs != nullptr (a caller that is one wave, wave-private LDS of 4 (txn + tyn) ints): the tiles' corner columns and rows
-// are computed once into cs and the descriptor loop reads them (the same values; fewer f64 operations per tile)
 __device__ void roi_tables_fill(int32_t* tab, int4* tdesc, int tdesc_stride, int tabw, int tabh, int tw, int th,
-                                int W, int H, int slot, F2 lt, const AngleNode& nd, int src_bits, int t0, int nt,
-                                int32_t* cs = nullptr) {
+                                int W, int H, int slot, F2 lt, const AngleNode& nd, int src_bits, int t0, int nt) {
     const int RW = tw + 6, RH = th + 6;
     const int txn = (RW + ROI_T - 1) / ROI_T, tyn = (RH + ROI_T - 1) / ROI_T;
     double M[6];
@@ -2370,19 +2366,6 @@ __device__ void roi_tables_fill(int32_t* tab, int4* tdesc, int tdesc_stride, int
         const int q = roi_tab_row_pos(y);
         t[2 * tabw + q] = x0 * (1 << kTabShift); t[2 * tabw + tabh + q] = y0 * (1 << kTabShift);
     }
-    if (cs) {   // cs: [2 txn] ad, [2 txn] bd of columns (tx, first / last), [2 tyn] x0, [2 tyn] y0 of rows
-        for (int k = t0; k < 2 * txn; k += nt) {
-            const int cx = k >> 1, c = (k & 1) ? min(cx * ROI_T + ROI_T, RW) - 1 : cx * ROI_T;
-            cs[k] = rint_i(M[0] * c * kAbScale);
-            cs[2 * txn + k] = rint_i(M[3] * c * kAbScale);
-        }
-        for (int k = t0; k < 2 * tyn; k += nt) {
-            const int cy = k >> 1, r = (k & 1) ? min(cy * ROI_T + ROI_T, RH) - 1 : cy * ROI_T;
-            cs[4 * txn + k] = rint_i((M[1] * r + M[2]) * kAbScale) + kRoundDelta;
-            cs[4 * txn + 2 * tyn + k] = rint_i((M[4] * r + M[5]) * kAbScale) + kRoundDelta;
-        }
-        wave_sync();
-    }
     for (int i = t0; i < txn * tyn; i += nt) {
         const int ty = i / txn, tx = i - ty * txn;
         const int cx0 = tx * ROI_T, cx1 = min(cx0 + ROI_T, RW) - 1;
@@ -2391,16 +2374,9 @@ __device__ void roi_tables_fill(int32_t* tab, int4* tdesc, int tdesc_stride, int
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int c = (k & 1) ? cx1 : cx0, r = (k & 2) ? ry1 : ry0;
-            int ad, bd, x0, y0;
-            if (cs) {
-                const int ci = 2 * tx + (k & 1), ri = 2 * ty + ((k >> 1) & 1);
-                ad = cs[ci]; bd = cs[2 * txn + ci];
-                x0 = cs[4 * txn + ri]; y0 = cs[4 * txn + 2 * tyn + ri];
-            } else {
-                ad = rint_i(M[0] * c * kAbScale); bd = rint_i(M[3] * c * kAbScale);
-                x0 = rint_i((M[1] * r + M[2]) * kAbScale) + kRoundDelta;
-                y0 = rint_i((M[4] * r + M[5]) * kAbScale) + kRoundDelta;
-            }
+            const int ad = rint_i(M[0] * c * kAbScale), bd = rint_i(M[3] * c * kAbScale);
+            const int x0 = rint_i((M[1] * r + M[2]) * kAbScale) + kRoundDelta;
+            const int y0 = rint_i((M[4] * r + M[5]) * kAbScale) + kRoundDelta;
             const int X = (x0 + ad) >> (kAbBits - kInterBits);
             const int Y = (y0 + bd) >> (kAbBits - kInterBits);
             bx0 = min(bx0, X >> kInterBits); bx1 = max(bx1, X >> kInterBits);
@@ -4154,13 +4130,10 @@ __device__ int cand_step_one(const RoiArgs& a, int id, const float* score, const
 }
 
 // the next layer's tables of a survivor at live position p (RoiArgs::nt_tab; wave j <-> refinement angle j)
-// cs: the wave's LDS scratch of cs_ints ints for roi_tables_fill's corner rows / columns (too small: recomputed per tile)
 __device__ __forceinline__ void cand_next_tables(const RoiArgs& a, int id, int p, const CandState& s,
-                                                 const AngleNode& nd, int j, int lane, int32_t* cs, int cs_ints) {
-    const int txn = (a.nt_tw + 6 + ROI_T - 1) / ROI_T, tyn = (a.nt_th + 6 + ROI_T - 1) / ROI_T;
+                                                 const AngleNode& nd, int j, int lane) {
     roi_tables_fill(a.nt_tab, a.tdesc, a.tdesc_stride, a.nt_tabw, a.nt_tabh, a.nt_tw, a.nt_th, a.nt_W, a.nt_H,
-                    p * a.n3 + j, s.lt, nd, (id / a.per_source) << kTileSrcShift, lane, 64,
-                    4 * (txn + tyn) <= cs_ints ? cs : nullptr);
+                    p * a.n3 + j, s.lt, nd, (id / a.per_source) << kTileSrcShift, lane, 64);
 }
 
 // the candidate step as its own launch over the live list (after k_roi_small's equal1 records)
@@ -4179,7 +4152,6 @@ __global__ __launch_bounds__(256) void k_cand_step(RoiArgs a) {
 // the candidate step with the next layer's tables (RoiArgs::nt_tab): one workgroup per live candidate, thread 0
 // steps, wave j writes the tables of the survivor's angle j (saves the next layer's k_roi_tables launch)
 __global__ __launch_bounds__(192) void k_cand_step_tab(RoiArgs a) {
-    __shared__ int32_t cs_all[3][512];
     __shared__ int pos;
     __shared__ CandState ns;
     __shared__ AngleNode nn[3];
@@ -4198,7 +4170,7 @@ __global__ __launch_bounds__(192) void k_cand_step_tab(RoiArgs a) {
             ns = s;
         }
         __syncthreads();
-        if (pos >= 0 && j < a.n3) cand_next_tables(a, id, pos, ns, nn[j], j, lane, cs_all[j], 512);
+        if (pos >= 0 && j < a.n3) cand_next_tables(a, id, pos, ns, nn[j], j, lane);
     }
 }
 
@@ -4341,7 +4313,7 @@ __global__ __launch_bounds__(192) void k_roi_eval(RoiArgs a) {
         }
         if (!a.nt_tab) continue;
         __syncthreads();
-        if (pos >= 0) cand_next_tables(a, id, pos, ns, nn[j], j, lane, (int32_t*)blk_all[j], 2 * kEvalBuf / 4);   // the next layer's tables (no k_roi_tables)
+        if (pos >= 0) cand_next_tables(a, id, pos, ns, nn[j], j, lane);   // the next layer's tables (no k_roi_tables)
     }
 }
 
