@@ -10,7 +10,8 @@
 //                     (:309-328, :461-512, :527-598): k_roi_tables / k_roi_warp / k_roi_corr (i8 MFMA) / k_roi_eval
 //                     for large templates, k_roi_small (the ROI sampled into LDS, never stored) for small ones
 //       k_cand_step   best-of-3 / early break / back-mapping (:331-366) after k_roi_small (small batches: after
-//                     the last of consecutive small layers, the earlier steps in k_roi_small's prologue)
+//                     the last of consecutive small layers, the earlier steps in k_roi_small's prologue);
+//                     k_cand_step_tab / k_roi_eval also write the next layer's k_roi_tables output (RoiArgs::nt_tab)
 //       k_overlap_pairs filterWithRotatedRect's pair tests (:1133-1194), decisions replayed on the host
 //
 // Numerics contract: built with -ffp-contract=off, no fast-math; integer sums are exact; the per-row
