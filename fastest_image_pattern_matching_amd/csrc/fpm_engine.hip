@@ -784,10 +784,6 @@ int enqueue_search(fpm_ctx* ctx) {
     const char* stab_env = getenv("FPM_STEP_TABLES");
     const bool step_tables = (stab_env ? atoi(stab_env) != 0 : true) && (size_t)P.C * P.n3 <= (size_t)P.slot_cap;
     bool tables_done = false;   // this layer's tables were written by the previous layer's step
-    // k_roi_eval's row-sum stream 3 blocks deep for batches of few sources (each block's memory latency is on the
-    // critical path when a handful of candidates run); FPM_EVAL_DEEP=0/1 overrides (result-neutral: same fold order)
-    const char* deep_env = getenv("FPM_EVAL_DEEP");
-    const int eval_deep = deep_env ? (atoi(deep_env) != 0) : (S <= kPrologueMaxSources);
     for (int l = L - 1; l >= 0; --l) {
         const int d = L - 1 - l;
         const SrcLevel& lv = ctx->src[l];
@@ -819,7 +815,6 @@ int enqueue_search(fpm_ctx* ctx) {
         ra.wsq = P.d_wsq.as<uint64_t>();
         ra.rec = P.d_rec.as<RoiRecord>();
         ra.step = l > 0 ? 1 : 0;   // candidate step fused into k_roi_eval (layer 0 is decided on the host)
-        ra.eval_deep = eval_deep;
         ra.mark_reached0 = l - 1 == 0 ? 1 : 0;
         ra.live_out = live[cur_list ^ 1];
         ra.live_out_count = livecnt + d + 1;

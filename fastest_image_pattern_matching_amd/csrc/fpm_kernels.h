@@ -149,7 +149,6 @@ struct RoiArgs {
     int32_t* nt_tab;
     const AngleNode* nt_nodes;   // the next layer's nodes
     int32_t nt_tabw, nt_tabh, nt_tw, nt_th, nt_W, nt_H;
-    int32_t eval_deep;           // k_roi_eval with 3 row-sum blocks in flight per wave (few candidates)
     uint64_t* stamps;        // profiling ablations only (scripts/roi_microbench.hip): per-phase s_memtime stamps
 };
 

@@ -4185,9 +4185,6 @@ constexpr int kEvalDma = (kEvalRows * 49 / 4 + 63) / 64;   // 16-byte LDS-DMA lo
 constexpr int kEvalBuf = kEvalDma * 1024;                    // bytes per block buffer
 static_assert(kEvalDma == 10, "the counted s_waitcnt vmcnt(10) in eval_roi assumes 10 loads per block");
 
-// NB: block buffers per wave, NB - 1 blocks' loads in flight while one folds (2: the batch form; 4: few candidates,
-// where every block's memory latency is on the critical path -- RoiArgs::eval_deep)
-template <int NB>
 __device__ void eval_roi(const RoiArgs& a, int slot, int lane, uint8_t* blk, float* sc, RoiRecord* out,
                          RoiRecord* keep) {
     const int th = a.th;
@@ -4237,17 +4234,15 @@ __device__ void eval_roi(const RoiArgs& a, int slot, int lane, uint8_t* blk, flo
     };
     float accF = 0.f;
     uint64_t accI = 0;
-    for (int b = 0; b < NB - 1 && b < nblk; ++b) issue_block(b, blk + b * kEvalBuf);
+    issue_block(0, blk);
     for (int b = 0; b < nblk; ++b) {
-        const uint32_t* cb = (const uint32_t*)(blk + (b % NB) * kEvalBuf);
-        // blocks b + 1 .. b + NB - 2 are in flight; issue b + NB - 1 into the buffer block b - 1 left, then wait
-        // for block b only (kEvalDma loads per later block may stay in flight)
-        if (b + NB - 1 < nblk) issue_block(b + NB - 1, blk + ((b + NB - 1) % NB) * kEvalBuf);
-        const int ahead = min(NB - 1, nblk - 1 - b);
-        if (ahead >= 3) asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
-        else if (ahead == 2) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
-        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t* cb = (const uint32_t*)(blk + (b & 1) * kEvalBuf);
+        if (b + 1 < nblk) {
+            issue_block(b + 1, blk + ((b + 1) & 1) * kEvalBuf);
+            asm volatile("s_waitcnt vmcnt(10)" ::: "memory");   // kEvalDma loads of block b + 1 may stay in flight
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         wave_sync();
         const int rows = min(kEvalRows, th - b * kEvalRows);
         if (lane < 49) {
@@ -4265,7 +4260,7 @@ __device__ void eval_roi(const RoiArgs& a, int slot, int lane, uint8_t* blk, flo
                 for (int t = 0; t < rows; ++t) accI += cb[t * 49 + lane];
             }
         }
-        wave_sync();   // block b folded before its buffer is refilled with block b + NB
+        wave_sync();   // block b folded before its buffer is refilled with block b + 2
     }
     if (lane < 49) {
         const double num = a.fold ? (double)accF : (double)(float)(double)accI;
@@ -4291,9 +4286,8 @@ __device__ void eval_roi(const RoiArgs& a, int slot, int lane, uint8_t* blk, flo
     }
 }
 
-template <int NB>
 __global__ __launch_bounds__(192) void k_roi_eval(RoiArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t eval_blk[];   // [n3][NB * kEvalBuf]
+    __shared__ __attribute__((aligned(16))) uint8_t blk_all[3][2 * kEvalBuf];
     __shared__ float sc_all[3][64];
     __shared__ RoiRecord recs[3];
     __shared__ int pos;
@@ -4307,8 +4301,7 @@ __global__ __launch_bounds__(192) void k_roi_eval(RoiArgs a) {
         const int id = a.live[li];
         const int slot = li * a.n3 + j - base;
         __syncthreads();   // previous candidate's records consumed
-        eval_roi<NB>(a, slot, lane, eval_blk + (size_t)j * NB * kEvalBuf, sc_all[j], a.rec + (size_t)id * a.n3 + j,
-                     &recs[j]);
+        eval_roi(a, slot, lane, blk_all[j], sc_all[j], a.rec + (size_t)id * a.n3 + j, &recs[j]);
         if (!a.step) continue;
         __syncthreads();
         if (threadIdx.x == 0) {   // TemplateMatcher.cpp:329-366
@@ -4432,15 +4425,7 @@ void launch_roi_eval(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0) return;
     const int cands = (a.slot_cap + a.n3 - 1) / a.n3;
     const int grid = cands < 4096 ? cands : 4096;
-    if (a.eval_deep) {
-        const size_t lds = (size_t)a.n3 * 4 * kEvalBuf;
-        ensure_lds_attr((const void*)k_roi_eval<4>, lds);
-        hipLaunchKernelGGL(k_roi_eval<4>, dim3(grid), dim3(64 * a.n3), lds, st, a);
-        return;
-    }
-    const size_t lds = (size_t)a.n3 * 2 * kEvalBuf;
-    ensure_lds_attr((const void*)k_roi_eval<2>, lds);
-    hipLaunchKernelGGL(k_roi_eval<2>, dim3(grid), dim3(64 * a.n3), lds, st, a);
+    hipLaunchKernelGGL(k_roi_eval, dim3(grid), dim3(64 * a.n3), 0, st, a);
 }
 
 void launch_roi_small(const RoiArgs& a, hipStream_t st) {

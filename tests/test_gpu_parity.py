@@ -294,15 +294,12 @@ def test_src7_sampler_forms(gpu_matcher_factory, templates, monkeypatch, warp3):
     assert got == [o.match(s) for s in srcs]
 
 
-@pytest.mark.parametrize("eval_deep", ["0", "1"])
 @pytest.mark.parametrize("step_tables", ["0", "1"])
 @pytest.mark.parametrize("nsrc", [1, 3])
-def test_step_tables_forms(gpu_matcher_factory, templates, monkeypatch, step_tables, nsrc, eval_deep):
+def test_step_tables_forms(gpu_matcher_factory, templates, monkeypatch, step_tables, nsrc):
     """The next layer's warp tables written by the step (k_roi_eval / k_cand_step_tab, FPM_STEP_TABLES=1, the
-    default) or by a k_roi_tables launch per layer (=0), and k_roi_eval's row-sum stream 1 or 3 blocks deep
-    (FPM_EVAL_DEEP): the Src7 searches equal the oracle's in every form."""
+    default) or by a k_roi_tables launch per layer (=0): the Src7 searches equal the oracle's either way."""
     monkeypatch.setenv("FPM_STEP_TABLES", step_tables)
-    monkeypatch.setenv("FPM_EVAL_DEEP", eval_deep)
     t = templates["Dst7"]
     srcs = [synth.src7_scene(t, seed=71 + i)[0] for i in range(nsrc)]
     m = gpu_matcher_factory(max_pos=3, tolerance_angle=180.0, score=0.7)
