@@ -633,9 +633,11 @@ __global__ __launch_bounds__(256) void k_pyr_down2(const uint8_t* __restrict__ s
 
 // FPM_PYR2_OH (16 or 32): profiling override of the two-level chunk height (32 is faster at the sizes the engine
 // uses the kernel for: one Src7 source, levels 0-2, 11.3 vs 13.2 us; 16 at 43 sources, 217 vs 237 us)
+// Unset: 32, or 16 where the 32-row chunks would give fewer units than the chip has CUs (the small level pairs of a
+// lone search, whose workgroups each run one unit: half the rows on each workgroup's serial path).
 static const int kPyr2OH = [] {
     const char* e = getenv("FPM_PYR2_OH");
-    return e && atoi(e) == 16 ? 16 : 32;
+    return e ? (atoi(e) == 16 ? 16 : 32) : 0;
 }();
 // one launch for pyramid levels l+1 and l+2 of nimg images (the units shared over kPyrWGs workgroups as
 // launch_pyr_down; seg_chunks > 0: that many units per workgroup, so runs start mid-strip -- tests)
@@ -643,8 +645,9 @@ void launch_pyr_down2(const uint8_t* src, int sw, int sh, int sp, size_t s_img, 
                       size_t b_img, uint8_t* cdst, int cw, int ch, int cp, size_t c_img, int nimg, hipStream_t st,
                       int seg_chunks, int32_t* zero, int nzero) {
     if (bw <= 0 || bh <= 0 || cw <= 0 || ch <= 0 || nimg <= 0) return;
-    const int ohb = kPyr2OH;
-    const int gx = (cw + PD2_OWC - 1) / PD2_OWC, chunks = (bh + ohb - 1) / ohb;
+    const int gx = (cw + PD2_OWC - 1) / PD2_OWC;
+    const int ohb = kPyr2OH ? kPyr2OH : ((long)gx * ((bh + 31) / 32) * nimg < 256 ? 16 : 32);
+    const int chunks = (bh + ohb - 1) / ohb;
     const long units = (long)gx * chunks * nimg;
     const long g = seg_chunks > 0 ? (units + seg_chunks - 1) / seg_chunks : std::min(units, (long)kPyrWGs);
     if (ohb == 16)
