@@ -88,7 +88,7 @@ SIGNATURES = {
     "fpm_match_staged_finish": (C.c_int, [_P, C.POINTER(Result), C.c_int32, C.POINTER(C.c_int32)]),
     "fpm_op_pyr_down": (C.c_int, [_P, _U8P, C.c_int32, C.c_int32, C.c_size_t, _U8P, C.c_size_t]),
     "fpm_op_pyr_down2": (C.c_int, [_P, _U8P, C.c_int32, C.c_int32, C.c_size_t, _U8P, C.c_size_t, _U8P, C.c_size_t,
-                                   C.c_int32]),
+                                   C.c_int32, C.c_int32]),
     "fpm_op_warp_affine": (C.c_int, [_P, _U8P, C.c_int32, C.c_int32, C.c_size_t, C.POINTER(C.c_double), _U8P,
                                      C.c_int32, C.c_int32, C.c_size_t, C.c_int32]),
     "fpm_op_ncc_map": (C.c_int, [_P, _U8P, C.c_int32, C.c_int32, C.c_size_t, C.c_int32, C.c_int32,

@@ -747,10 +747,14 @@ int enqueue_search(fpm_ctx* ctx) {
             na.sdone = P.d_livecnt.as<int32_t>() + P.off_skey + 6 * J;
         }
         int mdim = 0;
-        for (int a = 0; a < P.nang; ++a) mdim = std::max(mdim, std::max(P.map_w[a], P.map_h[a]));
+        long mpx = 0;
+        for (int a = 0; a < P.nang; ++a) {
+            mdim = std::max(mdim, std::max(P.map_w[a], P.map_h[a]));
+            mpx = std::max(mpx, (long)P.map_w[a] * P.map_h[a]);
+        }
         // plain path: k_nms also initialises the candidates (the live counter was zeroed by k_warp)
         cand_fused = !P.by_block && P.cap <= kNmsInitCap && (size_t)J * P.cap == (size_t)P.C;
-        launch_nms(na, J, P.max_nblk, mdim, P.max_cells, st, P.max_nitems, cand_fused ? &ca : nullptr);
+        launch_nms(na, J, P.max_nblk, mdim, P.max_cells, st, P.max_nitems, cand_fused ? &ca : nullptr, mpx);
     }
     if (!cand_fused) {
         ProfScope ps(ctx, FPM_K_CAND_INIT, 0);
@@ -1782,9 +1786,10 @@ int fpm_op_pyr_down(fpm_ctx* ctx, const uint8_t* src, int32_t w, int32_t h, size
 }
 
 int fpm_op_pyr_down2(fpm_ctx* ctx, const uint8_t* src, int32_t w, int32_t h, size_t ss, uint8_t* dst1, size_t ds1,
-                     uint8_t* dst2, size_t ds2, int32_t seg_chunks) {
+                     uint8_t* dst2, size_t ds2, int32_t seg_chunks, int32_t chunk_rows) {
     if (!ctx) return FPM_E_INVALID_ARG;
-    if (!src || !dst1 || !dst2 || w <= 0 || h <= 0 || ss < (size_t)w || seg_chunks < 0) {
+    if (!src || !dst1 || !dst2 || w <= 0 || h <= 0 || ss < (size_t)w || seg_chunks < 0 ||
+        (chunk_rows != 0 && chunk_rows != 16 && chunk_rows != 32)) {
         ctx->err = "bad image";
         return FPM_E_INVALID_ARG;
     }
@@ -1799,7 +1804,7 @@ int fpm_op_pyr_down2(fpm_ctx* ctx, const uint8_t* src, int32_t w, int32_t h, siz
     HIP_TRY(hipMemcpy2DAsync(ctx->d_op_a.p, sp, src, ss, w, h, hipMemcpyHostToDevice, ctx->stream));
     uint8_t* b = ctx->d_op_b.as<uint8_t>();
     launch_pyr_down2(ctx->d_op_a.as<uint8_t>(), w, h, sp, 0, b, bw, bh, bp, 0, b + boff, cw, ch, cp, 0, 1, ctx->stream,
-                     seg_chunks);
+                     seg_chunks, nullptr, 0, chunk_rows);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpy2DAsync(dst1, ds1, b, bp, bw, bh, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipMemcpy2DAsync(dst2, ds2, b + boff, cp, cw, ch, hipMemcpyDeviceToHost, ctx->stream));

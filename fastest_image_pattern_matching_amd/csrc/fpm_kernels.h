@@ -180,7 +180,7 @@ void launch_pyr_down(const uint8_t* src, int sw, int sh, int sp, size_t s_img, u
 // two pyramid levels in one launch: src -> b (level l+1, written) -> c (level l+2); same arguments per level
 void launch_pyr_down2(const uint8_t* src, int sw, int sh, int sp, size_t s_img, uint8_t* bdst, int bw, int bh, int bp,
                       size_t b_img, uint8_t* cdst, int cw, int ch, int cp, size_t c_img, int nimg, hipStream_t st,
-                      int seg_chunks = 0, int32_t* zero = nullptr, int nzero = 0);
+                      int seg_chunks = 0, int32_t* zero = nullptr, int nzero = 0, int chunk_rows = 0);
 // zero / nzero: counters the search zeroes before its later kernels use them (block (0, 0) clears them), so the
 // graph carries no memset nodes
 void launch_warp(const WarpJob* jobs, int njobs, int max_pixels, hipStream_t st, int32_t* zero = nullptr,
@@ -195,8 +195,9 @@ constexpr int kNmsCandCap = 8192;   // s_BlockMax candidates (pixels >= the top-
 // ci (plain getNextMaxLoc path only, cap <= kNmsInitCap): k_nms also does k_cand_init's work for its job's
 // candidate slots (one launch fewer); the live counter must have been zeroed by an earlier launch
 constexpr int kNmsInitCap = 128;
+// max_map_px: the largest map's pixel count (sizes k_nms's dynamic LDS; -1 = unknown)
 void launch_nms(const NmsArgs& a, int njobs, int max_blocks, int max_map_dim, int max_cells, hipStream_t st,
-                int max_items = 0, const CandInitArgs* ci = nullptr);
+                int max_items = 0, const CandInitArgs* ci = nullptr, long max_map_px = -1);
 int nms_block_items(int mw, int mh, int tw, int th, int mfc);
 void launch_cand_init(const CandInitArgs& a, hipStream_t st);
 // K2-K5 fused for small canvases (plain peak path): LDS bytes of one (source, angle) job, and the launch (one

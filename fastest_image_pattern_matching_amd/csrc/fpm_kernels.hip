@@ -640,13 +640,16 @@ static const int kPyr2OH = [] {
     return e ? (atoi(e) == 16 ? 16 : 32) : 0;
 }();
 // one launch for pyramid levels l+1 and l+2 of nimg images (the units shared over kPyrWGs workgroups as
-// launch_pyr_down; seg_chunks > 0: that many units per workgroup, so runs start mid-strip -- tests)
+// launch_pyr_down; seg_chunks > 0: that many units per workgroup, so runs start mid-strip -- tests; chunk_rows 16 /
+// 32 forces the level-(l+1) chunk height, 0 chooses it as above)
 void launch_pyr_down2(const uint8_t* src, int sw, int sh, int sp, size_t s_img, uint8_t* bdst, int bw, int bh, int bp,
                       size_t b_img, uint8_t* cdst, int cw, int ch, int cp, size_t c_img, int nimg, hipStream_t st,
-                      int seg_chunks, int32_t* zero, int nzero) {
+                      int seg_chunks, int32_t* zero, int nzero, int chunk_rows) {
     if (bw <= 0 || bh <= 0 || cw <= 0 || ch <= 0 || nimg <= 0) return;
     const int gx = (cw + PD2_OWC - 1) / PD2_OWC;
-    const int ohb = kPyr2OH ? kPyr2OH : ((long)gx * ((bh + 31) / 32) * nimg < 256 ? 16 : 32);
+    // chunk_rows 16 / 32: forced (parity tests of both ring carries); else the env override or the rule above
+    const int ohb = chunk_rows == 16 || chunk_rows == 32 ? chunk_rows
+                    : kPyr2OH ? kPyr2OH : ((long)gx * ((bh + 31) / 32) * nimg < 256 ? 16 : 32);
     const int chunks = (bh + ohb - 1) / ohb;
     const long units = (long)gx * chunks * nimg;
     const long g = seg_chunks > 0 ? (units + seg_chunks - 1) / seg_chunks : std::min(units, (long)kPyrWGs);
@@ -1160,16 +1163,20 @@ __device__ void cand_init_job(const CandInitArgs& c, int mode, int job, int cnt,
 
 constexpr int kNmsPlainBlk = 4096;   // plain path: 64-pixel block maxima kept in LDS (maps up to 256 K pixels)
 constexpr long kNmsBlkMinWork = 1 << 16;   // ... used when peak slots x map pixels reach this
-// ci_mode 0: peaks only; 1-3: also the job's candidate slots (cand_init_job; plain path, cap <= kNmsInitCap)
-__global__ __launch_bounds__(256) void k_nms(NmsArgs a, CandInitArgs ci, int ci_mode) {
+constexpr size_t kNmsPlainBlkLds = (size_t)8 * kNmsPlainBlk;   // dynamic LDS of k_nms's block maxima
+// ci_mode 0: peaks only; 1-3: also the job's candidate slots (cand_init_job; plain path, cap <= kNmsInitCap).
+// blk_lds: the launch carries kNmsPlainBlkLds of dynamic LDS for the plain path's block maxima (launch_nms gives it
+// only where some job can take that path, so the other launches keep their occupancy)
+__global__ __launch_bounds__(256) void k_nms(NmsArgs a, CandInitArgs ci, int ci_mode, int blk_lds) {
     __shared__ float sv[4];
     __shared__ int si[4];
     __shared__ int naff;
     __shared__ int aff[256];
     __shared__ Peak spk[kNmsInitCap];
     __shared__ int sbase;
-    __shared__ float pbv[kNmsPlainBlk];
-    __shared__ int pbi[kNmsPlainBlk];
+    extern __shared__ __attribute__((aligned(16))) uint8_t nms_dyn[];
+    float* const pbv = (float*)nms_dyn;
+    int* const pbi = (int*)(nms_dyn + 4 * kNmsPlainBlk);
     const NmsJob& j = a.jobs[blockIdx.x];
     if (a.cand && a.cand_cnt[blockIdx.x] < 0) return;   // taken by k_nms_greedy
     float* m = j.map;
@@ -1196,7 +1203,7 @@ __global__ __launch_bounds__(256) void k_nms(NmsArgs a, CandInitArgs ci, int ci_
     const int nb64 = (n + 63) >> 6;
     // (small loops keep the full-map scan: a lone Src7 search's 41 maps of ~2 K pixels and 8 peak slots ran 10.8 us
     // that way, 15.0 us with the block maxima's extra barriers, profiles/r04_end)
-    const bool chunked = !blocks && nb64 <= kNmsPlainBlk && (long)a.cap * n >= kNmsBlkMinWork;
+    const bool chunked = blk_lds && !blocks && nb64 <= kNmsPlainBlk && (long)a.cap * n >= kNmsBlkMinWork;
     const bool m16 = ((uintptr_t)m & 15) == 0;
     auto scan_blk = [&](int b) {   // first maximum of block b: its 16 loads in flight, compared in index order
         const int k0 = b << 6, k1 = min(n, k0 + 64);
@@ -1736,12 +1743,17 @@ constexpr int kNmsLdsBlocksMax = 12 * 1024;   // block maxima kept in LDS up to 
 constexpr int kNmsLdsBytes = 160 * 1024 - 4096;   // k_nms_fast dynamic LDS budget (statics take the rest)
 
 void launch_nms(const NmsArgs& a0, int njobs, int max_blocks, int max_map_dim, int max_cells, hipStream_t st,
-                int max_items, const CandInitArgs* ci) {
+                int max_items, const CandInitArgs* ci, long max_map_px) {
     if (njobs <= 0) return;
     NmsArgs a = a0;
     CandInitArgs cz{};
+    // k_nms's block maxima (its plain path on maps where peak slots x pixels >= kNmsBlkMinWork): LDS only if some map
+    // can take that path (max_map_px < 0: unknown, always)
+    const int blk = max_map_px < 0 || (long)a.cap * max_map_px >= kNmsBlkMinWork;
+    const size_t blds = blk ? kNmsPlainBlkLds : 0;
     if (!a.by_block && ci && a.cap <= kNmsInitCap) {   // plain path with the candidate init fused
-        hipLaunchKernelGGL(k_nms, dim3(njobs), dim3(256), 0, st, a, *ci, ci->refine == 0 ? 1 : (ci->refine == 2 ? 3 : 2));
+        hipLaunchKernelGGL(k_nms, dim3(njobs), dim3(256), blds, st, a, *ci,
+                           ci->refine == 0 ? 1 : (ci->refine == 2 ? 3 : 2), blk);
         return;
     }
     if (a.by_block && max_blocks > 0) {
@@ -1759,7 +1771,7 @@ void launch_nms(const NmsArgs& a0, int njobs, int max_blocks, int max_map_dim, i
                 hipLaunchKernelGGL(k_nms_greedy, dim3(njobs), dim3(256), nms_greedy_lds(max_cells), st, gA);
             }
             a.lds_blocks = 0;
-            hipLaunchKernelGGL(k_nms, dim3(njobs), dim3(256), 0, st, a, cz, 0);
+            hipLaunchKernelGGL(k_nms, dim3(njobs), dim3(256), blds, st, a, cz, 0, blk);
             return;
         }
         const size_t fixed = nms_fast_lds(max_blocks, a.cap, 0);
@@ -1780,7 +1792,7 @@ void launch_nms(const NmsArgs& a0, int njobs, int max_blocks, int max_map_dim, i
         }
     }
     a.lds_blocks = 0;
-    hipLaunchKernelGGL(k_nms, dim3(njobs), dim3(256), 0, st, a, cz, 0);
+    hipLaunchKernelGGL(k_nms, dim3(njobs), dim3(256), blds, st, a, cz, 0, blk);
 }
 
 // ============================================================================================== init

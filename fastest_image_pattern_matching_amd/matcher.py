@@ -304,14 +304,16 @@ class TemplateMatcher:
             raise ValueError(self.last_error())
         return out
 
-    def pyr_down2(self, img, seg_chunks: int = 0):
-        """(pyrDown(img), pyrDown(pyrDown(img))) from the search's two-level pyramid kernel."""
+    def pyr_down2(self, img, seg_chunks: int = 0, chunk_rows: int = 0):
+        """(pyrDown(img), pyrDown(pyrDown(img))) from the search's two-level pyramid kernel (chunk_rows 16 / 32 forces
+        its level-1 chunk height; 0 chooses it as the search does)."""
         g = _gray(img)
         h, w = g.shape
         b = np.zeros(((h + 1) // 2, (w + 1) // 2), np.uint8)
         c = np.zeros(((b.shape[0] + 1) // 2, (b.shape[1] + 1) // 2), np.uint8)
         rc = self._check(self._lib.fpm_op_pyr_down2(self._ctx, L.u8ptr(g), w, h, g.strides[0], L.u8ptr(b), b.strides[0],
-                                                    L.u8ptr(c), c.strides[0], int(seg_chunks)), "pyr_down2")
+                                                    L.u8ptr(c), c.strides[0], int(seg_chunks), int(chunk_rows)),
+                         "pyr_down2")
         if rc != L.FPM_OK:
             raise ValueError(self.last_error())
         return b, c

@@ -86,6 +86,51 @@ def gather_results(local: Sequence[Sequence[Sequence[float]]], n_total: int, cap
     return full
 
 
+def pack_result_arrays(views: Sequence[Tuple[np.ndarray, np.ndarray]], slots: int, cap: int) -> np.ndarray:
+    """pack_results from ``match_staged_array`` views -- (counts [n], results [n, buffer cap, 12]) of consecutive
+    source runs, e.g. one per context -- without building Python objects (the per-step exchange of bench.py)."""
+    block = np.zeros((slots, 1 + cap * FIELDS), dtype=np.float64)
+    row = 0
+    for cnt, res in views:
+        n = len(cnt)
+        if row + n > slots:
+            raise ValueError(f"{row + n} sources do not fit {slots} slots")
+        if n and int(cnt.max()) > cap:
+            raise ValueError(f"{int(cnt.max())} results exceed capacity {cap}")
+        k = min(cap, res.shape[1])
+        block[row:row + n, 0] = cnt
+        # rows past a source's count are zeroed so the block does not depend on stale buffer contents
+        keep = np.arange(k)[None, :] < cnt[:, None]
+        block[row:row + n, 1:1 + k * FIELDS] = np.where(keep[..., None], res[:, :k], 0.0).reshape(n, k * FIELDS)
+        row += n
+    return block
+
+
+def gather_result_arrays(views: Sequence[Tuple[np.ndarray, np.ndarray]], n_total: int, cap: int, group=None,
+                         device=None) -> Tuple[np.ndarray, np.ndarray]:
+    """gather_results over array views: this rank's shard_range(n_total, world, rank) sources as (counts, results)
+    runs; returns (counts [n_total], results [n_total, cap, 12]) in source order on every rank (one all_gather)."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    sizes = shard_sizes(n_total, world)
+    if sum(len(c) for c, _ in views) != sizes[rank]:
+        raise ValueError(f"rank {rank}: views hold {sum(len(c) for c, _ in views)} sources, shard has {sizes[rank]}")
+    slots = max(max(sizes), 1)
+    mine = torch.from_numpy(pack_result_arrays(views, slots, cap))
+    if device is not None:
+        mine = mine.to(device)
+    parts = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(parts, mine, group=group)
+    full = np.concatenate([parts[k].cpu().numpy()[:sizes[k]] for k in range(world)])
+    counts = full[:, 0].astype(np.int64)
+    if counts.size and (counts.min() < 0 or counts.max() > cap):
+        raise ValueError("corrupt result block")
+    return counts, full[:, 1:].reshape(len(full), cap, FIELDS)
+
+
 def match_sharded(matcher, sources: Sequence[np.ndarray], cap: int = 256, group=None, device=None):
     """Search this rank's slice of `sources` with `matcher` (a TemplateMatcher bound to this rank's GPU) and
     return every source's results, in source order, on every rank."""

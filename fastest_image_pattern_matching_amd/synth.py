@@ -103,14 +103,15 @@ def src10_scene(t=None, seed: int = 10):
     return s, t
 
 
-def batch_sources(n: int, size: int = 4096, tsize: int = 512, seed0: int = 1000):
+def batch_sources(n: int, size: int = 4096, tsize: int = 512, seed0: int = 1000, first: int = 0):
     """configs[3]: n box-blurred uniform sources; the template is the tsize crop of source 0 at the centre,
-    re-pasted into every source at a seeded angle and position."""
+    re-pasted into every source at a seeded angle and position.  ``first``: the sources first .. first + n - 1 of
+    the same sequence (one rank's shard: every source depends only on its index)."""
     base = box_blur(np.random.default_rng(seed0).integers(0, 256, (size, size), dtype=np.uint8), 5)
     c0 = (size - tsize) // 2
     t = base[c0:c0 + tsize, c0:c0 + tsize].copy()
     out = []
-    for i in range(n):
+    for i in range(first, first + n):
         s = base.copy() if i == 0 else box_blur(
             np.random.default_rng(seed0 + i).integers(0, 256, (size, size), dtype=np.uint8), 5)
         rng = np.random.default_rng(seed0 + 10_000 + i)

@@ -171,10 +171,13 @@ int fpm_op_pyr_down(fpm_ctx* ctx, const uint8_t* src, int32_t w, int32_t h, size
                     uint8_t* dst, size_t dst_stride);
 /* Two cv::pyrDown levels in one device launch (the search's pyramid kernel, k_pyr_down2): dst1 = pyrDown(src),
  * dst2 = pyrDown(dst1), each with cv::pyrDown's own reflect-101 border at its level (buildPyramid,
- * TemplateMatcher.cpp:124).  seg_chunks > 0 gives each workgroup that many 32-row chunks of level 1 (runs that start
- * mid-image, as a multi-source search has them); 0 sizes the grid as the search does. */
+ * TemplateMatcher.cpp:124).  Level 1 is walked in chunks of 16 or 32 rows: chunk_rows 16 or 32 forces that
+ * height, 0 lets the kernel choose as the search does (32, or 16 where 32-row chunks would leave CUs idle).
+ * seg_chunks > 0 gives each workgroup that many chunks of level 1 (runs that start mid-image, as a multi-source
+ * search has them); 0 sizes the grid as the search does. */
 int fpm_op_pyr_down2(fpm_ctx* ctx, const uint8_t* src, int32_t w, int32_t h, size_t src_stride,
-                     uint8_t* dst1, size_t dst1_stride, uint8_t* dst2, size_t dst2_stride, int32_t seg_chunks);
+                     uint8_t* dst1, size_t dst1_stride, uint8_t* dst2, size_t dst2_stride, int32_t seg_chunks,
+                     int32_t chunk_rows);
 /* cv::warpAffine(INTER_LINEAR, BORDER_CONSTANT=border) with forward 2x3 matrix m (row-major), as called at
  * TemplateMatcher.cpp:175 (top layer) and :1089 (getRotatedROI, border 0). */
 int fpm_op_warp_affine(fpm_ctx* ctx, const uint8_t* src, int32_t w, int32_t h, size_t src_stride,

@@ -61,7 +61,7 @@ int main() {
         } else {
             hipLaunchKernelGGL(k_nms_blocks, dim3((g.nb + 3) / 4), dim3(256), 0, 0, b);
             b.lds_blocks = 0;
-            hipLaunchKernelGGL(k_nms, dim3(1), dim3(256), 0, 0, b);
+            hipLaunchKernelGGL(k_nms, dim3(1), dim3(256), 0, 0, b, CandInitArgs{}, 0, 0);
         }
         hipEventRecord(e1);
         CK(hipEventSynchronize(e1));

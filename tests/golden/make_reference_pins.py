@@ -26,8 +26,16 @@ running the oracle on the pair -- such a pin's count is fitted, not an independe
       0.764 / 0.703 in the oracle, so at Score 0.8 it returns one (``count_at_published``); the pin runs Score 0.7
       (fitted);
   Result4.jpg = Src4/Dst4 (Test5, parameters not published): Tol 180, TargetNum 30, Score 0.7 (all fitted): 24;
-  Result6.jpg = Src6/Dst6, README Test6 parameters: 15 detections.
-Result1/2/7/9 have no source image in the reference (Src1/2/7/10 are missing large blobs; Result9's scene is absent).
+  Result6.jpg = Src6/Dst6, README Test6 parameters: 15 detections;
+  Result7.jpg = Src8/Dst8 (not in the README table; the view shows the Src8 scene: the gear top left, two
+      overlapping E-clips top right, one clip bottom left; the template is the 200x200 clip Dst8): 3 detections,
+      score order.  Its parameters are unpublished (all fitted); the values chosen are README Test1's (TargetNum 5,
+      Overlap 0.8, Score 0.8, Tol 180), which reproduce the count.  It is the one shipped output whose result depends
+      on filterWithRotatedRect KEEPING an overlapping pair (TemplateMatcher.cpp:1133-1194; MatchToolDlg.cpp:1071):
+      the two right-hand boxes overlap by between 0.3 and 0.4 of the box area, so MaxOverlap <= 0.3 deletes label 2
+      (``overlap_count``).  Its third cross is drawn with the vertical bar one column left of the box's middle
+      column, so this pin reads crosses by their strongest row / column (``cross_bars``).
+Result1/2/9 have no source image in the reference (Src1/2/10 are missing large blobs; Result9's scene is absent).
 
 Run from the repo root with the reference at /root/reference (this container only); the outputs are committed.
 """
@@ -83,10 +91,18 @@ PINS = [
          # is what it shows, not the salt itself
          perturbation=dict(salt=2, frac=0.01, fitted=True,
                            full_order_rate={"0.003": "6/32", "0.01": "10/32", "0.03": "20/32"})),
+    dict(name="result7_src8", screenshot="Result7.jpg", source="Src8.bmp", template="Dst8.bmp", count=3,
+         params=dict(max_pos=5, max_overlap=0.8, score=0.8, tolerance_angle=180.0), published=None,
+         fitted=["max_overlap", "max_pos", "score", "tolerance_angle"], order="score",
+         labels=[[0, 222, 459], [1, 470, 226], [2, 614, 263]], inferred=[], cross_bars=True,
+         # detections at MaxOverlap 0.3 / 0.4 (the oracle; everything else as ``params``): the overlapping pair
+         # is kept only above its overlap ratio
+         overlap_count={"0.3": 2, "0.4": 3}),
 ]
 
 
-def crosses(path):
+def crosses(path, bars=False):
+    """centre crosses of a screenshot; ``bars``: test the strongest row / column instead of the middle ones"""
     im = np.asarray(Image.open(path).convert("RGB")).astype(int)
     r, g, b = im[..., 0], im[..., 1], im[..., 2]
     lab, _ = ndimage.label((g > 150) & (r < 120) & (b < 120))
@@ -94,8 +110,8 @@ def crosses(path):
     for i, sl in enumerate(ndimage.find_objects(lab)):
         h, w = sl[0].stop - sl[0].start, sl[1].stop - sl[1].start
         m = lab[sl] == i + 1
-        if 10 <= h <= 13 and 10 <= w <= 13 and m[h // 2, :].sum() >= w - 2 and m[:, w // 2].sum() >= h - 2 \
-                and m.sum() <= 3 * (w + h):
+        row, col = (m.sum(axis=1).max(), m.sum(axis=0).max()) if bars else (m[h // 2, :].sum(), m[:, w // 2].sum())
+        if 10 <= h <= 13 and 10 <= w <= 13 and row >= w - 2 and col >= h - 2 and m.sum() <= 3 * (w + h):
             ys, xs = np.nonzero(m)
             out.append([round(float(sl[1].start + xs.mean()), 2), round(float(sl[0].start + ys.mean()), 2)])
     return [im.shape[1], im.shape[0]], sorted(out)
@@ -110,7 +126,8 @@ def main():
             if f == "Src6.jpg":
                 continue   # already committed as tests/golden/Src6.jpg
             shutil.copyfile(os.path.join(REF, "Test Images", f), dst)
-        p["display"], p["crosses"] = crosses(os.path.join(REF, "Result Images", p["screenshot"]))
+        p["display"], p["crosses"] = crosses(os.path.join(REF, "Result Images", p["screenshot"]),
+                                             p.get("cross_bars", False))
     with open(os.path.join(OUT, "reference_pins.json"), "w") as fh:
         json.dump(PINS, fh, indent=1)
 

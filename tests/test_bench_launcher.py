@@ -33,7 +33,19 @@ def test_gpus_mismatch_is_refused():
 
 def test_default_is_one_rank():
     out = subprocess.run([sys.executable, BENCH, "--dry-run"], capture_output=True, text=True, timeout=60, env=_env())
-    assert out.returncode == 0 and json.loads(out.stdout) == {"rank": 0, "world": 1, "local_rank": 0}
+    assert out.returncode == 0 and json.loads(out.stdout) == {"rank": 0, "world": 1, "local_rank": 0,
+                                                              "workload": "src7"}
+
+
+def test_config3_shards_sources_over_ranks():
+    """--workload config3 (BASELINE.json configs[3]): the 64 sources of the job split into contiguous blocks, one per
+    rank the launcher starts (strong scaling over --gpus N)."""
+    out = subprocess.run([sys.executable, BENCH, "--workload", "config3", "--gpus", "2", "--dry-run"],
+                         capture_output=True, text=True, timeout=240, env=_env())
+    assert out.returncode == 0, out.stderr
+    ranks = sorted((r["rank"], r["world"], r["workload"], tuple(r["sources"]))
+                   for r in (json.loads(m) for m in re.findall(r"\{[^{}]*\}", out.stdout)))
+    assert ranks == [(0, 2, "config3", (0, 32)), (1, 2, "config3", (32, 64))]
 
 
 def _bench_module():

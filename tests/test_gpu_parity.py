@@ -44,12 +44,15 @@ def test_pyr_down(hip, shape):
                                    (127, 255), (128, 256), (129, 258), (130, 514), (100, 333), (521, 762),
                                    (1518, 2012), (3036, 4024)])
 @pytest.mark.parametrize("seg", [0, 1, 2, 3])
-def test_pyr_down2(hip, shape, seg):
+@pytest.mark.parametrize("rows", [0, 16, 32])
+def test_pyr_down2(hip, shape, seg, rows):
     """Two levels in one launch (k_pyr_down2) = two oracle pyrDowns: strip edges at both levels (widths around the
-    64-column level-2 strip), odd and tiny sizes, runs starting mid-image (seg 1-3 chunks per workgroup)."""
+    64-column level-2 strip), odd and tiny sizes, runs starting mid-image (seg 1-3 chunks per workgroup), with the
+    level-1 chunk height the search would choose (rows 0: 16 for most single images) and each height forced, so the
+    ring carry at a run start is pinned for both 16- and 32-row chunks on every shape."""
     rng = np.random.default_rng(shape[0] * 11 + shape[1] + seg)
     img = rng.integers(0, 256, shape, dtype=np.uint8)
-    b, c = hip.pyr_down2(img, seg)
+    b, c = hip.pyr_down2(img, seg, rows)
     ob = oracle.pyr_down(img)
     assert np.array_equal(b, ob)
     assert np.array_equal(c, oracle.pyr_down(ob))

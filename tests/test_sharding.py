@@ -174,3 +174,82 @@ def test_match_sharded_gloo_real_searches():
     assert sum(len(e) for e in exp) >= n   # real detections in every source
     for r in range(world):
         assert got[r] == exp, r
+
+
+def _views_of(per_source, cap_buf, runs):
+    """per-source result tuples -> match_staged_array-style (counts, results) views, split into `runs` (one per
+    context); the buffer beyond each count holds garbage, as a reused result buffer does."""
+    out, pos = [], 0
+    for n in runs:
+        part = per_source[pos:pos + n]
+        cnt = np.array([len(r) for r in part], np.int32)
+        arr = np.full((n, cap_buf, 12), 777.0)
+        for i, res in enumerate(part):
+            for j, r in enumerate(res):
+                arr[i, j] = r
+        out.append((cnt, arr))
+        pos += n
+    return out
+
+
+def _array_worker(rank, world, port, n, q):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        a, b = sharding.shard_range(n, world, rank)
+        mine = _expected(_sources(n))[a:b]
+        k = b - a
+        views = _views_of(mine, 6, [k // 2, k - k // 2])      # two contexts per rank
+        cnt, arr = sharding.gather_result_arrays(views, n, cap=4)
+        q.put((rank, cnt.tolist(), arr.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_result_arrays_gloo():
+    """bench.py --workload config3's per-step exchange (world 2, gloo): each rank's context views all-gathered into
+    the whole job's (counts, results) in source order, equal to the object path (gather_results)."""
+    n, world = 9, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_array_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        rank, cnt, arr = q.get(timeout=120)
+        got[rank] = (cnt, arr)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    exp = _expected(_sources(n))
+    for r in range(world):
+        cnt, arr = got[r]
+        assert cnt == [len(e) for e in exp]
+        assert [[tuple(arr[i][j]) for j in range(cnt[i])] for i in range(n)] == exp
+        # padding is zeroed, not the stale buffer contents
+        assert all(v == 0.0 for i in range(n) for j in range(cnt[i], 4) for v in arr[i][j])
+
+
+def test_pack_result_arrays_matches_pack_results():
+    per = _expected(_sources(7))
+    views = _views_of(per, 5, [3, 0, 4])
+    assert np.array_equal(sharding.pack_result_arrays(views, 8, 4), sharding.pack_results(per, 8, 4))
+    with pytest.raises(ValueError):
+        sharding.pack_result_arrays(views, 8, 2)      # a source with 3 results over capacity 2
+    with pytest.raises(ValueError):
+        sharding.pack_result_arrays(views, 6, 4)      # 7 sources, 6 slots
+
+
+def test_config3_sources_shard_by_index():
+    """configs[3]'s sources depend only on their index: a rank's block equals the same slice of the whole batch."""
+    from fastest_image_pattern_matching_amd import synth
+
+    full, t = synth.batch_sources(5, size=96, tsize=16)
+    for a, b in [(0, 2), (2, 5), (4, 5)]:
+        part, t2 = synth.batch_sources(b - a, size=96, tsize=16, first=a)
+        assert np.array_equal(t, t2) and all(np.array_equal(x, y) for x, y in zip(part, full[a:b]))
