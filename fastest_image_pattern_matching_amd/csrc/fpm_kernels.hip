@@ -4345,6 +4345,14 @@ void launch_roi_tables(const RoiArgs& a, hipStream_t st) {
 // (5-6 waves); with it (61 VGPRs at batch 8), batch 8 at 7 waves 458, batch 4 / 8 / 12 at 8 waves 448 / 450 / 446
 // (scripts/gpu_kpass_mb.sh, profiles/r03_i)
 constexpr int kWarpFootBatch = 12, kWarpWaves = 8;
+// FPM_GRID_WARP / FPM_GRID_CORR / FPM_GRID_SMALL (> 0): caps on the workgroup counts of the sampler, the correlation
+// and the small-template kernel (scheduling knobs for concurrent contexts: every one of these kernels loops over its
+// work, so the results do not depend on the grid); unset or 0: the defaults below
+static int grid_cap_env(const char* v) { return v && atoi(v) > 0 ? atoi(v) : 0; }
+static const int kGridWarp = grid_cap_env(getenv("FPM_GRID_WARP"));
+static const int kGridCorr = grid_cap_env(getenv("FPM_GRID_CORR"));
+static const int kGridSmall = grid_cap_env(getenv("FPM_GRID_SMALL"));
+static int capped(int grid, int cap) { return cap > 0 && grid > cap ? cap : grid; }
 void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0 || a.equal1) return;
     const long tiles = (long)a.slot_cap * ((a.th + 6 + ROI_T - 1) / ROI_T) * ((a.tw + 6 + ROI_T - 1) / ROI_T);
@@ -4360,7 +4368,8 @@ void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
         const long want3 = (tiles / 3 + 3) / 4;
         // 7 waves per SIMD with the first ROI's tables requested before the staging (8 would spill them): microbenchmark
         // 405.5 / 406.3 -> 400.6 / 402.0 us (round 3)
-        hipLaunchKernelGGL((k_roi_warp3<7, kFtPitch, 0>), dim3((int)(want3 < 16384 ? want3 : 16384)), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((k_roi_warp3<7, kFtPitch, 0>), dim3(capped((int)(want3 < 16384 ? want3 : 16384), kGridWarp)),
+                           dim3(256), 0, st, a);
         return;
     }
     hipLaunchKernelGGL((k_roi_warp<kWarpFootBatch, 0, kWarpWaves>), dim3(grid), dim3(256), 0, st, a);
@@ -4383,7 +4392,7 @@ static void launch_corr_regs(const RoiArgs& a, long items, size_t lds, hipStream
         // ... and at 8 k-steps since the load addressing is scalar (136 VGPRs at 3 waves, 4 spilled at 4 waves: Src7
         // layer 1 107.7 -> 99.4 us per 43-source microbenchmark launch, profiles/r03_y)
         if (NK == 4 && lds * 4 <= kLdsPerCu) {
-            const int grid = (int)(items < 256 * 4 ? items : 256 * 4);
+            const int grid = capped((int)(items < 256 * 4 ? items : 256 * 4), kGridCorr);
             hipLaunchKernelGGL((k_roi_corr<0, true, 4, NK, false, 1, true>), dim3(grid), dim3(256), lds, st, a);
             return;
         }
@@ -4391,13 +4400,13 @@ static void launch_corr_regs(const RoiArgs& a, long items, size_t lds, hipStream
         // (43 Src7 sources: layer 0 269.8 -> 241.1 us, profiles/r04/mb_r04e.txt; layer 1 103.0 -> 93.5 us,
         // profiles/r04/mbl1_r04g.txt; host-checked)
         if ((NK == 8 || NK == 12) && lds * 4 <= kLdsPerCu) {
-            const int grid = (int)(items < 256 * 4 ? items : 256 * 4);
+            const int grid = capped((int)(items < 256 * 4 ? items : 256 * 4), kGridCorr);
             hipLaunchKernelGGL((k_roi_corr<0, true, 4, NK, false, 1, true, true>), dim3(grid), dim3(256), lds, st, a);
             return;
         }
         // row results staged in LDS and flushed during the next item's staging (SE; Src7 microbenchmark at 43 sources:
         // layer 0 293.6 -> 264.4 us, layer 1 124.2 -> 115.4, bit-identical)
-        const int grid = (int)(items < 256 * kCorrWaves ? items : 256 * kCorrWaves);
+        const int grid = capped((int)(items < 256 * kCorrWaves ? items : 256 * kCorrWaves), kGridCorr);
         hipLaunchKernelGGL((k_roi_corr<0, true, kCorrWaves, NK, false, 1, true>), dim3(grid), dim3(256), lds, st, a);
     } else {
         const int grid = (int)(items < kCorrRunWGs ? items : kCorrRunWGs);
@@ -4452,7 +4461,7 @@ void launch_roi_small(const RoiArgs& a, hipStream_t st) {
         return;
     }
     const size_t lds = (size_t)small_layout(a.tw, a.th).total;
-    const int grid = a.slot_cap < 8192 ? a.slot_cap : 8192;
+    const int grid = capped(a.slot_cap < 8192 ? a.slot_cap : 8192, kGridSmall);
     // 4 waves per SIMD where 4 workgroups' LDS fit a CU (Src7 layers 5 and 4: 46.8 -> 42.4 and 54.7 -> 47.4 us per
     // 43-source launch despite a 48-byte spill; 5 waves spill 176 bytes and measured slower), else 3
     if (a.prev_rec) {   // small batches only (the engine's rule): occupancy matters less than spills (3 vs 28 VGPRs)
@@ -4598,9 +4607,10 @@ __global__ __launch_bounds__(256) void k_overlap_pairs(const OvRect* __restrict_
         }
         if (lane == 0) { offcnt[2 * i] = base; offcnt[2 * i + 1] = nd; }
     }
-    // lists / offcnt / meta live in mapped pinned host memory (not coherent by default): make every store visible
-    // at system scope before the kernel ends, as k_pack does
-    __threadfence_system();
+    // lists / offcnt live in mapped pinned host memory: the host reads them only after the stream's next copy and
+    // hipStreamSynchronize, which make the kernel's stores visible to it (HIP's stream-order and synchronisation
+    // semantics for host-pinned memory).  A system-scope fence here in every workgroup (round 4) wrote the L2 back once
+    // per workgroup: +80 us on the Src10 +-180 tail (0.28 -> 0.36 ms, scripts/gpu_tail_ab.sh, profiles/r05b)
 }
 
 void launch_overlap_pairs(const OvRect* r, const float4* box, int n, double max_overlap, int32_t* lists, int list_cap,
