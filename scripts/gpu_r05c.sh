@@ -23,3 +23,6 @@ run s768 FPM_GRID_SMALL=768
 run s512 FPM_GRID_SMALL=512
 run w1536c768 FPM_GRID_WARP=1536 FPM_GRID_CORR=768
 run base2 FPM_NONE=1
+# the round-2 fused sampler + correlation (k_roi_fused, FPM_EXPERIMENTAL) against today's split chain, 43 sources
+MB_NSRC=43 timeout -k 10 300 ./build/fused_bench 10 > gpurun_out/fused_r05c.txt 2>&1 || { tail -5 gpurun_out/fused_r05c.txt; exit 1; }
+tail -12 gpurun_out/fused_r05c.txt
