@@ -1842,19 +1842,13 @@ void launch_cand_init(const CandInitArgs& a, hipStream_t st) {
 // 106.4 for k_warp + k_ncc_tile + k_nms; round-3 ablations (a profiling build, since removed from the product) put
 // 21 us in the taps, 19 in the correlation, 3 in the peak loop.
 constexpr int kTopThreads = 256;   // k_top_fused workgroup (measured: 512 threads per job no faster)
-__global__ __launch_bounds__(kTopThreads) void k_top_fused(const WarpJob* __restrict__ wjobs,
-                                                           const NccJob* __restrict__ njobs,
-                                                           NmsArgs a, int32_t* zero, int nzero,
-                                                           CandInitArgs ci, int ci_mode, const int32_t* order) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t tf_lds[];
-    __shared__ float sv[kTopThreads / 64];
-    __shared__ int si[kTopThreads / 64];
-    __shared__ Peak spk[kNmsInitCap];   // ci_mode != 0: the job's peaks for cand_init_job
-    __shared__ int sbase;
+// one (source, angle) job of k_top_fused (returns when the job is done; the caller separates jobs by a barrier)
+__device__ __forceinline__ void top_fused_job(int job, const WarpJob* __restrict__ wjobs,
+                                              const NccJob* __restrict__ njobs, const NmsArgs& a,
+                                              const CandInitArgs& ci, int ci_mode, uint32_t* tf_lds, float* sv,
+                                              int* si, Peak* spk, int* sbase_p) {
+    int& sbase = *sbase_p;
     const int tid = threadIdx.x;
-    if (blockIdx.x == 0)
-        for (int i = tid; i < nzero; i += kTopThreads) zero[i] = 0;
-    const int job = order ? order[blockIdx.x] : (int)blockIdx.x;
     const WarpJob& w = wjobs[job];
     const NccJob& j = njobs[job];
     const int dw = w.dw, dh = w.dh, cpw = ((dw + 3) >> 2) + 1;   // canvas words per row (+1: the funnel reads)
@@ -1987,6 +1981,25 @@ __global__ __launch_bounds__(kTopThreads) void k_top_fused(const WarpJob* __rest
     if (ci_mode) cand_init_job(ci, ci_mode, job, cnt, spk, &sbase);
 }
 
+// jobs k = blockIdx.x, + gridDim.x, ... in `order` (the grid may be smaller than the job count: FPM_GRID_TOP)
+__global__ __launch_bounds__(kTopThreads) void k_top_fused(const WarpJob* __restrict__ wjobs,
+                                                           const NccJob* __restrict__ njobs,
+                                                           NmsArgs a, int32_t* zero, int nzero,
+                                                           CandInitArgs ci, int ci_mode, const int32_t* order,
+                                                           int njobs_n) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t tf_lds[];
+    __shared__ float sv[kTopThreads / 64];
+    __shared__ int si[kTopThreads / 64];
+    __shared__ Peak spk[kNmsInitCap];   // ci_mode != 0: the job's peaks for cand_init_job
+    __shared__ int sbase;
+    if (blockIdx.x == 0)
+        for (int i = threadIdx.x; i < nzero; i += kTopThreads) zero[i] = 0;
+    for (int k = blockIdx.x; k < njobs_n; k += gridDim.x) {
+        if (k != (int)blockIdx.x) __syncthreads();   // the previous job is done with the LDS
+        top_fused_job(order ? order[k] : k, wjobs, njobs, a, ci, ci_mode, tf_lds, sv, si, spk, &sbase);
+    }
+}
+
 size_t top_fused_lds(int bw, int bh, int tw, int th) {
     const int cpw = ((bw + 3) >> 2) + 1, ntw = (tw + 3) >> 2;
     const size_t map = (size_t)std::max(bw - tw + 1, 0) * std::max(bh - th + 1, 0);
@@ -2024,8 +2037,13 @@ void launch_top_fused(const WarpJob* wjobs, const NccJob* njobs, const NmsArgs& 
                      mode);
         std::abort();
     }
-    hipLaunchKernelGGL(k_top_fused, dim3(njobs_n), dim3(kTopThreads), lds, st, wjobs, njobs, a, zero, nzero,
-                       fuse ? *ci : cz, mode, order);
+    // FPM_GRID_TOP: workgroup cap (a scheduling knob: the jobs loop; read when a search is recorded), 0 / unset: one
+    // workgroup per job
+    const char* gte = getenv("FPM_GRID_TOP");
+    const int grid_cap = gte && atoi(gte) > 0 ? atoi(gte) : 0;
+    const int grid = grid_cap > 0 && njobs_n > grid_cap ? grid_cap : njobs_n;
+    hipLaunchKernelGGL(k_top_fused, dim3(grid), dim3(kTopThreads), lds, st, wjobs, njobs, a, zero, nzero,
+                       fuse ? *ci : cz, mode, order, njobs_n);
 }
 
 // ============================================================================================== K6+K7+K8
@@ -4345,14 +4363,17 @@ void launch_roi_tables(const RoiArgs& a, hipStream_t st) {
 // (5-6 waves); with it (61 VGPRs at batch 8), batch 8 at 7 waves 458, batch 4 / 8 / 12 at 8 waves 448 / 450 / 446
 // (scripts/gpu_kpass_mb.sh, profiles/r03_i)
 constexpr int kWarpFootBatch = 12, kWarpWaves = 8;
-// FPM_GRID_WARP / FPM_GRID_CORR / FPM_GRID_SMALL (> 0): caps on the workgroup counts of the sampler, the correlation
-// and the small-template kernel (scheduling knobs for concurrent contexts: every one of these kernels loops over its
-// work, so the results do not depend on the grid); unset or 0: the defaults below
-static int grid_cap_env(const char* v) { return v && atoi(v) > 0 ? atoi(v) : 0; }
-static const int kGridWarp = grid_cap_env(getenv("FPM_GRID_WARP"));
-static const int kGridCorr = grid_cap_env(getenv("FPM_GRID_CORR"));
-static const int kGridSmall = grid_cap_env(getenv("FPM_GRID_SMALL"));
+// Workgroup caps of the looping kernels (every one of them loops over its work, so the results do not depend on the
+// grid).  With several contexts in flight (the bench: three HIP streams), a grid of one workgroup per work item keeps
+// the kernel's queue ahead of the other streams' kernels for its whole run; a persistent grid of the kernel's own
+// residency leaves the slots its workgroups free at the end to the other contexts.  Measured on the bench (128
+// Src7 sources over 3 contexts, one box, profiles/r05c, r05d): k_roi_small capped at its residency 33.27-33.52k ->
+// 33.93-34.23k searches/s, the sampler at 6-7 workgroups per CU +0.5 % more.  FPM_GRID_WARP / FPM_GRID_CORR /
+// FPM_GRID_SMALL (read when a search is recorded): N > 0 caps the kernel at N workgroups, 0 lifts the cap (the
+// uncapped grids of round 4), unset: the defaults at each launch below.
+static int grid_cap_env(const char* v, int dflt) { return v ? (atoi(v) > 0 ? atoi(v) : 0) : dflt; }
 static int capped(int grid, int cap) { return cap > 0 && grid > cap ? cap : grid; }
+constexpr int kCUs = 256;   // MI355X
 void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0 || a.equal1) return;
     const long tiles = (long)a.slot_cap * ((a.th + 6 + ROI_T - 1) / ROI_T) * ((a.tw + 6 + ROI_T - 1) / ROI_T);
@@ -4368,7 +4389,7 @@ void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
         const long want3 = (tiles / 3 + 3) / 4;
         // 7 waves per SIMD with the first ROI's tables requested before the staging (8 would spill them): microbenchmark
         // 405.5 / 406.3 -> 400.6 / 402.0 us (round 3)
-        hipLaunchKernelGGL((k_roi_warp3<7, kFtPitch, 0>), dim3(capped((int)(want3 < 16384 ? want3 : 16384), kGridWarp)),
+        hipLaunchKernelGGL((k_roi_warp3<7, kFtPitch, 0>), dim3(capped((int)(want3 < 16384 ? want3 : 16384), grid_cap_env(getenv("FPM_GRID_WARP"), 7 * kCUs))),
                            dim3(256), 0, st, a);
         return;
     }
@@ -4392,7 +4413,7 @@ static void launch_corr_regs(const RoiArgs& a, long items, size_t lds, hipStream
         // ... and at 8 k-steps since the load addressing is scalar (136 VGPRs at 3 waves, 4 spilled at 4 waves: Src7
         // layer 1 107.7 -> 99.4 us per 43-source microbenchmark launch, profiles/r03_y)
         if (NK == 4 && lds * 4 <= kLdsPerCu) {
-            const int grid = capped((int)(items < 256 * 4 ? items : 256 * 4), kGridCorr);
+            const int grid = capped((int)(items < 256 * 4 ? items : 256 * 4), grid_cap_env(getenv("FPM_GRID_CORR"), 0));
             hipLaunchKernelGGL((k_roi_corr<0, true, 4, NK, false, 1, true>), dim3(grid), dim3(256), lds, st, a);
             return;
         }
@@ -4400,13 +4421,13 @@ static void launch_corr_regs(const RoiArgs& a, long items, size_t lds, hipStream
         // (43 Src7 sources: layer 0 269.8 -> 241.1 us, profiles/r04/mb_r04e.txt; layer 1 103.0 -> 93.5 us,
         // profiles/r04/mbl1_r04g.txt; host-checked)
         if ((NK == 8 || NK == 12) && lds * 4 <= kLdsPerCu) {
-            const int grid = capped((int)(items < 256 * 4 ? items : 256 * 4), kGridCorr);
+            const int grid = capped((int)(items < 256 * 4 ? items : 256 * 4), grid_cap_env(getenv("FPM_GRID_CORR"), 0));
             hipLaunchKernelGGL((k_roi_corr<0, true, 4, NK, false, 1, true, true>), dim3(grid), dim3(256), lds, st, a);
             return;
         }
         // row results staged in LDS and flushed during the next item's staging (SE; Src7 microbenchmark at 43 sources:
         // layer 0 293.6 -> 264.4 us, layer 1 124.2 -> 115.4, bit-identical)
-        const int grid = capped((int)(items < 256 * kCorrWaves ? items : 256 * kCorrWaves), kGridCorr);
+        const int grid = capped((int)(items < 256 * kCorrWaves ? items : 256 * kCorrWaves), grid_cap_env(getenv("FPM_GRID_CORR"), 0));
         hipLaunchKernelGGL((k_roi_corr<0, true, kCorrWaves, NK, false, 1, true>), dim3(grid), dim3(256), lds, st, a);
     } else {
         const int grid = (int)(items < kCorrRunWGs ? items : kCorrRunWGs);
@@ -4461,7 +4482,11 @@ void launch_roi_small(const RoiArgs& a, hipStream_t st) {
         return;
     }
     const size_t lds = (size_t)small_layout(a.tw, a.th).total;
-    const int grid = capped(a.slot_cap < 8192 ? a.slot_cap : 8192, kGridSmall);
+    // default cap: the kernel's residency (workgroups per CU: its waves per SIMD, or fewer where the LDS runs out)
+    const int wpe = a.prev_rec ? 3 : (lds * 4 <= kLdsPerCu ? 4 : 3);
+    const int per_cu = (int)std::min<size_t>((size_t)wpe, kLdsPerCu / std::max<size_t>(lds, 1));
+    const int grid = capped(a.slot_cap < 8192 ? a.slot_cap : 8192,
+                            grid_cap_env(getenv("FPM_GRID_SMALL"), std::max(per_cu, 1) * kCUs));
     // 4 waves per SIMD where 4 workgroups' LDS fit a CU (Src7 layers 5 and 4: 46.8 -> 42.4 and 54.7 -> 47.4 us per
     // 43-source launch despite a 48-byte spill; 5 waves spill 176 bytes and measured slower), else 3
     if (a.prev_rec) {   // small batches only (the engine's rule): occupancy matters less than spills (3 vs 28 VGPRs)

@@ -182,6 +182,28 @@ def test_src7_top_layer_forms(gpu_matcher_factory, templates, monkeypatch, top_f
     assert_same_results(gpu, orc, f"src7 top_fused={top_fused}")
 
 
+@pytest.mark.parametrize("caps", [{}, {"FPM_GRID_TOP": "7", "FPM_GRID_SMALL": "5", "FPM_GRID_WARP": "37",
+                                      "FPM_GRID_CORR": "11"},
+                                  {"FPM_GRID_TOP": "1000", "FPM_GRID_SMALL": "768", "FPM_GRID_WARP": "1536"},
+                                  {"FPM_GRID_SMALL": "0", "FPM_GRID_WARP": "0"}])
+def test_src7_grid_caps(gpu_matcher_factory, templates, monkeypatch, caps):
+    """The workgroup caps of the persistent forms (FPM_GRID_TOP / _SMALL / _WARP / _CORR; read when a fresh context
+    records its search; {} = the defaults, "0" = uncapped grids): with tiny caps every workgroup of the fused top layer, the small-template refinement, the
+    sampler and the correlation loops over many jobs; a batch of seven Src7 sources (fused top layer: >= 256 jobs)
+    equals the oracle."""
+    for k, v in caps.items():
+        monkeypatch.setenv(k, v)
+    t = templates["Dst7"]
+    srcs = [synth.src7_scene(t, seed=21 + i)[0] for i in range(7)]
+    m = gpu_matcher_factory(max_pos=3, tolerance_angle=180.0, score=0.7)
+    assert m.learnPattern(t)
+    m.stage(srcs)
+    got = [[r.as_tuple() for r in rr] for rr in m.match_staged()]
+    o = oracle.OracleMatcher().set(max_pos=3, tolerance_angle=180.0, score=0.7)
+    o.learnPattern(t)
+    assert got == [o.match(s) for s in srcs]
+
+
 def test_top_fused_lds_threshold(gpu_matcher_factory, templates, monkeypatch):
     """k_top_fused forced (FPM_TOP_FUSED=1) on top canvases either side of its LDS limit (64 KB minus the kernel's
     static LDS, read with hipFuncGetAttributes): Dst10 at +-180 over square sources whose largest rotated top canvas
