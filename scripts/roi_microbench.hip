@@ -360,6 +360,11 @@ int main(int argc, char** argv) {
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 3, 12, false, 1, true, true>), dim3(grid), dim3(256), lds, 0, a); }, "corrA SE DMA 3w");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 4, 12, false, 1, true, true>), dim3((int)std::min<long>(items, 1024)), dim3(256), lds, 0, a); }, "corrA SE DMA 4w");
         timeit([&] { hipLaunchKernelGGL((k_roi_corr<0, true, 4, 12, false, 1, false, true>), dim3((int)std::min<long>(items, 1024)), dim3(256), lds, 0, a); }, "corrA DMA 4w");
+        // round 5: the product form's phases (MODE ablations of k_roi_corr<., true, 4, 12, false, 1, true, true>)
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<2, true, 4, 12, false, 1, true, true>), dim3((int)std::min<long>(items, 1024)), dim3(256), lds, 0, a); }, "corrA SE DMA 4w no mfma+epi");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<5, true, 4, 12, false, 1, true, true>), dim3((int)std::min<long>(items, 1024)), dim3(256), lds, 0, a); }, "corrA SE DMA 4w no stores");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<6, true, 4, 12, false, 1, true, true>), dim3((int)std::min<long>(items, 1024)), dim3(256), lds, 0, a); }, "corrA SE DMA 4w no partials");
+        timeit([&] { hipLaunchKernelGGL((k_roi_corr<7, true, 4, 12, false, 1, true, true>), dim3((int)std::min<long>(items, 1024)), dim3(256), lds, 0, a); }, "corrA SE DMA 4w no rowsums");
         {
             const size_t lds_db = lds + 16 + (size_t)38 * a.roi_pitch;
             hipFuncSetAttribute((const void*)k_roi_corr<0, true, 2, 12, false, 1, true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_db);
