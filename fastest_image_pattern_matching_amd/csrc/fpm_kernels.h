@@ -215,6 +215,7 @@ void launch_top_fused(const WarpJob* wjobs, const NccJob* njobs, const NmsArgs& 
 void launch_roi_tables(const RoiArgs& a, hipStream_t st);
 void launch_roi_warp(const RoiArgs& a, hipStream_t st);
 void launch_roi_corr(const RoiArgs& a, hipStream_t st);
+bool launch_roi_corr16(const RoiArgs& a, hipStream_t st);   // false: the shape does not fit its form
 void launch_roi_eval(const RoiArgs& a, hipStream_t st);
 #ifdef FPM_EXPERIMENTAL   // measurement-only fused K6+K7 (scripts/fused_bench.hip; never in libfpm_hip.so)
 bool roi_fused_fits(int tw);           // the fused sampling + correlation kernel applies (templates <= 1024 wide)

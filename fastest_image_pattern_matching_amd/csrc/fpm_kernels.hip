@@ -3469,6 +3469,202 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
+// ---- K7, round 5: the register-A / LDS-DMA correlation with items of ONE 16-row M tile (k_roi_corr's band is two).
+// A k_roi_corr item waits for its 38 ROI rows (one LDS-DMA round trip) and two barriers before its matrix work, and
+// its 40 KB of LDS allow 4 items in flight per CU.  Here an item is (ROI, 16 template rows = one window-sum chunk):
+// 22 ROI rows (18 KB), a 2-wave workgroup (wave w takes the N tile of ROI rows 16 w .. 16 w + 15, both waves the
+// band's A fragments), about 22 KB of LDS, so 7 items are in flight per CU at the same waves per SIMD.  The price is
+// 22 / 16 staged rows per template row instead of 38 / 32, and the same banded MFMA count (two N tiles per M tile).
+// Outputs are k_roi_corr's exactly: the row dot products [t][49] (exact u32, through LDS as 16-byte runs during the
+// next item, SE), and the window-sum partial of the item's chunk (one 16-row chunk per item).
+constexpr int kB16Rows = kMmaRows, kB16Src = kB16Rows + 6;
+__host__ __device__ inline size_t roi_corr16_lds(int roi_pitch) {
+    return (size_t)kB16Src * roi_pitch + sizeof(uint32_t) * (2 * 7 * kB16Src + kB16Rows + kB16Rows * 49) + 64;
+}
+template <int NK, int WPE>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_corr16(RoiArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int NT = 128;
+    const int tw = a.tw, th = a.th, RW = tw + 6;
+    const int SBp = a.roi_pitch;
+    uint8_t* const SB = smem;                                   // kB16Src rows x SBp, bytes ^ 0x80
+    uint32_t* wi = (uint32_t*)(SB + (size_t)kB16Src * SBp);     // [row][dx] window sums of I
+    uint32_t* wq = wi + kB16Src * 7;                            // [row][dx] window sums of I^2
+    uint32_t* lts = wq + kB16Src * 7;                           // the band's template-row sums
+    uint32_t* rsb = lts + kB16Rows;                             // the band's [t][49] row results (16-byte aligned)
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int nband = (th + kB16Rows - 1) / kB16Rows;
+    const int rois = roi_count(a), items = rois * nband;
+    const int nwr = (RW + 3) >> 2;
+    const int g = lane >> 4, n = lane & 15;
+    const int txn = (RW + ROI_T - 1) / ROI_T;
+    const XcdSplit xs = xcd_split(items);
+    const int64_t span = xs.hi - xs.lo;
+    const int it_lo = xs.lo + (int)(span * xs.k / xs.nk), it_hi = xs.lo + (int)(span * (xs.k + 1) / xs.nk);
+    fpm_v4i Areg[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) Areg[k] = fpm_v4i{0, 0, 0, 0};
+    int a_band = -1;
+    int pv_slot = -1, pv_T0 = 0, pv_rb = 0;
+    auto flush = [&]() {   // the previous item's row results: LDS -> its [rb][49] range of the ROI's series
+        if (pv_slot < 0) return;
+        uint32_t* dst = a.rowsum + (((size_t)th * 49 + 3) & ~(size_t)3) * pv_slot + (size_t)pv_T0 * 49;
+        const int nw = pv_rb * 49, n16 = nw >> 2;
+        for (int i = tid; i < n16; i += NT) *(uint4*)(dst + 4 * i) = *(const uint4*)(rsb + 4 * i);
+        if (tid < (nw & 3)) dst[4 * n16 + tid] = rsb[4 * n16 + tid];
+    };
+    // item it's ROI rows wv + 2 i -> SB by LDS-DMA (one global_load_lds_dwordx4 per row and wave; lanes past the ROI
+    // width idle: those LDS chunks meet the template's zero padding only)
+    auto dma_rows = [&](int it) {
+        const int bd = it / rois, sl = it - bd * rois;
+        const int T0n = bd * kB16Rows, nsn = min(kB16Rows, th - T0n) + 6;
+        const uint8_t* rsrc = a.roi + (size_t)sl * a.roi_stride;
+        const uint32_t lane_off = ((uint32_t)(lane >> 1) << 10) + 16u * (uint32_t)(lane & 1);
+        const int wvu = __builtin_amdgcn_readfirstlane(wv);
+        const bool in_roi = lane < 2 * txn;
+#pragma unroll
+        for (int i = 0; i < (kB16Src + 1) / 2; ++i) {
+            const int r = wvu + 2 * i;
+            if (r < nsn && in_roi) {
+                const int R = T0n + r;
+                const uint8_t* gp = rsrc + ((size_t)((R >> 5) * txn) << 10) + (R & 31) * ROI_T + lane_off;
+                const uint32_t ldsa = __builtin_amdgcn_readfirstlane(lds_offset_of(SB + (size_t)r * SBp));
+                uint32_t keep;
+                asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                             "s_mov_b32 m0, %0"
+                             : "=&s"(keep) : "v"(gp), "s"(ldsa) : "memory");
+            }
+        }
+    };
+    for (int item = it_lo; item < it_hi; ++item) {
+        const int band = item / rois, slot = item - band * rois;
+        const int T0 = band * kB16Rows, rb = min(kB16Rows, th - T0), nsrc = rb + 6;
+        __syncthreads();   // the previous item is done with SB / wi / rsb
+        dma_rows(item);
+        flush();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (band != a_band) {   // this band's A fragments (both waves: the item's one M tile) and template-row sums
+            a_band = band;
+            if (tid < kB16Rows) lts[tid] = tid < rb ? (uint32_t)a.tsum[T0 + tid] : 0u;
+            const int8_t* ap = a.tmpl8 + (size_t)(T0 + n) * a.tp8 + 16 * g;
+#pragma unroll
+            for (int k = 0; k < NK; ++k)
+                if (k < a.nk) Areg[k] = *(const fpm_v4i*)(ap + 64 * k);
+        }
+        __syncthreads();
+        if (tid < 4 * nsrc) {
+            // row r's window sums by the quad of lanes 4r .. 4r + 3 (k_roi_corr's RS 1 form): full-row sums of I and I^2
+            // reduced by DPP within the quad, each lane subtracting the edge pixels of its windows dx = q, q + 4
+            const int r = tid >> 2, qq = tid & 3;
+            const int per = (nwr + 3) >> 2, k0 = qq * per, k1 = min(nwr, k0 + per);
+            const uint32_t* row = (const uint32_t*)(SB + (size_t)r * SBp);
+            uint32_t s1 = 0, s2 = 0;
+            int k = k0;
+            for (; k + 8 <= k1; k += 8) {
+                uint32_t x[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) x[u] = row[k + u] ^ 0x80808080u;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    s1 = __builtin_amdgcn_udot4(x[u], 0x01010101u, s1, false);
+                    s2 = __builtin_amdgcn_udot4(x[u], x[u], s2, false);
+                }
+            }
+            for (; k < k1; ++k) {
+                const uint32_t x = row[k] ^ 0x80808080u;
+                s1 = __builtin_amdgcn_udot4(x, 0x01010101u, s1, false);
+                s2 = __builtin_amdgcn_udot4(x, x, s2, false);
+            }
+            const uint32_t l0 = row[0] ^ 0x80808080u, l1 = row[1] ^ 0x80808080u;
+            const int wr = tw >> 2;
+            const uint32_t x0 = row[wr], x1 = row[wr + 1], x2 = row[wr + 2];
+            const uint32_t e0 = __builtin_amdgcn_alignbyte(x1, x0, (uint32_t)tw) ^ 0x80808080u;
+            const uint32_t e1 = __builtin_amdgcn_alignbyte(x2, x1, (uint32_t)tw) ^ 0x80808080u;
+            s1 += (uint32_t)__builtin_amdgcn_mov_dpp((int)s1, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+            s2 += (uint32_t)__builtin_amdgcn_mov_dpp((int)s2, 0xB1, 0xF, 0xF, false);
+            s1 += (uint32_t)__builtin_amdgcn_mov_dpp((int)s1, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+            s2 += (uint32_t)__builtin_amdgcn_mov_dpp((int)s2, 0x4E, 0xF, 0xF, false);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int dx = qq + 4 * h;
+                if (dx < 7) {
+                    const uint32_t ml0 = dx >= 4 ? 0xffffffffu : (1u << (8 * dx)) - 1u;
+                    const uint32_t ml1 = dx <= 4 ? 0u : (1u << (8 * (dx - 4))) - 1u;
+                    const uint32_t mr0 = dx >= 4 ? 0u : ~((1u << (8 * dx)) - 1u);
+                    const uint32_t mr1 = dx <= 4 ? 0xffffu : dx == 5 ? 0xff00u : 0u;
+                    const uint32_t a0 = l0 & ml0, a1 = l1 & ml1, b0 = e0 & mr0, b1 = e1 & mr1;
+                    uint32_t q1 = __builtin_amdgcn_udot4(a0, 0x01010101u, 0u, false);
+                    q1 = __builtin_amdgcn_udot4(a1, 0x01010101u, q1, false);
+                    q1 = __builtin_amdgcn_udot4(b0, 0x01010101u, q1, false);
+                    q1 = __builtin_amdgcn_udot4(b1, 0x01010101u, q1, false);
+                    uint32_t q2 = __builtin_amdgcn_udot4(a0, a0, 0u, false);
+                    q2 = __builtin_amdgcn_udot4(a1, a1, q2, false);
+                    q2 = __builtin_amdgcn_udot4(b0, b0, q2, false);
+                    q2 = __builtin_amdgcn_udot4(b1, b1, q2, false);
+                    wi[r * 7 + dx] = s1 - q1;
+                    wq[r * 7 + dx] = s2 - q2;
+                }
+            }
+        }
+        __syncthreads();
+        if (kMmaRows * wv < nsrc) {   // wave-uniform: wave 1's N tile exists
+            int sr = kMmaRows * wv + n;
+            if (sr >= nsrc) sr = 0;   // column outside the band: computed, never stored
+            const uint8_t* bp = SB + (size_t)sr * SBp + 16 * g;
+            fpm_v4i acc[7];
+            band_mfma_regs<NK>(Areg, bp, a.nk, acc);
+            const uint32_t kFix = 16384u * (uint32_t)tw;
+            int t0 = 4 * g;
+            asm volatile("" : "+v"(t0));
+            const int s_ = kMmaRows * wv + n;
+            const uint4 ts4 = *(const uint4*)(lts + t0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int t = t0 + r, dy = s_ - t;
+                if (t < rb && s_ < nsrc && dy >= 0 && dy < 7) {
+                    const uint32_t ts = r == 0 ? ts4.x : r == 1 ? ts4.y : r == 2 ? ts4.z : ts4.w;
+                    const uint32_t o = (uint32_t)(t * 49 + dy * 7);
+#pragma unroll
+                    for (int d = 0; d < 7; ++d) rsb[o + d] = (uint32_t)acc[d][r] + 128u * (wi[s_ * 7 + d] + ts) - kFix;
+                }
+            }
+        }
+        // the item's chunk partial of the window sums (positions k by lane pairs, 8 rows each, combined by DPP)
+        if (tid < 2 * 49) {
+            const int k = tid >> 1, half = tid & 1;
+            const int chunk = T0 >> 4;
+            const int pdy = k / 7, ddx = k - pdy * 7;
+            const int t0 = 8 * half, n8 = min(8, rb - t0);
+            uint32_t s1 = 0, x[8], y[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = (t0 + u + pdy) * 7 + ddx;
+                x[u] = u < n8 ? wi[i] : 0u;
+                y[u] = u < n8 ? wq[i] : 0u;
+            }
+            uint64_t s2 = 0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) { s1 += x[u]; s2 += y[u]; }
+            s1 += (uint32_t)__builtin_amdgcn_mov_dpp((int)s1, 0xB1, 0xF, 0xF, false);
+            const uint32_t lo = (uint32_t)s2, hi = (uint32_t)(s2 >> 32);
+            s2 += (uint64_t)(uint32_t)__builtin_amdgcn_mov_dpp((int)lo, 0xB1, 0xF, 0xF, false) |
+                  ((uint64_t)(uint32_t)__builtin_amdgcn_mov_dpp((int)hi, 0xB1, 0xF, 0xF, false) << 32);
+            if (half == 0 && chunk < a.nchunk) {
+                uint32_t kk = (uint32_t)k;
+                asm volatile("" : "+v"(kk));
+                const uint32_t wo = ((uint32_t)slot * (uint32_t)a.nchunk + (uint32_t)chunk) * 49u + kk;
+                a.wsum[wo] = s1;
+                a.wsq[wo] = s2;
+            }
+        }
+        pv_slot = slot; pv_T0 = T0; pv_rb = rb;
+    }
+    if (pv_slot >= 0) {   // the last item's row results
+        __syncthreads();
+        flush();
+    }
+}
+
 #ifdef FPM_EXPERIMENTAL   // measurement-only kernel (scripts/fused_bench.hip); the product Makefile never defines it
 // ---- K6+K7 fused (templates too large for k_roi_small): the ROI never leaves the CU.  A work unit is one ROI and
 // one run of consecutive 32-row template bands; a workgroup walks its run band by band:
@@ -4434,8 +4630,25 @@ static void launch_corr_regs(const RoiArgs& a, long items, size_t lds, hipStream
         hipLaunchKernelGGL((k_roi_corr<0, true, kCorrRunWaves, NK>), dim3(grid), dim3(256), lds, st, a);
     }
 }
+// k_roi_corr16 (16-row items, 2-wave workgroups): as many workgroups as the LDS holds per CU, persistent
+bool launch_roi_corr16(const RoiArgs& a, hipStream_t st) {
+    if (a.nk > 12 || (a.roi_pitch >> 4) > 64) return false;
+    const size_t lds = roi_corr16_lds(a.roi_pitch);
+    const int per_cu = (int)std::min<size_t>(8, kLdsPerCu / lds);
+    if (per_cu < 1) return false;
+    const long items = (long)a.slot_cap * ((a.th + kB16Rows - 1) / kB16Rows);
+    const int grid = capped((int)std::min<long>(items, (long)per_cu * kCUs), grid_cap_env(getenv("FPM_GRID_CORR"), 0));
+    if (a.nk <= 4) hipLaunchKernelGGL((k_roi_corr16<4, 4>), dim3(grid), dim3(128), lds, st, a);
+    else if (a.nk <= 8) hipLaunchKernelGGL((k_roi_corr16<8, 4>), dim3(grid), dim3(128), lds, st, a);
+    else hipLaunchKernelGGL((k_roi_corr16<12, 4>), dim3(grid), dim3(128), lds, st, a);
+    return true;
+}
+
 void launch_roi_corr(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0 || a.equal1) return;
+    // FPM_CORR16=1: the 16-row-item form (measurement switch while it is evaluated; read when a search is recorded)
+    const char* c16 = getenv("FPM_CORR16");
+    if (c16 && atoi(c16) == 1 && launch_roi_corr16(a, st)) return;
     const size_t lds = roi_corr_lds(a.roi_pitch, a.tw, a.rc, kCorrGlobalA);
     // register-A form where its staged rows fit one 64-lane pass and A fits 16 k-steps (templates <= 1024 wide);
     // the slot-major form below serves wider templates
