@@ -2,7 +2,7 @@
 # Submit one gpurun call, re-submitting only while the pool reports no free slot / box (exit status 3: nothing ran,
 # nothing was charged); any other status (including a failed command) ends it.  usage: gpurun_wait.sh TIMEOUT CMD
 T=$1; shift
-for i in $(seq 1 15); do
+for i in $(seq 1 ${GPURUN_ATTEMPTS:-15}); do
   /usr/local/graft/bin/gpurun --timeout "$T" -- "$@"
   rc=$?
   [ $rc -ne 3 ] && exit $rc
