@@ -18,4 +18,6 @@ run b256c4 --batch 256 --contexts 4
 run b96c3 --batch 96
 run b128c3p1024 -- FPM_PYR_WGS=1024
 run b128c3p2048 -- FPM_PYR_WGS=2048
+run b128c3w -- FPM_GRID_WARP=1792
 run b128c3b
+run b128c3wb -- FPM_GRID_WARP=1792
