@@ -4564,9 +4564,9 @@ constexpr int kWarpFootBatch = 12, kWarpWaves = 8;
 // the kernel's queue ahead of the other streams' kernels for its whole run; a persistent grid of the kernel's own
 // residency leaves the slots its workgroups free at the end to the other contexts.  Measured on the bench (128
 // Src7 sources over 3 contexts, one box, profiles/r05c, r05d): k_roi_small capped at its residency 33.27-33.52k ->
-// 33.93-34.23k searches/s.  The sampler at its residency (7 per CU) measured +0.5 % more (noise level: 34.07-34.16k
-// vs 33.93-34.12k, profiles/r05d, r05e) but stretched its own launches (roofline frac 0.209 -> 0.196): left uncapped
-// by default.  FPM_GRID_WARP / FPM_GRID_CORR /
+// 33.93-34.23k searches/s.  The sampler at its residency (7 per CU) +0.3-1.2 % more (profiles/r05f: 34.25k / 34.30k
+// vs 33.85k / 33.98k uncapped, alternated on one box), while its own launches stretch (the other contexts' kernels
+// share the chip during them: bench roofline frac 0.208 -> 0.195) -- the whole job is faster.  FPM_GRID_WARP / FPM_GRID_CORR /
 // FPM_GRID_SMALL (read when a search is recorded): N > 0 caps the kernel at N workgroups, 0 lifts the cap (the
 // uncapped grids of round 4), unset: the defaults at each launch below.
 static int grid_cap_env(const char* v, int dflt) { return v ? (atoi(v) > 0 ? atoi(v) : 0) : dflt; }
@@ -4587,7 +4587,7 @@ void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
         const long want3 = (tiles / 3 + 3) / 4;
         // 7 waves per SIMD with the first ROI's tables requested before the staging (8 would spill them): microbenchmark
         // 405.5 / 406.3 -> 400.6 / 402.0 us (round 3)
-        hipLaunchKernelGGL((k_roi_warp3<7, kFtPitch, 0>), dim3(capped((int)(want3 < 16384 ? want3 : 16384), grid_cap_env(getenv("FPM_GRID_WARP"), 0))),
+        hipLaunchKernelGGL((k_roi_warp3<7, kFtPitch, 0>), dim3(capped((int)(want3 < 16384 ? want3 : 16384), grid_cap_env(getenv("FPM_GRID_WARP"), 7 * kCUs))),
                            dim3(256), 0, st, a);
         return;
     }
