@@ -5,8 +5,9 @@ A step is one full TemplateMatcher::match pass (pyramid -> top-layer rotation sw
 refinement -> host filters) over a batch of ``--batch`` synthetic Src7 sources per GPU that are already
 resident in HBM (staged before timing; the PCIe upload is not in ``value``), split over ``--contexts`` contexts
 (one HIP stream each) that run as a stream of passes: a context relaunches as soon as its previous pass is
-finished, so host post-processing overlaps device work.  Defaults: 128 sources over 3 contexts (the throughput
-plateau of scripts/sweep_batch.sh: 21.5k searches/s at 32 / 2, 24.3k at 128 / 3, 24.5k at 192 / 3).  ``value`` = searches/s over all
+finished, so host post-processing overlaps device work.  Defaults: 192 sources over 3 contexts (round 5, one box,
+alternated: 34.17k / 34.23k searches/s at 128, 34.38k / 34.43k at 160, 34.51k / 34.52k at 192, 33.67k at 240;
+3 contexts beat 2 and 4 at every batch, profiles/r05f, r05g).  ``value`` = searches/s over all
 ranks.  Multi-GPU: one process per GPU (torchrun), every rank searches its own sources (weak scaling, no
 data-path collective); barrier + synchronize bracket the K timed steps and the max time over ranks is used.
 
@@ -302,7 +303,7 @@ def main():
     ap.add_argument("--workload", choices=("src7", "config3"), default="src7",
                     help="src7: BASELINE.json configs[1], the headline (default); config3: configs[3], 64 x 4096^2 "
                          "sources at a 1 deg top step sharded over the ranks")
-    ap.add_argument("--batch", type=int, default=128, help="src7: sources searched per GPU per step")
+    ap.add_argument("--batch", type=int, default=192, help="src7: sources searched per GPU per step")
     ap.add_argument("--sources", type=int, default=C3_SOURCES,
                     help="config3: sources of the whole job per step, sharded over the ranks")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (0 = skip)")
