@@ -5,6 +5,10 @@ TAG=${1:-r05_end}
 cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out
 bash scripts/gpu_kpass_mb.sh $TAG tests || exit $?
 cd $GRAFT_REPO_ROOT
+# the PMC traffic of this build's kernel pass, installed where the bench reads it (the committed copy is updated from
+# gpurun_out/pmc_bench_$TAG/summary.csv afterwards)
+bash scripts/pmc_bench.sh $TAG || exit $?
+cd $GRAFT_REPO_ROOT && cp gpurun_out/pmc_bench_$TAG/summary.csv profiles/latest/pmc_traffic.csv
 timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || exit $?
 tail -1 gpurun_out/smoke_$TAG.log
 timeout -k 10 400 python -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.log || exit $?
