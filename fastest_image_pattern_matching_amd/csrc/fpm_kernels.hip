@@ -4564,9 +4564,10 @@ constexpr int kWarpFootBatch = 12, kWarpWaves = 8;
 // the kernel's queue ahead of the other streams' kernels for its whole run; a persistent grid of the kernel's own
 // residency leaves the slots its workgroups free at the end to the other contexts.  Measured on the bench (128
 // Src7 sources over 3 contexts, one box, profiles/r05c, r05d): k_roi_small capped at its residency 33.27-33.52k ->
-// 33.93-34.23k searches/s.  The sampler at its residency (7 per CU) +0.3-1.2 % more (profiles/r05f: 34.25k / 34.30k
-// vs 33.85k / 33.98k uncapped, alternated on one box), while its own launches stretch (the other contexts' kernels
-// share the chip during them: bench roofline frac 0.208 -> 0.195) -- the whole job is faster.  FPM_GRID_WARP / FPM_GRID_CORR /
+// 33.93-34.23k searches/s.  The sampler at its residency (7 per CU) gained +0.3-1.2 % at 128 sources per step
+// (profiles/r05f) but nothing at the bench's 192 (34.58k / 34.59k vs 34.56k / 34.54k uncapped, 34.61k / 34.66k at
+// 2688, alternated, profiles/r05j), while its static task ranges make each launch 7 % slower on its own (239 vs
+// 222 us at 64 sources): uncapped by default.  FPM_GRID_WARP / FPM_GRID_CORR /
 // FPM_GRID_SMALL (read when a search is recorded): N > 0 caps the kernel at N workgroups, 0 lifts the cap (the
 // uncapped grids of round 4), unset: the defaults at each launch below.
 static int grid_cap_env(const char* v, int dflt) { return v ? (atoi(v) > 0 ? atoi(v) : 0) : dflt; }
@@ -4587,7 +4588,7 @@ void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
         const long want3 = (tiles / 3 + 3) / 4;
         // 7 waves per SIMD with the first ROI's tables requested before the staging (8 would spill them): microbenchmark
         // 405.5 / 406.3 -> 400.6 / 402.0 us (round 3)
-        hipLaunchKernelGGL((k_roi_warp3<7, kFtPitch, 0>), dim3(capped((int)(want3 < 16384 ? want3 : 16384), grid_cap_env(getenv("FPM_GRID_WARP"), 7 * kCUs))),
+        hipLaunchKernelGGL((k_roi_warp3<7, kFtPitch, 0>), dim3(capped((int)(want3 < 16384 ? want3 : 16384), grid_cap_env(getenv("FPM_GRID_WARP"), 0))),
                            dim3(256), 0, st, a);
         return;
     }
