@@ -3971,8 +3971,18 @@ __host__ __device__ inline SmallLayout small_layout(int tw, int th) {
     const int ub = th16 * L.tbp > 4 * ROI_FT ? th16 * L.tbp : 4 * ROI_FT;
     L.tab = L.u + ub;
     L.sum = L.tab + 4 * (2 * L.sbp + 2 * ((L.rh + 3) & ~3));
-    L.rs = L.sum + 4 * (2 * L.rh + 2 * 7 * L.rh) + 8 * 49 * 2;
-    L.sc = L.rs + 4 * kBandRows * 49;
+    // the band's row sums live only in the band phase, when the footprints (U) and the warp tables (tab) are dead and U
+    // holds the template rows: placed after those rows when they fit there (Src7 layer 3: 46.1 -> 39.8 KB per
+    // workgroup, 3 -> 4 workgroups per CU), else after the window sums
+    const int rs_size = 4 * kBandRows * 49;
+    const int after_sums = L.sum + 4 * (2 * L.rh + 2 * 7 * L.rh) + 8 * 49 * 2;
+    if (th16 * L.tbp + rs_size <= L.sum - L.u) {
+        L.rs = L.u + th16 * L.tbp;
+        L.sc = after_sums;
+    } else {
+        L.rs = after_sums;
+        L.sc = L.rs + rs_size;
+    }
     L.ts = L.sc + 4 * 64;
     L.total = L.ts + 4 * th16;
     return L;

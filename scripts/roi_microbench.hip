@@ -280,7 +280,7 @@ int main(int argc, char** argv) {
         printf("tiles: %ld interior+LDS, %ld LDS border, %ld global taps, %ld empty\n", fast, lds_border, glob, empty);
     }
     timeit([&] { launch_roi_warp(a, 0); }, "prod warp");
-    if (!envi("MB_CORR", 0)) {   // MB_CORR=1: the correlation section only (the ROIs from the product warp above)
+    if (!envi("MB_CORR", 0) && !envi("MB_SMALL_ONLY", 0)) {
         const long tiles = (long)a.slot_cap * ((TH + 6 + 31) / 32) * ((TW + 6 + 31) / 32);
         const int grid = (int)std::min<long>((tiles + 3) / 4, 16384);
         timeit([&] { hipLaunchKernelGGL(k_roi_warp<0>, dim3(grid), dim3(256), 0, 0, a); }, "warp foot LDS-DMA");
@@ -348,6 +348,7 @@ int main(int argc, char** argv) {
         printf("tiles %ld\n", tiles);
     }
     if (envi("MB_WARP_ONLY", 0)) return 0;
+    if (!envi("MB_SMALL_ONLY", 0)) {   // MB_SMALL_ONLY=1: the small-template section only
     launch_roi_warp(a, 0);   // the product's ROIs (the warp variants above may have left other bytes)
     timeit([&] { launch_roi_corr(a, 0); }, "prod corr");
     if (TW > 512 && TW <= 768) {   // register-A form (12 k-steps, the Src7 layer-0 product) and its phase ablations
@@ -469,6 +470,7 @@ int main(int argc, char** argv) {
             (void)RW;
         }
         printf("corr host check: %s (%d mismatches)\n", bad ? "FAIL" : "OK", bad);
+    }
     }
     if (envi("MB_CORR", 0)) return 0;
     {   // small-template single-kernel refinement at Src7 layer-3 geometry: 96x66 template, 503x380 level,
