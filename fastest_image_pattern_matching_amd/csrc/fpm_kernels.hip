@@ -3961,14 +3961,25 @@ __device__ __forceinline__ CandState cand_step_state(CandState s, int n3, const 
 struct SmallLayout {
     int sbp, tbp, rh, u, tab, sum, rs, sc, ts, total;
 };
-__host__ __device__ inline SmallLayout small_layout(int tw, int th) {
+// The U region holds, one after the other: the ROI's whole source footprint or (when that does not fit) one 32x32
+// tile's footprint per wave, then the template rows.  A pure rotation keeps the footprint's box within the ROI's
+// diagonal D (+ the sampling margins and alignment of k_roi_small: width <= D + 14, height <= D + 4), so where that
+// box is smaller than the per-wave tile buffers U is sized to it and the tile path is never taken (it then reads
+// its taps from global memory, should it be).  nw = waves per workgroup.
+__host__ __device__ inline int small_footprint_bound(int rw, int rh) {
+    const int d = (int)ceilf(sqrtf((float)((rw - 1) * (rw - 1) + (rh - 1) * (rh - 1)))) + 2;
+    return ((d + 16) * (d + 6) + 15) & ~15;
+}
+__host__ __device__ inline SmallLayout small_layout(int tw, int th, int nw = 4) {
     SmallLayout L;
     L.sbp = roi_pitch_calc(tw);
     L.tbp = tmpl_lds_pitch(64 * ((tw + 63) / 64));
     L.rh = th + 6;
     const int th16 = (th + kMmaRows - 1) / kMmaRows * kMmaRows;
     L.u = ((L.rh + 16) * L.sbp + 15) & ~15;       // SB rows + slack rows read by the last band's N tiles
-    const int ub = th16 * L.tbp > 4 * ROI_FT ? th16 * L.tbp : 4 * ROI_FT;
+    const int fb = small_footprint_bound(tw + 6, th + 6);
+    const int fp = fb < nw * ROI_FT ? fb : nw * ROI_FT;
+    const int ub = th16 * L.tbp > fp ? th16 * L.tbp : fp;
     L.tab = L.u + ub;
     L.sum = L.tab + 4 * (2 * L.sbp + 2 * ((L.rh + 3) & ~3));
     // the band's row sums live only in the band phase, when the footprints (U) and the warp tables (tab) are dead and U
@@ -3996,11 +4007,14 @@ size_t roi_small_lds(int tw, int th) { return (size_t)small_layout(tw, th).total
 // s_memtime stamps (a.stamps)
 // PROL: the previous layer's candidate step in the prologue (a.prev_rec set; a separate instantiation: its registers
 // would cost the plain form spills, 11 -> 33 VGPRs at 4 waves, k_roi_small 178 -> 207 us per 43-source pass)
-template <int MODE, int WPE = 3, bool PROL = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_small(RoiArgs a) {
+// NT: threads per workgroup (256, or 128: two waves per ROI, so twice the ROIs per CU where the waves and not the LDS
+// bound the residency; the four MFMA tile pairs of a band then take two passes per wave); needs RW <= 4 NT
+template <int MODE, int WPE = 3, bool PROL = false, int NT = 256>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_small(RoiArgs a) {
+    constexpr int NW = NT / 64;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int tw = a.tw, th = a.th, RW = tw + 6, RH = th + 6, W = a.W, H = a.H;
-    const SmallLayout LY = small_layout(tw, th);
+    const SmallLayout LY = small_layout(tw, th, NW);
     const int SBp = LY.sbp, TBp = LY.tbp;
     uint8_t* SB = smem;                                  // RH ROI rows x SBp (u8, then ^ 0x80)
     uint8_t* TB = smem + LY.u;                           // template rows (i8) x TBp
@@ -4022,7 +4036,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const int q4 = SBp >> 4, nwr = (RW + 3) >> 2;
     const int txn = (RW + ROI_T - 1) / ROI_T, tyn = (RH + ROI_T - 1) / ROI_T;
     const int g = lane >> 4, n = lane & 15;
-    const int mt = wv & 1, nt = mt + (wv >> 1);
     const int lr = lane >> 3, lg = lane & 7;
     auto STAMP = [&](int k) {
         if (MODE == 9 && tid == 0 && blockIdx.x < 64) a.stamps[blockIdx.x * 16 + k] = __builtin_readcyclecounter();
@@ -4053,11 +4066,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         {   // warpAffine tables of this ROI (getRotatedROI :1074-1090)
             double M[6];
             roi_matrix(W, H, f2(st.lt.x * 2, st.lt.y * 2), nd.c, nd.s, M);
-            for (int x = tid; x < RW; x += 256) {
+            for (int x = tid; x < RW; x += NT) {
                 lad[x] = rint_i(M[0] * x * kAbScale);
                 lbd[x] = rint_i(M[3] * x * kAbScale);
             }
-            for (int y = tid; y < RH; y += 256) {
+            for (int y = tid; y < RH; y += NT) {
                 lx0[y] = rint_i((M[1] * y + M[2]) * kAbScale) + kRoundDelta;
                 ly0[y] = rint_i((M[4] * y + M[5]) * kAbScale) + kRoundDelta;
             }
@@ -4085,13 +4098,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         if (g_any && gftw * gfth <= LY.tab - LY.u) {   // wave-uniform (same values in every thread)
             uint8_t* FT = FTall;
             const int wpr = gftw >> 2;
-            stage_block4(FT, gftw, lvl + (size_t)gby0 * a.P + gbxa, a.P, gfth, wpr, gbxa, a.P, tid, 256);
+            stage_block4(FT, gftw, lvl + (size_t)gby0 * a.P + gbxa, a.P, gfth, wpr, gbxa, a.P, tid, NT);
             __syncthreads();
             STAMP(8);
             // thread -> one fixed group of 4 columns (its column table entries held in registers) and every
             // nrl-th row: no per-item division, 2 table reads per 4 pixels instead of 10
             const int ngrp = (RW + 3) >> 2;
-            const int nrl = 256 / ngrp;                   // row lanes (>= 1: RW <= 1024 for this kernel)
+            const int nrl = NT / ngrp;                    // row lanes (>= 1: RW <= 4 NT for this kernel)
             const int rl = tid / ngrp, c0 = 4 * (tid - rl * ngrp);
             int ad4[4], bd4[4];
 #pragma unroll
@@ -4141,10 +4154,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             }
             STAMP(9);
         } else if (!g_any) {   // the ROI lies entirely outside the image: all zero (BORDER_CONSTANT 0)
-            for (int i = tid; i < RH * (SBp >> 2); i += 256) ((uint32_t*)SB)[i] = 0u;
-        } else {   // footprint too large: one 32x32 tile per wave at a time
+            for (int i = tid; i < RH * (SBp >> 2); i += NT) ((uint32_t*)SB)[i] = 0u;
+        } else {   // footprint too large: one 32x32 tile per wave at a time (in LDS where U holds a buffer per wave)
+            const bool tile_bufs = NW * ROI_FT <= LY.tab - LY.u;
             uint8_t* FT = FTall + wv * ROI_FT;
-            for (int task = wv; task < txn * tyn; task += 4) {
+            for (int task = wv; task < txn * tyn; task += NW) {
                 const int ty = task / txn, tx = task - ty * txn;
                 const int cx0 = tx * ROI_T, cx1 = min(cx0 + ROI_T, RW) - 1;
                 const int ry0 = ty * ROI_T, ry1 = min(ry0 + ROI_T, RH) - 1;
@@ -4166,7 +4180,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 if (((ftw >> 2) & 1) == 0) ftw += 4;
                 const int fth = any ? by1 - by0 + 1 : 0;
                 const int wpr = ftw >> 2;
-                const bool in_lds = wpr <= 16 && ftw * fth <= ROI_FT;
+                const bool in_lds = tile_bufs && wpr <= 16 && ftw * fth <= ROI_FT;
                 wave_sync();
                 if (any && in_lds) stage_footprint<4>(FT, ftw, wpr, fth, lvl + (size_t)by0 * a.P + bxa, a.P, bxa, a.P, lane);
                 wave_sync();
@@ -4198,7 +4212,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         __syncthreads();
         if (MODE == 1) continue;
         STAMP(2);
-        for (int r = tid; r < RH; r += 256) {   // exact full-row sums of I and I^2, one thread per row
+        for (int r = tid; r < RH; r += NT) {   // exact full-row sums of I and I^2, one thread per row
             const uint32_t* row = (const uint32_t*)(SB + (size_t)r * SBp);
             uint32_t s1 = 0, s2 = 0;
             int k = 0;
@@ -4221,7 +4235,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             rallq[r] = s2;
         }
         __syncthreads();
-        for (int i = tid; i < RH * q4; i += 256) {   // bytes flipped to the signed MFMA operand
+        for (int i = tid; i < RH * q4; i += NT) {   // bytes flipped to the signed MFMA operand
             uint4* v = (uint4*)SB + i;   // rows are contiguous (pitch SBp = 16 * q4)
             uint4 x = *v;
             x.x ^= 0x80808080u; x.y ^= 0x80808080u; x.z ^= 0x80808080u; x.w ^= 0x80808080u;
@@ -4229,14 +4243,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
         {   // all template rows (padded to 16) of the i8 slab
             const int trows = (th + kMmaRows - 1) / kMmaRows * kMmaRows;
-            stage_block16(TB, TBp, (const uint8_t*)a.tmpl8, a.tp8, trows, a.tp8 >> 4, tid, 256);
+            stage_block16(TB, TBp, (const uint8_t*)a.tmpl8, a.tp8, trows, a.tp8 >> 4, tid, NT);
             // and the template-row sums (trows <= 256) for the band epilogues (3 waves per SIMD: 82.9 -> 81.0 us per
             // Src7 layer-3 launch; the 4-wave form reads them from global memory there, as its registers spill more)
-            if (WPE < 4 && tid < trows) lts[tid] = (uint32_t)a.tsum[tid];
+            if (WPE < 4)
+                for (int i = tid; i < (NT >= 256 ? min(trows, NT) : trows); i += NT) lts[i] = (uint32_t)a.tsum[i];
         }
         __syncthreads();
         STAMP(3);
-        for (int r = tid; r < RH; r += 256) {   // windows [dx, dx + tw) of a row: full row minus <= 6 edge pixels,
+        for (int r = tid; r < RH; r += NT) {    // windows [dx, dx + tw) of a row: full row minus <= 6 edge pixels,
             const uint8_t* sbr = SB + (size_t)r * SBp;   // the row's 12 edge bytes read once by one thread
             uint32_t lv[6], rv[6];
 #pragma unroll
@@ -4254,11 +4269,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 wq[r * 7 + dx] = q2;
             }
         }
-        if (tid < 98) tot[tid] = 0;
+        if (tid < 98) tot[tid] = 0;   // (NT >= 128)
         __syncthreads();
         STAMP(4);
-        if (tid < 4 * 49) {   // window totals of the 49 positions (exact): 4 threads per position, u64 LDS adds
-            const int part = tid / 49, k = tid - part * 49, pdy = k / 7, ddx = k - pdy * 7;
+        // window totals of the 49 positions (exact): 4 threads per position, u64 LDS adds (NT < 196: a loop)
+#pragma unroll 1
+        for (int q = tid; q < (NT >= 4 * 49 ? (tid < 4 * 49 ? tid + 1 : 0) : 4 * 49); q += NT) {
+            const int part = q / 49, k = q - part * 49, pdy = k / 7, ddx = k - pdy * 7;
             const int t0 = part * th / 4, t1 = (part + 1) * th / 4;
             uint64_t s1 = 0, s2 = 0;
             int t = t0;
@@ -4280,6 +4297,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const uint32_t kFix = 16384u * (uint32_t)tw;
         for (int T0 = 0; T0 < th; T0 += kBandRows) {   // bands in row order: MFMA -> LDS row sums -> fold
             const int rb = min(kBandRows, th - T0), nsrc = rb + 6;
+            // the band's four (M, N) tile pairs (t, s) = (0, 0), (1, 1), (0, 1), (1, 2): pair p on wave p % NW
+#pragma unroll
+            for (int pass = 0; pass < 4 / NW; ++pass) {
+            const int p = wv + pass * NW, mt = p & 1, nt = mt + (p >> 1);
             if (kMmaRows * mt < rb && kMmaRows * nt < nsrc) {
                 const uint8_t* ap = TB + (size_t)(T0 + kMmaRows * mt + n) * TBp + 16 * g;
                 const uint8_t* bp = SB + (size_t)(T0 + kMmaRows * nt + n) * SBp + 16 * g;   // slack rows cover sr >= RH
@@ -4296,6 +4317,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                             rs[t * 49 + dy * 7 + d] = (uint32_t)acc[d][r] + 128u * (wi[(T0 + s_) * 7 + d] + ts) - kFix;
                     }
                 }
+            }
             }
             __syncthreads();
             if (MODE != 3 && tid < 49) {
@@ -4705,6 +4727,22 @@ void launch_roi_small(const RoiArgs& a, hipStream_t st) {
         RoiArgs b = a;
         b.step = 0;
         launch_roi_eval(b, st);
+        return;
+    }
+    // two-wave workgroups at 4 waves per SIMD (8 per CU) where that holds more ROIs per CU than the four-wave form, i.e.
+    // where the waves and not the LDS bound the residency (Src7 layers 4 and 5: 8 ROIs per CU instead of 4, with the
+    // U region sized to the footprint bound): k_roi_small 22.1 -> 21.1 ms per 100 bench steps, bench 34.62k / 34.75k
+    // -> 35.06k / 35.05k alternated (profiles/r05l; at 3 waves per SIMD: 35.01k).  FPM_SMALL_NT=256 keeps the
+    // four-wave form (read when a search is recorded).
+    const char* nte = getenv("FPM_SMALL_NT");
+    const size_t lds2 = (size_t)small_layout(a.tw, a.th, 2).total, lds4 = (size_t)small_layout(a.tw, a.th).total;
+    const int per_cu2 = (int)std::min<size_t>(8, kLdsPerCu / std::max<size_t>(lds2, 1));
+    const int per_cu4 = (int)std::min<size_t>((size_t)(lds4 * 4 <= kLdsPerCu ? 4 : 3), kLdsPerCu / std::max<size_t>(lds4, 1));
+    if (!a.prev_rec && a.tw + 6 <= 512 && per_cu2 > per_cu4 && (nte ? atoi(nte) != 256 : true)) {
+        const int grid = capped(a.slot_cap < 16384 ? a.slot_cap : 16384,
+                                grid_cap_env(getenv("FPM_GRID_SMALL"), per_cu2 * kCUs));
+        ensure_lds_attr((const void*)k_roi_small<0, 4, false, 128>, lds2);
+        hipLaunchKernelGGL((k_roi_small<0, 4, false, 128>), dim3(grid), dim3(128), lds2, st, a);
         return;
     }
     const size_t lds = (size_t)small_layout(a.tw, a.th).total;

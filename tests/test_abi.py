@@ -101,4 +101,4 @@ def test_product_switches_are_result_neutral():
             names |= set(re.findall(r'getenv\("(FPM_[A-Z0-9_]+)"\)', open(os.path.join(csrc, f)).read()))
     assert names <= {"FPM_SCRATCH_MB", "FPM_TOP_FUSED", "FPM_OVERLAP_DEVICE_MIN", "FPM_TAIL_TIMES", "FPM_PYR_WGS",
                      "FPM_PYR_OH", "FPM_PYR2_OH", "FPM_STEP_PROLOGUE", "FPM_STEP_TABLES", "FPM_PYR2", "FPM_WARP3", "FPM_HOST_THREADS", "FPM_POOL_TRACE",
-                     "FPM_HOST_WARM", "FPM_GRID_WARP", "FPM_GRID_CORR", "FPM_GRID_SMALL", "FPM_GRID_TOP", "FPM_CORR16"}, names
+                     "FPM_HOST_WARM", "FPM_GRID_WARP", "FPM_GRID_CORR", "FPM_GRID_SMALL", "FPM_GRID_TOP", "FPM_CORR16", "FPM_SMALL_NT"}, names
