@@ -4620,7 +4620,11 @@ void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
         const long want3 = (tiles / 3 + 3) / 4;
         // 7 waves per SIMD with the first ROI's tables requested before the staging (8 would spill them): microbenchmark
         // 405.5 / 406.3 -> 400.6 / 402.0 us (round 3)
-        hipLaunchKernelGGL((k_roi_warp3<7, kFtPitch, 0>), dim3(capped((int)(want3 < 16384 ? want3 : 16384), grid_cap_env(getenv("FPM_GRID_WARP"), 0))),
+        // small launches (at most two workgroups per resident slot, e.g. a lone Src7 search's layer 0: 3.4 K) run at the
+        // residency -- fewer workgroup dispatches: 19.3 -> 15.1 us (profiles/r05_end2 vs r05_end lat_*.txt); large ones
+        // keep the full grid (its dynamic balance beats the persistent grid's static task ranges, r05j)
+        const int dflt_cap = want3 <= 2 * 7 * kCUs ? 7 * kCUs : 0;
+        hipLaunchKernelGGL((k_roi_warp3<7, kFtPitch, 0>), dim3(capped((int)(want3 < 16384 ? want3 : 16384), grid_cap_env(getenv("FPM_GRID_WARP"), dflt_cap))),
                            dim3(256), 0, st, a);
         return;
     }
@@ -4738,7 +4742,12 @@ void launch_roi_small(const RoiArgs& a, hipStream_t st) {
     const size_t lds2 = (size_t)small_layout(a.tw, a.th, 2).total, lds4 = (size_t)small_layout(a.tw, a.th).total;
     const int per_cu2 = (int)std::min<size_t>(8, kLdsPerCu / std::max<size_t>(lds2, 1));
     const int per_cu4 = (int)std::min<size_t>((size_t)(lds4 * 4 <= kLdsPerCu ? 4 : 3), kLdsPerCu / std::max<size_t>(lds4, 1));
-    if (!a.prev_rec && a.tw + 6 <= 512 && per_cu2 > per_cu4 && (nte ? atoi(nte) != 256 : true)) {
+    // (only where the layer has more ROIs than the four-wave form holds at once: with fewer, as in a lone search, each
+    // ROI's chain of phases is what counts, and two waves take longer over it: 10.7 -> 13.2 us, r05_end2)
+    // FPM_SMALL_NT=128 forces the two-wave form wherever it applies, 256 never uses it
+    const int nt_env = nte ? atoi(nte) : 0;
+    if (!a.prev_rec && a.tw + 6 <= 512 && per_cu2 > per_cu4 && nt_env != 256 &&
+        (nt_env == 128 || a.slot_cap > per_cu4 * kCUs)) {
         const int grid = capped(a.slot_cap < 16384 ? a.slot_cap : 16384,
                                 grid_cap_env(getenv("FPM_GRID_SMALL"), per_cu2 * kCUs));
         ensure_lds_attr((const void*)k_roi_small<0, 4, false, 128>, lds2);
