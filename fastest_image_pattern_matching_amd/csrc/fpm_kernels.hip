@@ -4620,10 +4620,12 @@ void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
         const long want3 = (tiles / 3 + 3) / 4;
         // 7 waves per SIMD with the first ROI's tables requested before the staging (8 would spill them): microbenchmark
         // 405.5 / 406.3 -> 400.6 / 402.0 us (round 3)
-        // small launches (at most two workgroups per resident slot, e.g. a lone Src7 search's layer 0: 3.4 K) run at the
-        // residency -- fewer workgroup dispatches: 19.3 -> 15.1 us (profiles/r05_end2 vs r05_end lat_*.txt); large ones
-        // keep the full grid (its dynamic balance beats the persistent grid's static task ranges, r05j)
-        const int dflt_cap = want3 <= 2 * 7 * kCUs ? 7 * kCUs : 0;
+        // batches of at most two sources (a lone search) run at the residency: the grid is sized for the plan's candidate
+        // capacity, mostly idle workgroups there, and fewer dispatches take a lone Src7 search's layer 0 from 19.5 to
+        // 15.1 us (profiles/r05m vs r05_end lat_*.txt); larger batches keep the full grid (its dynamic balance beats the
+        // persistent grid's static task ranges, r05j)
+        const int srcs = a.slot_cap / std::max(1, a.per_source * a.n3);
+        const int dflt_cap = srcs <= 2 ? 7 * kCUs : 0;
         hipLaunchKernelGGL((k_roi_warp3<7, kFtPitch, 0>), dim3(capped((int)(want3 < 16384 ? want3 : 16384), grid_cap_env(getenv("FPM_GRID_WARP"), dflt_cap))),
                            dim3(256), 0, st, a);
         return;
