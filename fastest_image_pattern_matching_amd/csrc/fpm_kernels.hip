@@ -4441,10 +4441,17 @@ __global__ __launch_bounds__(192) void k_cand_step_tab(RoiArgs a) {
 // :329-366: best of the n3 angles, early break below vecLayerScore, back-mapping of ptLT, append to the next live
 // list.  Each wave streams its [th][49] series through wave-private LDS in blocks of kEvalRows rows, the next
 // block's loads in flight while 49 lanes fold the current one in row order.  No workgroup barrier in the loop.
-constexpr int kEvalRows = 48;
+// Blocks of 40 rows: 8 loads per lane, 48 KB of LDS per three-wave workgroup, so three workgroups per CU -- 768
+// candidates at once, which holds the bench's 64-source context passes (<= 704 candidates per layer) in one round
+// (48-row blocks: 10 loads, 61 KB, two per CU; the same time per launch when one round holds the layer, round 4)
+#define FPM_EVAL_DMA 8
+constexpr int kEvalRows = 40;
 constexpr int kEvalDma = (kEvalRows * 49 / 4 + 63) / 64;   // 16-byte LDS-DMA loads per lane per block
 constexpr int kEvalBuf = kEvalDma * 1024;                    // bytes per block buffer
-static_assert(kEvalDma == 10, "the counted s_waitcnt vmcnt(10) in eval_roi assumes 10 loads per block");
+static_assert(kEvalDma == FPM_EVAL_DMA && kEvalRows * 49 % 4 == 0,
+              "the counted s_waitcnt in eval_roi assumes FPM_EVAL_DMA loads per block of whole uint4");
+#define FPM_STR2(x) #x
+#define FPM_STR(x) FPM_STR2(x)
 
 __device__ void eval_roi(const RoiArgs& a, int slot, int lane, uint8_t* blk, float* sc, RoiRecord* out,
                          RoiRecord* keep) {
@@ -4500,7 +4507,8 @@ __device__ void eval_roi(const RoiArgs& a, int slot, int lane, uint8_t* blk, flo
         const uint32_t* cb = (const uint32_t*)(blk + (b & 1) * kEvalBuf);
         if (b + 1 < nblk) {
             issue_block(b + 1, blk + ((b + 1) & 1) * kEvalBuf);
-            asm volatile("s_waitcnt vmcnt(10)" ::: "memory");   // kEvalDma loads of block b + 1 may stay in flight
+            // the kEvalDma loads of block b + 1 may stay in flight
+            asm volatile("s_waitcnt vmcnt(" FPM_STR(FPM_EVAL_DMA) ")" ::: "memory");
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -4750,6 +4758,8 @@ void launch_roi_small(const RoiArgs& a, hipStream_t st) {
     const int nt_env = nte ? atoi(nte) : 0;
     if (!a.prev_rec && a.tw + 6 <= 512 && per_cu2 > per_cu4 && nt_env != 256 &&
         (nt_env == 128 || a.slot_cap > per_cu4 * kCUs)) {
+        // (5 waves per SIMD, 10 workgroups per CU -- layers 4-5 in one round at 64 sources -- spill 172 bytes: 21.1 ->
+        // 23.3 ms per 100 bench steps, profiles/r05n)
         const int grid = capped(a.slot_cap < 16384 ? a.slot_cap : 16384,
                                 grid_cap_env(getenv("FPM_GRID_SMALL"), per_cu2 * kCUs));
         ensure_lds_attr((const void*)k_roi_small<0, 4, false, 128>, lds2);
