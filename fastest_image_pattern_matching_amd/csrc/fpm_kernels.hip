@@ -4766,7 +4766,7 @@ void launch_roi_small(const RoiArgs& a, hipStream_t st) {
         hipLaunchKernelGGL((k_roi_small<0, 4, false, 128>), dim3(grid), dim3(128), lds2, st, a);
         return;
     }
-    const size_t lds = (size_t)small_layout(a.tw, a.th).total;
+    const size_t lds = lds4;
     // default cap: the kernel's residency (workgroups per CU: its waves per SIMD, or fewer where the LDS runs out)
     const int wpe = a.prev_rec ? 3 : (lds * 4 <= kLdsPerCu ? 4 : 3);
     const int per_cu = (int)std::min<size_t>((size_t)wpe, kLdsPerCu / std::max<size_t>(lds, 1));
