@@ -4007,8 +4007,9 @@ size_t roi_small_lds(int tw, int th) { return (size_t)small_layout(tw, th).total
 // s_memtime stamps (a.stamps)
 // PROL: the previous layer's candidate step in the prologue (a.prev_rec set; a separate instantiation: its registers
 // would cost the plain form spills, 11 -> 33 VGPRs at 4 waves, k_roi_small 178 -> 207 us per 43-source pass)
-// NT: threads per workgroup (256, or 128: two waves per ROI, so twice the ROIs per CU where the waves and not the LDS
-// bound the residency; the four MFMA tile pairs of a band then take two passes per wave); needs RW <= 4 NT
+// NT: threads per workgroup (256; 128: two waves per ROI, so twice the ROIs per CU where the waves and not the LDS
+// bound the residency, the four MFMA tile pairs of a band then in two passes per wave; 512: eight waves per ROI for
+// layers with fewer ROIs than CUs, the sampling and staging spread over twice the lanes); needs RW <= 4 NT
 template <int MODE, int WPE = 3, bool PROL = false, int NT = 256>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_small(RoiArgs a) {
     constexpr int NW = NT / 64;
@@ -4297,11 +4298,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         const uint32_t kFix = 16384u * (uint32_t)tw;
         for (int T0 = 0; T0 < th; T0 += kBandRows) {   // bands in row order: MFMA -> LDS row sums -> fold
             const int rb = min(kBandRows, th - T0), nsrc = rb + 6;
-            // the band's four (M, N) tile pairs (t, s) = (0, 0), (1, 1), (0, 1), (1, 2): pair p on wave p % NW
+            // the band's four (M, N) tile pairs (t, s) = (0, 0), (1, 1), (0, 1), (1, 2): pair p on wave p % NW (NW = 8:
+            // waves 4-7 have none)
 #pragma unroll
-            for (int pass = 0; pass < 4 / NW; ++pass) {
+            for (int pass = 0; pass < (4 + NW - 1) / NW; ++pass) {
             const int p = wv + pass * NW, mt = p & 1, nt = mt + (p >> 1);
-            if (kMmaRows * mt < rb && kMmaRows * nt < nsrc) {
+            if (p < 4 && kMmaRows * mt < rb && kMmaRows * nt < nsrc) {
                 const uint8_t* ap = TB + (size_t)(T0 + kMmaRows * mt + n) * TBp + 16 * g;
                 const uint8_t* bp = SB + (size_t)(T0 + kMmaRows * nt + n) * SBp + 16 * g;   // slack rows cover sr >= RH
                 fpm_v4i acc[7];
@@ -4749,6 +4751,21 @@ void launch_roi_small(const RoiArgs& a, hipStream_t st) {
     // -> 35.06k / 35.05k alternated (profiles/r05l; at 3 waves per SIMD: 35.01k).  FPM_SMALL_NT=256 keeps the
     // four-wave form (read when a search is recorded).
     const char* nte = getenv("FPM_SMALL_NT");
+    // eight-wave workgroups for a lone search's layers (batches of at most two sources: fewer ROIs than CUs, so each
+    // ROI's chain of phases is the time; FPM_SMALL_NT=512 forces them, another value keeps them off)
+    const int srcs = a.slot_cap / std::max(1, a.per_source * a.n3);
+    if (nte ? atoi(nte) == 512 : srcs <= 2) {
+        const size_t lds8 = (size_t)small_layout(a.tw, a.th, 8).total;
+        const int grid = capped(a.slot_cap < 8192 ? a.slot_cap : 8192, grid_cap_env(getenv("FPM_GRID_SMALL"), kCUs));
+        if (a.prev_rec) {
+            ensure_lds_attr((const void*)k_roi_small<0, 2, true, 512>, lds8);
+            hipLaunchKernelGGL((k_roi_small<0, 2, true, 512>), dim3(grid), dim3(512), lds8, st, a);
+        } else {
+            ensure_lds_attr((const void*)k_roi_small<0, 2, false, 512>, lds8);
+            hipLaunchKernelGGL((k_roi_small<0, 2, false, 512>), dim3(grid), dim3(512), lds8, st, a);
+        }
+        return;
+    }
     const size_t lds2 = (size_t)small_layout(a.tw, a.th, 2).total, lds4 = (size_t)small_layout(a.tw, a.th).total;
     const int per_cu2 = (int)std::min<size_t>(8, kLdsPerCu / std::max<size_t>(lds2, 1));
     const int per_cu4 = (int)std::min<size_t>((size_t)(lds4 * 4 <= kLdsPerCu ? 4 : 3), kLdsPerCu / std::max<size_t>(lds4, 1));

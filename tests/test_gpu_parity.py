@@ -187,13 +187,14 @@ def test_src7_top_layer_forms(gpu_matcher_factory, templates, monkeypatch, top_f
                                   {"FPM_GRID_TOP": "1000", "FPM_GRID_SMALL": "768", "FPM_GRID_WARP": "1536"},
                                   {"FPM_GRID_SMALL": "0", "FPM_GRID_WARP": "0"},
                                   {"FPM_CORR16": "1"}, {"FPM_CORR16": "1", "FPM_GRID_CORR": "13"},
-                                  {"FPM_SMALL_NT": "256"}, {"FPM_SMALL_NT": "128"},
+                                  {"FPM_SMALL_NT": "256"}, {"FPM_SMALL_NT": "128"}, {"FPM_SMALL_NT": "512"},
                                   {"FPM_SMALL_NT": "128", "FPM_GRID_SMALL": "5"}])
 def test_src7_grid_caps(gpu_matcher_factory, templates, monkeypatch, caps):
     """The workgroup caps of the persistent forms (FPM_GRID_TOP / _SMALL / _WARP / _CORR; read when a fresh context
     records its search; {} = the defaults, "0" = uncapped grids; FPM_CORR16 = the 16-row-item correlation;
-    FPM_SMALL_NT=256 / 128 = four- / two-wave workgroups for every small-template layer where they apply; by default
-    two-wave ones only for layers with more ROIs than the four-wave form holds at once): with tiny
+    FPM_SMALL_NT=256 / 128 / 512 = four- / two- / eight-wave workgroups for every small-template layer where they
+    apply; by default eight-wave ones for batches of at most two sources, two-wave ones for layers with more ROIs than
+    the four-wave form holds at once): with tiny
     caps every workgroup of the fused top layer, the small-template refinement, the
     sampler and the correlation loops over many jobs; a batch of seven Src7 sources (fused top layer: >= 256 jobs)
     equals the oracle."""
