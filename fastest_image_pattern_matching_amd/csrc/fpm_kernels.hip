@@ -4904,9 +4904,11 @@ __global__ __launch_bounds__(256) void k_overlap_pairs(const OvRect* __restrict_
                 const OvRect rj = r[j];
                 F2 pts[24];
                 int np = 0;
-                const int kind = rrect_isect_pts(ri.w, ri.h, rj.w, rj.h, ri.c, rj.c, pts, &np);
+                const int kind = rrect_isect_pts<false>(ri.w, ri.h, rj.w, rj.h, ri.c, rj.c, pts, &np);
                 int verdict = INT_MIN;
-                if (kind == 2) {
+                if (kind < 0) {   // more than 8 intersection points after the near-duplicate pass: the host decides
+                    verdict = ~j;
+                } else if (kind == 2) {
                     verdict = j;
                 } else if (kind == 1 && np >= 3) {
                     if (!sort_pts_fast(pts, np)) verdict = ~j;

@@ -15,6 +15,10 @@ FPM_HD float fmin_std(float a, float b) { return (b < a) ? b : a; }   // std::mi
 // cv::rotatedRectangleIntersection (OpenCV 4.5.x) on the two rectangles' corners A, B (rrect corners, in order) and
 // their sizes: 0 = INTERSECT_NONE, 1 = INTERSECT_PARTIAL, 2 = INTERSECT_FULL; the intersection points go to pts
 // (room for 24: at most 16 edge crossings + 8 corners before the near-duplicate pass, at most 8 after it).
+// FULL = false (the device kernel): where more than 8 points survive the near-duplicate pass (rare) it returns -1 instead
+// of running the reference's closest-pair reduction, whose 24 x 24 distance table would otherwise sit in every lane's
+// scratch (2.7 KB per lane: few waves in flight); the caller hands such a pair to the host.
+template <bool FULL = true>
 FPM_HD int rrect_isect_pts(float wa, float ha, float wb, float hb, const F2* A, const F2* B, F2* pts, int* np) {
     int n = 0;
     F2 eA[4], eB[4];
@@ -92,6 +96,10 @@ FPM_HD int rrect_isect_pts(float wa, float ha, float wb, float hb, const F2* A, 
             *np = m;
             return kind;
         }
+    }
+    if constexpr (!FULL) {
+        *np = n;
+        return -1;
     }
     const int stride = n;
     float dist[24 * 24];
