@@ -4443,20 +4443,21 @@ __global__ __launch_bounds__(192) void k_cand_step_tab(RoiArgs a) {
 // :329-366: best of the n3 angles, early break below vecLayerScore, back-mapping of ptLT, append to the next live
 // list.  Each wave streams its [th][49] series through wave-private LDS in blocks of kEvalRows rows, the next
 // block's loads in flight while 49 lanes fold the current one in row order.  No workgroup barrier in the loop.
-// Blocks of 40 rows: 8 loads per lane, 48 KB of LDS per three-wave workgroup, so three workgroups per CU -- 768
-// candidates at once, which holds the bench's 64-source context passes (<= 704 candidates per layer) in one round
-// (48-row blocks: 10 loads, 61 KB, two per CU; the same time per launch when one round holds the layer, round 4)
-#define FPM_EVAL_DMA 8
-constexpr int kEvalRows = 40;
-constexpr int kEvalDma = (kEvalRows * 49 / 4 + 63) / 64;   // 16-byte LDS-DMA loads per lane per block
-constexpr int kEvalBuf = kEvalDma * 1024;                    // bytes per block buffer
-static_assert(kEvalDma == FPM_EVAL_DMA && kEvalRows * 49 % 4 == 0,
-              "the counted s_waitcnt in eval_roi assumes FPM_EVAL_DMA loads per block of whole uint4");
-#define FPM_STR2(x) #x
-#define FPM_STR(x) FPM_STR2(x)
+// Blocks of ROWS rows: 40 for batches (8 loads per lane, 48 KB of LDS per three-wave workgroup, so three workgroups per
+// CU -- 768 candidates at once, which holds the bench's 64-source context passes (<= 704 candidates per layer) in one
+// round; 48-row blocks: 10 loads, 61 KB, two per CU, the same time per launch when one round holds the layer, round
+// 4), 48 for a lone search (fewer blocks, so fewer LDS-DMA round trips in each wave's chain)
+template <int ROWS>
+struct EvalBlk {
+    static_assert(ROWS * 49 % 4 == 0, "a block is whole uint4 of the [th][49] series");
+    static constexpr int dma = (ROWS * 49 / 4 + 63) / 64;   // 16-byte LDS-DMA loads per lane per block
+    static constexpr int buf = dma * 1024;                  // bytes per block buffer
+};
 
+template <int ROWS>
 __device__ void eval_roi(const RoiArgs& a, int slot, int lane, uint8_t* blk, float* sc, RoiRecord* out,
                          RoiRecord* keep) {
+    constexpr int kEvalRows = ROWS, kEvalDma = EvalBlk<ROWS>::dma, kEvalBuf = EvalBlk<ROWS>::buf;
     const int th = a.th;
     if (a.equal1) {   // CCOEFF_Denominator: matResult = 1 everywhere (:529-533)
         if (lane == 0) {
@@ -4509,8 +4510,7 @@ __device__ void eval_roi(const RoiArgs& a, int slot, int lane, uint8_t* blk, flo
         const uint32_t* cb = (const uint32_t*)(blk + (b & 1) * kEvalBuf);
         if (b + 1 < nblk) {
             issue_block(b + 1, blk + ((b + 1) & 1) * kEvalBuf);
-            // the kEvalDma loads of block b + 1 may stay in flight
-            asm volatile("s_waitcnt vmcnt(" FPM_STR(FPM_EVAL_DMA) ")" ::: "memory");
+            asm volatile("s_waitcnt vmcnt(%0)" :: "i"(kEvalDma) : "memory");   // block b + 1's loads may stay in flight
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -4557,8 +4557,9 @@ __device__ void eval_roi(const RoiArgs& a, int slot, int lane, uint8_t* blk, flo
     }
 }
 
+template <int ROWS>
 __global__ __launch_bounds__(192) void k_roi_eval(RoiArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t blk_all[3][2 * kEvalBuf];
+    __shared__ __attribute__((aligned(16))) uint8_t blk_all[3][2 * EvalBlk<ROWS>::buf];
     __shared__ float sc_all[3][64];
     __shared__ RoiRecord recs[3];
     __shared__ int pos;
@@ -4572,7 +4573,7 @@ __global__ __launch_bounds__(192) void k_roi_eval(RoiArgs a) {
         const int id = a.live[li];
         const int slot = li * a.n3 + j - base;
         __syncthreads();   // previous candidate's records consumed
-        eval_roi(a, slot, lane, blk_all[j], sc_all[j], a.rec + (size_t)id * a.n3 + j, &recs[j]);
+        eval_roi<ROWS>(a, slot, lane, blk_all[j], sc_all[j], a.rec + (size_t)id * a.n3 + j, &recs[j]);
         if (!a.step) continue;
         __syncthreads();
         if (threadIdx.x == 0) {   // TemplateMatcher.cpp:329-366
@@ -4734,7 +4735,9 @@ void launch_roi_eval(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0) return;
     const int cands = (a.slot_cap + a.n3 - 1) / a.n3;
     const int grid = cands < 4096 ? cands : 4096;
-    hipLaunchKernelGGL(k_roi_eval, dim3(grid), dim3(64 * a.n3), 0, st, a);
+    const int srcs = a.slot_cap / std::max(1, a.per_source * a.n3);   // (batches of <= 2 sources: a lone search)
+    if (srcs <= 2) hipLaunchKernelGGL(k_roi_eval<48>, dim3(grid), dim3(64 * a.n3), 0, st, a);
+    else hipLaunchKernelGGL(k_roi_eval<40>, dim3(grid), dim3(64 * a.n3), 0, st, a);
 }
 
 void launch_roi_small(const RoiArgs& a, hipStream_t st) {
@@ -4751,10 +4754,12 @@ void launch_roi_small(const RoiArgs& a, hipStream_t st) {
     // -> 35.06k / 35.05k alternated (profiles/r05l; at 3 waves per SIMD: 35.01k).  FPM_SMALL_NT=256 keeps the
     // four-wave form (read when a search is recorded).
     const char* nte = getenv("FPM_SMALL_NT");
-    // eight-wave workgroups for a lone search's layers (batches of at most two sources: fewer ROIs than CUs, so each
-    // ROI's chain of phases is the time; FPM_SMALL_NT=512 forces them, another value keeps them off)
+    // eight-wave workgroups (one per CU) for a lone search's layers: batches of at most two sources whose plan holds at
+    // most 1024 ROIs (a lone Src7 search: 936, 99 live), so each ROI's chain of phases is the time -- not a search with
+    // thousands of candidates (Src10 +-180, TargetNum 100: 14.8 K), whose ROIs need the residency of the smaller forms.
+    // FPM_SMALL_NT=512 forces them, another value keeps them off.
     const int srcs = a.slot_cap / std::max(1, a.per_source * a.n3);
-    if (nte ? atoi(nte) == 512 : srcs <= 2) {
+    if (nte ? atoi(nte) == 512 : (srcs <= 2 && a.slot_cap <= 4 * kCUs)) {
         const size_t lds8 = (size_t)small_layout(a.tw, a.th, 8).total;
         const int grid = capped(a.slot_cap < 8192 ? a.slot_cap : 8192, grid_cap_env(getenv("FPM_GRID_SMALL"), kCUs));
         if (a.prev_rec) {
