@@ -103,6 +103,13 @@ struct Plan {
     size_t canvas_bytes = 0, map_floats = 0, blk_count = 0;
     int max_canvas = 0, max_map = 0, max_nblk = 0, max_cells = 0, max_nitems = 0;
     int off_skey = 0, nzero = 0;   // d_livecnt layout: strip keys' offset, words zeroed by k_warp
+    // the matrix-core top layer (k_top_mma + k_nms_greedy on its candidate lists): layout and
+    // constants of the launch (pointers set at plan time), the unit list and B fragments in d_tmu, the values of the
+    // lists in d_tcandv (indices in d_ncand), their counts at d_livecnt + L + 2 (zeroed by the first pyramid launch)
+    bool top_mma = false;
+    TopMmaArgs tma{};
+    int tcand_cap = 0;
+    DevBuf d_tmu, d_tcandv;
     // device buffers owned by the plan
     DevBuf d_ncand;                            // s_BlockMax candidate lists (k_nms_blocks -> k_nms_fast)
     DevBuf d_canvas, d_map, d_bmax, d_bloc, d_jobs, d_nodes, d_top, d_topn, d_peaks, d_counts, d_state,
@@ -115,7 +122,7 @@ struct Plan {
     size_t h_counts = 0, h_peaks = 0, h_live = 0, h_live0 = 0, h_state = 0, h_rec = 0, h_total = 0;
     char* h_dev = nullptr;   // device-side address of h_out (k_pack writes it over PCIe)
     void release() {
-        for (DevBuf* b : {&d_ncand, &d_canvas, &d_map, &d_bmax, &d_bloc, &d_jobs, &d_nodes, &d_top, &d_topn, &d_peaks,
+        for (DevBuf* b : {&d_tmu, &d_tcandv, &d_ncand, &d_canvas, &d_map, &d_bmax, &d_bloc, &d_jobs, &d_nodes, &d_top, &d_topn, &d_peaks,
                           &d_counts, &d_state, &d_live, &d_livecnt, &d_rec, &d_rowsum, &d_wsum, &d_wsq, &d_tab, &d_roi, &d_tdesc, &d_state2, &d_rec2})
             b->release();
         h_out.release();
@@ -323,6 +330,105 @@ static bool angle_list_ok(const fpm_params& prm, double step, bool mfc) {
     return n <= kMaxTopAngles;
 }
 
+// The matrix-core top layer's plan (k_top_mma): whether it applies, its strip width and row runs
+// (work units), the B fragments of the top template level and the candidate-list buffers.  Applies where the template
+// level fits the kernel's two MFMA layouts, the layer score is > 0.01 (the greedy peak forms need thr > 0, and the lists
+// stay short), there is a pyramid launch to zero the list counters (L >= 1), the level is not flat (ResultEqual1) and
+// the greedy form can hold the maps' coverage cells; FPM_TOP_MMA=0 keeps the split / fused kernels (read when the plan is
+// built).
+int plan_top_mma(fpm_ctx* ctx, Plan& P, const TmplLevel& tt) {
+    P.top_mma = false;
+    const char* env = getenv("FPM_TOP_MMA");
+    if (env && atoi(env) == 0) return FPM_OK;
+    const int L = P.L, S = ctx->S, J = S * P.nang;
+    const double thr = P.layer_score[L];
+    int max_mw = 0, max_mh = 0;
+    for (int a = 0; a < P.nang; ++a) { max_mw = std::max(max_mw, P.map_w[a]); max_mh = std::max(max_mh, P.map_h[a]); }
+    if (L < 1 || J <= 0 || !top_mma_fits(tt.w, tt.h) || tt.equal1 || !(thr > 0.01) || max_mw <= 0 ||
+        std::max(max_mw, max_mh) >= 65536 || P.cap > 256 || P.max_cells > 12 * 1024)
+        return FPM_OK;
+    // strip width: one strip up to 192 output columns, else the fewest strips of at most 192, evened out
+    const int nstrip = (max_mw + kTopMmaMaxSw - 1) / kTopMmaMaxSw;
+    const int sw = (((max_mw + nstrip - 1) / nstrip) + 15) / 16 * 16;
+    // row runs: the longest (fewer first-band re-samplings of th - 1 rows) that still give >= 2048 units
+    std::vector<TopUnit> units;
+    int seg = 64;
+    for (int cand : {1 << 30, 256, 128, 64}) {
+        long n = 0;
+        for (int a = 0; a < P.nang; ++a)
+            if (P.map_w[a] > 0 && P.map_h[a] > 0)
+                n += (long)((P.map_w[a] + sw - 1) / sw) * ((P.map_h[a] + std::min(cand, P.map_h[a]) - 1) /
+                                                           std::min(cand, P.map_h[a]));
+        seg = cand;
+        if (n * S >= 2048) break;
+    }
+    int max_rows = 0;
+    for (int s = 0; s < S; ++s)
+        for (int a = 0; a < P.nang; ++a) {
+            const int mw = P.map_w[a], mh = P.map_h[a];
+            if (mw <= 0 || mh <= 0) continue;
+            const int run = std::min(seg, mh);
+            for (int x0 = 0; x0 < mw; x0 += sw)
+                for (int y0 = 0; y0 < mh; y0 += run) {
+                    TopUnit u;
+                    u.job = s * P.nang + a; u.x0 = x0; u.y0 = y0; u.y1 = std::min(mh, y0 + run);
+                    units.push_back(u);
+                    max_rows = std::max(max_rows, u.y1 - u.y0);
+                }
+        }
+    TopMmaArgs& A = P.tma;
+    A = TopMmaArgs{};
+    A.tw = tt.w; A.th = tt.h; A.area = tt.w * tt.h;
+    top_mma_layout(A, sw, max_rows);
+    if (top_mma_lds(A) > 160 * 1024 - 1024) return FPM_OK;
+    uint32_t tsum = 0;
+    for (uint8_t v : tt.px) tsum += v;
+    A.tsum = tsum;
+    // B fragments: slot q, lane (n = lane & 15, g = lane >> 4), byte i is k = 16 g + i -> template row r, column c - n
+    std::vector<int8_t> bf((size_t)A.nq * 64 * 16, 0);
+    for (int q = 0; q < A.nq; ++q)
+        for (int lane = 0; lane < 64; ++lane)
+            for (int i = 0; i < 16; ++i) {
+                const int n = lane & 15, g = lane >> 4;
+                const int r = A.R == 2 ? 2 * q + (g >> 1) : q;
+                const int c = (A.R == 2 ? 16 * (g & 1) : 16 * g) + i - n;
+                if (r < tt.h && c >= 0 && c < tt.w)
+                    bf[((size_t)q * 64 + lane) * 16 + i] = (int8_t)((int)tt.px[(size_t)r * tt.w + c] - 128);
+            }
+    const size_t ubytes = ((units.size() * sizeof(TopUnit)) + 255) & ~(size_t)255;
+    HIP_TRY(P.d_tmu.ensure(ubytes + bf.size()));
+    HIP_TRY(hipMemcpyAsync(P.d_tmu.p, units.data(), units.size() * sizeof(TopUnit), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(P.d_tmu.as<char>(ubytes), bf.data(), bf.size(), hipMemcpyHostToDevice, ctx->stream));
+    // candidate lists: s_BlockMax maps share d_ncand with k_nms_blocks' fallback lists (kNmsCandCap per map); plain
+    // maps need no more than the greedy form takes
+    P.tcand_cap = P.by_block ? kNmsCandCap : 4096;
+    // FPM_TOP_LIST_CAP=n (tests): lists of n entries, so every map with more candidates takes the fallback path
+    if (const char* lc = getenv("FPM_TOP_LIST_CAP"))
+        if (atoi(lc) > 0) P.tcand_cap = std::min(P.tcand_cap, atoi(lc));
+    HIP_TRY(P.d_ncand.ensure(sizeof(int32_t) * (size_t)P.tcand_cap * J));
+    HIP_TRY(P.d_tcandv.ensure(sizeof(float) * (size_t)P.tcand_cap * J));
+    A.wjobs = P.d_jobs.as<WarpJob>(P.off_warp);
+    A.njobs = P.d_jobs.as<NccJob>(P.off_ncc);
+    A.units = P.d_tmu.as<TopUnit>();
+    A.nunits = (int)units.size();
+    A.bfrag = P.d_tmu.as<uint8_t>(ubytes);
+    A.prefilter = A.area <= 258 ? 1 : 0;
+    const double tm = thr * (1.0 - 1e-5);
+    A.thrK = (float)(tm * tm * tt.norm * tt.norm * (double)A.area);
+    A.E = 1024.f;
+    A.thr = thr; A.mean = tt.mean; A.norm = tt.norm; A.inv_area = tt.inv_area;
+    A.cand = P.d_ncand.as<int32_t>();
+    A.cand_val = P.d_tcandv.as<float>();
+    A.cand_cap = P.tcand_cap;
+    if (!P.by_block) {   // plain maps: the list counters follow the live counts (s_BlockMax plans already zero them)
+        P.nzero = L + 2 + J;
+        HIP_TRY(P.d_livecnt.ensure(sizeof(int32_t) * (size_t)P.nzero));
+    }
+    A.cand_cnt = P.d_livecnt.as<int32_t>() + L + 2;
+    P.top_mma = true;
+    return FPM_OK;
+}
+
 int build_plan(fpm_ctx* ctx) {
     Plan& P = ctx->plan;
     const int L = ctx->src_L;
@@ -406,9 +512,10 @@ int build_plan(fpm_ctx* ctx) {
             const int rw = P.map_w[a] - ncol * bw, rh = P.map_h[a] - nrow * bh;
             if (!mfc) nb = ncol * nrow + (rw > 0) + (rh > 0) + (rw > 0 && rh > 0);
             else nb = (ncol == 0 || nrow == 0) ? 0 : ncol * nrow + ((rw > 0 && rh > 0) ? 2 : 1);
-            P.max_cells = std::max(P.max_cells, ((P.map_w[a] + tt.w - 1) / tt.w) * ((P.map_h[a] + tt.h - 1) / tt.h));
             P.max_nitems = std::max(P.max_nitems, nms_block_items(P.map_w[a], P.map_h[a], tt.w, tt.h, mfc ? 1 : 0));
         }
+        if (ok)   // coverage cells of the greedy peak forms (k_nms_greedy), plain and s_BlockMax alike
+            P.max_cells = std::max(P.max_cells, ((P.map_w[a] + tt.w - 1) / tt.w) * ((P.map_h[a] + tt.h - 1) / tt.h));
         P.nblk[a] = nb;
         P.max_nblk = std::max(P.max_nblk, nb);
         P.blk_off[a] = bo;
@@ -549,6 +656,10 @@ int build_plan(fpm_ctx* ctx) {
     HIP_TRY(hipMemcpyAsync(P.d_jobs.as<char>(P.off_warp), wj.data(), sizeof(WarpJob) * J, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(P.d_jobs.as<char>(P.off_ncc), nj.data(), sizeof(NccJob) * J, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(P.d_jobs.as<char>(P.off_nms), mj.data(), sizeof(NmsJob) * J, hipMemcpyHostToDevice, ctx->stream));
+    {
+        const int rc = plan_top_mma(ctx, P, tt);
+        if (rc != FPM_OK) return rc;
+    }
     {   // k_top_fused's workgroup -> job order: the angles with the largest map x template work first, every source's
         // job of an angle together (one launch covers S x nang jobs in ~1.4 rounds of resident workgroups at Src7: the
         // cheap jobs fill the last round); a scheduling choice only, every job writes its own outputs
@@ -655,6 +766,11 @@ int enqueue_search(fpm_ctx* ctx) {
         // launch limit (tests/test_gpu_parity.py::test_top_fused_lds_threshold runs canvases either side of it)
         if (top_mode == 0 || fused_lds > top_fused_lds_limit()) fused_lds = 0;
     }
+    // the matrix-core top layer (k_top_mma + greedy peaks from its lists) where the plan admits it, except where the
+    // fused small-canvas kernel applies; FPM_TOP_MMA=1 takes it there too (read when the search is recorded)
+    const char* mma_env = getenv("FPM_TOP_MMA");
+    const bool use_mma = P.top_mma && (fused_lds == 0 || (mma_env && atoi(mma_env) == 1));
+    if (use_mma) fused_lds = 0;
     int32_t* live[2] = {P.d_live.as<int32_t>(), P.d_live.as<int32_t>() + P.C};
     int32_t* livecnt = P.d_livecnt.as<int32_t>();
     CandInitArgs ca;   // the top peaks -> candidate states and the first live list (k_cand_init, or fused in k_nms)
@@ -675,7 +791,7 @@ int enqueue_search(fpm_ctx* ctx) {
     // L >= 1: the first pyrDown launch zeroes the counters before the top kernel's live-list atomics.  L == 0: no
     // pyramid launch precedes it, so its block 0 zeroes them -- safe only because the candidate init then runs in
     // mode 1 (refine == 0: states and live list written directly, no live-count atomics); launch_top_fused checks it
-    const bool pyr_zero = top_init && L >= 1;
+    const bool pyr_zero = (top_init && L >= 1) || use_mma;   // (use_mma implies L >= 1: plan_top_mma)
     // K1: source pyramid (all staged sources per launch).  Two levels per launch (k_pyr_down2) where the pair's input
     // is small (<= kPyr2MaxBytes over the batch: launch-bound levels, e.g. every pair of a single Src7 search: 14.8 ->
     // 11.3 us for levels 0-2), else one level per launch (k_pyr_down_s keeps more workgroups in flight: 43 Src7 levels
@@ -701,7 +817,7 @@ int enqueue_search(fpm_ctx* ctx) {
                             st, 0, zero, nzero);
         }
     }
-    NmsArgs na;
+    NmsArgs na{};
     na.jobs = P.d_jobs.as<NmsJob>(P.off_nms);
     na.peaks = P.d_peaks.as<Peak>();
     na.counts = P.d_counts.as<int32_t>();
@@ -720,14 +836,54 @@ int enqueue_search(fpm_ctx* ctx) {
                          top_init ? &ca : nullptr, P.d_jobs.as<int32_t>(P.off_order));
         cand_fused = top_init;
     }
+    if (use_mma) {
+        int mdim = 0;
+        long mpx = 0;
+        for (int a = 0; a < P.nang; ++a) {
+            mdim = std::max(mdim, std::max(P.map_w[a], P.map_h[a]));
+            mpx = std::max(mpx, (long)P.map_w[a] * P.map_h[a]);
+        }
+        TopMmaArgs ta = P.tma;
+        {   // canvases, correlation, scores and the lists of outputs >= the layer score; profiling bytes: the top level
+            // read per angle (its share of B_top; the map is never written)
+            ProfScope ps(ctx, FPM_K_TOP_NCC, (int64_t)S * P.nang * top.w * top.h);
+            ta.mode = 0;
+            launch_top_mma(ta, st);
+        }
+        const bool ci_ok = !P.by_block && P.cap <= kNmsInitCap && (size_t)J * P.cap == (size_t)P.C;
+        NmsArgs ga = na;
+        ga.cand = P.d_ncand.as<int32_t>(); ga.cand_val = P.d_tcandv.as<float>();
+        ga.cand_cnt = ta.cand_cnt; ga.cand_cap = P.tcand_cap;
+        ga.reset_untaken = P.by_block ? 1 : 0;
+        {
+            ProfScope ps(ctx, FPM_K_TOP_NMS, 0);
+            launch_top_greedy(ga, J, P.max_cells, st, ci_ok ? &ca : nullptr);
+        }
+        {   // the maps the lists could not give (overflow, or a shape the greedy form does not take): full maps
+            ProfScope ps(ctx, FPM_K_TOP_MAP, 0);
+            ta.mode = 1;
+            launch_top_mma(ta, st);
+        }
+        {   // ... and their peaks by the split kernels, which skip the maps the greedy form took (cand_cnt < 0)
+            ProfScope ps(ctx, FPM_K_TOP_NMS, 0);
+            NmsArgs fa = na;
+            fa.cand = ga.cand; fa.cand_cnt = ga.cand_cnt; fa.cand_cap = P.tcand_cap;
+            if (P.by_block) {
+                fa.skey = (uint64_t*)(P.d_livecnt.as<int32_t>() + P.off_skey);
+                fa.sdone = P.d_livecnt.as<int32_t>() + P.off_skey + 6 * J;
+            }
+            launch_nms(fa, J, P.max_nblk, mdim, P.max_cells, st, P.max_nitems, ci_ok ? &ca : nullptr, mpx);
+        }
+        cand_fused = ci_ok;
+    }
     // profiling bytes: each kernel's share of §8(d)'s B_top = sum_angles (W_L H_L + 4 |R_a|): the rotation reads the
     // top level, the correlation writes the map (the rotated canvases are this design's scratch)
-    if (fused_lds == 0) {
+    if (fused_lds == 0 && !use_mma) {
         const int64_t bytes = (int64_t)P.nang * top.w * top.h;
         ProfScope ps(ctx, FPM_K_TOP_WARP, bytes * S);
         launch_warp(P.d_jobs.as<WarpJob>(P.off_warp), J, P.max_canvas, st, P.d_livecnt.as<int32_t>(), P.nzero);
     }
-    if (fused_lds == 0) {
+    if (fused_lds == 0 && !use_mma) {
         int64_t bytes = 0;
         for (int a = 0; a < P.nang; ++a) bytes += 4LL * P.map_w[a] * P.map_h[a];
         ProfScope ps(ctx, FPM_K_TOP_NCC, bytes * S);
@@ -739,7 +895,7 @@ int enqueue_search(fpm_ctx* ctx) {
             launch_ncc_map(P.d_jobs.as<NccJob>(P.off_ncc), J, P.max_map, tt.w * tt.h, st);
         }
     }
-    if (fused_lds == 0) {
+    if (fused_lds == 0 && !use_mma) {
         ProfScope ps(ctx, FPM_K_TOP_NMS, 0);   // (reads the maps counted once in B_top)
         if (P.by_block) {   // (the counts and strip keys were zeroed by k_warp)
             na.cand = P.d_ncand.as<int32_t>(); na.cand_cnt = P.d_livecnt.as<int32_t>() + L + 2; na.cand_cap = kNmsCandCap;
@@ -901,6 +1057,8 @@ int enqueue_search(fpm_ctx* ctx) {
         PackArgs pa;
         pa.counts = P.d_counts.as<int32_t>(); pa.J = J;
         pa.peaks = P.d_peaks.as<Peak>(); pa.C = P.C;
+        pa.cap = P.cap;
+        if ((size_t)J * P.cap != (size_t)P.C) { ctx->err = "plan layout: C != J * cap"; return FPM_E_INTERNAL; }
         pa.livecnt = livecnt; pa.nlive = L + 2;
         pa.live0 = L > 0 ? live[cur_list] : nullptr;   // the layer-0 list
         pa.live0_count = livecnt + (L > 0 ? L - 1 : 0);

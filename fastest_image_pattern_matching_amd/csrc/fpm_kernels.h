@@ -63,6 +63,8 @@ struct NmsArgs {
     uint64_t* stamps;        // profiling only (scripts/nms_probe.hip): k_nms_fast phase cycles of job 0, else null
     uint64_t* skey;          // s_BlockMax mode: [job][3] strip-block maxima keys, zeroed before the launch
     int32_t* sdone;          // [job][3] finished chunks of each strip block, zeroed before the launch
+    const float* cand_val;   // k_nms_greedy: the candidates' values (k_top_mma's lists), nullptr = read the map
+    int32_t reset_untaken;   // k_nms_greedy: a map it does not take gets cand_cnt = 0 (k_nms_blocks recounts it)
 };
 
 // Angle-tree node: the reference's refinement angle for one path, with glibc trig of angle*D2R.
@@ -159,6 +161,7 @@ struct RoiArgs {
 struct PackArgs {
     const int32_t* counts; int32_t J;
     const Peak* peaks; int32_t C;
+    int32_t cap;                   // peak slots per job (C == J * cap)
     const int32_t* livecnt; int32_t nlive;
     const int32_t* live0;          // layer-0 live list (nullptr when the top layer is layer 0)
     const int32_t* live0_count;
@@ -212,12 +215,49 @@ constexpr int kTopFusedMinJobs = 256;   // fewer jobs than CUs: the three split 
 void launch_top_fused(const WarpJob* wjobs, const NccJob* njobs, const NmsArgs& a, int njobs_n, size_t lds,
                       int32_t* zero, int nzero, hipStream_t st, const CandInitArgs* ci = nullptr,
                       const int32_t* order = nullptr);
+// ---- the top layer on the matrix cores (k_top_mma): warp + TM_CCORR + CCOEFF_Denominator for every (source, angle)
+// job without materialising the rotated canvas or the map.  Work unit = (job, strip of output columns, run of output
+// rows); the host builds the unit list (top_mma_plan).
+struct TopUnit { int32_t job, x0, y0, y1; };
+constexpr int kTopMmaMaxSw = 192;              // strip width cap (output columns)   // output columns [x0, x0 + sw) and rows [y0, y1) of map `job`
+struct TopMmaArgs {
+    const WarpJob* wjobs;    // per job: source level, canvas size (dw x dh), inverse matrix, border
+    const NccJob* njobs;     // per job: map size (ow x oh) and, for mode 1, the map
+    const TopUnit* units;
+    int32_t nunits;
+    const uint8_t* bfrag;    // [nq][64 lanes][16 B] the correlation's B fragments (T - 128 as i8, Toeplitz-banded)
+    int32_t nq, R;           // MFMA slots per 16 x 16 output tile; template rows per slot (2: tw <= 17, 1: tw <= 49)
+    int32_t tw, th, area;
+    uint32_t tsum;           // sum of the template level's pixels
+    int32_t sw;              // strip width (output columns, multiple of 16)
+    int32_t cp;              // canvas ring row pitch (bytes, multiple of 16)
+    int32_t rr;              // ring rows (power of two >= 16 + th - 1): canvas bytes and H2 rows
+    int32_t hp;              // H2 ring row pitch (u32)
+    int32_t ct, rt;          // column / row table capacity (entries)
+    int32_t o_h2, o_colt, o_rowt, o_bf;   // dynamic LDS offsets (bytes)
+    int32_t mode;            // 0: candidate lists, 1: full maps of the jobs with cand_cnt >= 0 (fallback)
+    int32_t prefilter;       // 1: f32 bound before the exact f64 score (area <= 258, thr > 0)
+    float thrK, E;           // prefilter: (thr (1 - 1e-5))^2 * norm^2 * area, absolute slack of the f32 terms
+    double thr, mean, norm, inv_area;
+    int32_t* cand;           // [job][cand_cap] map indices of the outputs with score >= thr
+    float* cand_val;         // [job][cand_cap] their scores
+    int32_t* cand_cnt;       // [job] (zeroed before mode 0; may exceed cand_cap)
+    int32_t cand_cap;
+};
+size_t top_mma_lds(const TopMmaArgs& a);
+// fills the layout fields of `a` (sw, cp, rr, hp, ct, rt, o_*) for a strip width and the largest unit height
+void top_mma_layout(TopMmaArgs& a, int sw, int max_rows);
+bool top_mma_fits(int tw, int th);   // template shapes the kernel takes (R = 2 up to 17 wide, R = 1 up to 49)
+void launch_top_mma(const TopMmaArgs& a, hipStream_t st);
+// k_nms_greedy over k_top_mma's lists (a.cand_val set): plain getNextMaxLoc key (by_block 0) or s_BlockMax key; with ci
+// (plain, cap <= kNmsInitCap) the candidate init of the jobs it takes
+void launch_top_greedy(const NmsArgs& a, int njobs, int max_cells, hipStream_t st, const CandInitArgs* ci);
 void launch_roi_tables(const RoiArgs& a, hipStream_t st);
 void launch_roi_warp(const RoiArgs& a, hipStream_t st);
 void launch_roi_corr(const RoiArgs& a, hipStream_t st);
-bool launch_roi_corr16(const RoiArgs& a, hipStream_t st);   // false: the shape does not fit its form
 void launch_roi_eval(const RoiArgs& a, hipStream_t st);
 #ifdef FPM_EXPERIMENTAL   // measurement-only fused K6+K7 (scripts/fused_bench.hip; never in libfpm_hip.so)
+bool launch_roi_corr16(const RoiArgs& a, hipStream_t st);   // k_roi_corr16 (scripts/corr16_bench.hip)
 bool roi_fused_fits(int tw);           // the fused sampling + correlation kernel applies (templates <= 1024 wide)
 int roi_fused_parts(int th);           // runs of bands per ROI (work units per ROI) of k_roi_fused
 void launch_roi_fused(const RoiArgs& a, hipStream_t st);

@@ -1058,6 +1058,7 @@ __device__ __forceinline__ void nms_scan(const NmsArgs& a, const NmsJob& j, int3
 __global__ __launch_bounds__(256) void k_nms_blocks(NmsArgs a) {
     const NmsJob& j = a.jobs[blockIdx.y];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (a.cand && a.cand_cnt[blockIdx.y] < 0) return;   // taken by k_nms_greedy from k_top_mma's list (no map)
     BlockGeom g;
     g.init(j.mw, j.mh, a.tw, a.th, a.mfc);
     if (j.mw <= 0 || j.mh <= 0) return;
@@ -1615,21 +1616,32 @@ __device__ __forceinline__ bool greedy_before(float va, uint64_t ka, float vb, u
     return va > vb || (va == vb && ka < kb);
 }
 
-__global__ __launch_bounds__(256) void k_nms_greedy(NmsArgs a) {
+// Also the plain getNextMaxLoc loop (a.by_block == 0, TemplateMatcher.cpp:197-212 / :1196-1206): with every painted
+// rectangle the reference takes the first maximum of the map in row-major order, so the key is the position alone
+// (block 0 for every pixel), and the same greedy pass gives its peaks.  a.cand_val: the candidates' values come with the
+// list (k_top_mma, which never writes the map); ci_mode != 0 (plain path, cap <= kNmsInitCap): the candidate init of
+// the jobs this kernel takes (cand_init_job, as k_nms does); a.reset_untaken: a job it does not take gets cand_cnt = 0,
+// so k_nms_blocks can list that job's pixels again from the fallback map.
+__global__ __launch_bounds__(256) void k_nms_greedy(NmsArgs a, CandInitArgs ci, int ci_mode) {
     extern __shared__ __attribute__((aligned(16))) uint8_t nms_lds[];
+    __shared__ Peak spk[kNmsInitCap];
+    __shared__ int sbase, scnt;
     const NmsJob& j = a.jobs[blockIdx.x];
     const float* m = j.map;
     const int mw = j.mw, mh = j.mh, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const double ov = a.overlap;
     const int tw = a.tw, th = a.th;
     const int rw = (int)(2 * tw * (1 - ov)), rh = (int)(2 * th * (1 - ov));
+    const bool plain = !a.by_block;
     BlockGeom g;
     g.init(mw, mh, tw, th, a.mfc);
     const int K = a.cand_cnt[blockIdx.x];
     const int cxn = (mw + tw - 1) / tw, cyn = (mh + th - 1) / th, ncell = cxn * cyn;
-    if (!(mw > 0 && mh > 0 && g.ncol > 0 && g.nrow > 0 && rw > 0 && rh > 0 && a.thr > -1.0 && K >= 0 &&
-          K <= a.cand_cap && K <= kGreedyMax && ncell <= a.lds_blocks))
+    if (!(mw > 0 && mh > 0 && (plain || (g.ncol > 0 && g.nrow > 0)) && rw > 0 && rh > 0 && a.thr > -1.0 && K >= 0 &&
+          K <= a.cand_cap && K <= kGreedyMax && ncell <= a.lds_blocks)) {
+        if (a.reset_untaken && tid == 0 && K >= 0) a.cand_cnt[blockIdx.x] = 0;
         return;
+    }
     int P = 64;
     while (P < K) P <<= 1;
     float* sv = (float*)nms_lds;                       // [kGreedyMax] values
@@ -1644,8 +1656,8 @@ __global__ __launch_bounds__(256) void k_nms_greedy(NmsArgs a) {
             const int idx = cand[i], x = idx % mw, y = idx / mw;
             int b2;
             // MFC: the last block wins equal maxima, so the block part of the key counts down
-            const int b = g.mfc ? g.nb - 1 - nms_block_of_mfc(g, x, y) : nms_block_of(g, x, y, tw, th, b2);
-            sv[i] = m[idx];
+            const int b = plain ? 0 : g.mfc ? g.nb - 1 - nms_block_of_mfc(g, x, y) : nms_block_of(g, x, y, tw, th, b2);
+            sv[i] = a.cand_val ? a.cand_val[(size_t)blockIdx.x * a.cand_cap + i] : m[idx];
             sk[i] = ((uint64_t)b << 32) | (uint32_t)((y << 16) | x);
         } else {
             sv[i] = -INFINITY;
@@ -1669,9 +1681,9 @@ __global__ __launch_bounds__(256) void k_nms_greedy(NmsArgs a) {
             }
             __syncthreads();
         }
-    if (wv != 0) return;
     Peak* out = a.peaks + (size_t)blockIdx.x * a.cap;
     int cnt = 0;
+    if (wv == 0) {
     for (int base = 0; base < K && cnt < a.cap; base += 64) {
         const int i = base + lane;
         const bool valid = i < K;
@@ -1704,6 +1716,7 @@ __global__ __launch_bounds__(256) void k_nms_greedy(NmsArgs a) {
             if (lane == 0) {
                 out[cnt].x = tx; out[cnt].y = ty; out[cnt].score = tv;
                 accx[cnt] = sx; accy[cnt] = sy;
+                if (ci_mode && cnt < kNmsInitCap) { spk[cnt].x = tx; spk[cnt].y = ty; spk[cnt].score = tv; }
             }
             // register the rectangle in the <= 3 x 3 cells it covers (lanes 0-8)
             const int cx0 = max(sx, 0) / tw, cx1 = min(sx + rw - 1, mw - 1) / tw;
@@ -1726,7 +1739,13 @@ __global__ __launch_bounds__(256) void k_nms_greedy(NmsArgs a) {
     }
     if (lane == 0) {
         a.counts[blockIdx.x] = cnt;
-        a.cand_cnt[blockIdx.x] = -1;   // taken by this form: k_nms_fast skips the map
+        a.cand_cnt[blockIdx.x] = -1;   // taken by this form: k_nms_fast / k_nms / k_top_mma's fallback skip the map
+        scnt = cnt;
+    }
+    }   // wave 0
+    if (ci_mode) {   // workgroup-uniform: every wave reaches it
+        __syncthreads();
+        cand_init_job(ci, ci_mode, blockIdx.x, scnt, spk, &sbase);
     }
 }
 
@@ -1768,7 +1787,7 @@ void launch_nms(const NmsArgs& a0, int njobs, int max_blocks, int max_map_dim, i
             if (greedy) {
                 NmsArgs gA = a;
                 gA.lds_blocks = max_cells;
-                hipLaunchKernelGGL(k_nms_greedy, dim3(njobs), dim3(256), nms_greedy_lds(max_cells), st, gA);
+                hipLaunchKernelGGL(k_nms_greedy, dim3(njobs), dim3(256), nms_greedy_lds(max_cells), st, gA, cz, 0);
             }
             a.lds_blocks = 0;
             hipLaunchKernelGGL(k_nms, dim3(njobs), dim3(256), blds, st, a, cz, 0, blk);
@@ -1785,7 +1804,7 @@ void launch_nms(const NmsArgs& a0, int njobs, int max_blocks, int max_map_dim, i
             if (greedy) {
                 NmsArgs gA = a;
                 gA.lds_blocks = max_cells;
-                hipLaunchKernelGGL(k_nms_greedy, dim3(njobs), dim3(256), nms_greedy_lds(max_cells), st, gA);
+                hipLaunchKernelGGL(k_nms_greedy, dim3(njobs), dim3(256), nms_greedy_lds(max_cells), st, gA, cz, 0);
             }
             hipLaunchKernelGGL(k_nms_fast, dim3(njobs), dim3(256), lds, st, a);
             return;
@@ -3469,6 +3488,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
+#ifdef FPM_EXPERIMENTAL   // measured slower (bench 33.02k vs 34.10k searches/s): scripts/corr16_bench.hip only
 // ---- K7, round 5: the register-A / LDS-DMA correlation with items of ONE 16-row M tile (k_roi_corr's band is two).
 // A k_roi_corr item waits for its 38 ROI rows (one LDS-DMA round trip) and two barriers before its matrix work, and
 // its 40 KB of LDS allow 4 items in flight per CU.  Here an item is (ROI, 16 template rows = one window-sum chunk):
@@ -3664,6 +3684,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         flush();
     }
 }
+
+#endif   // FPM_EXPERIMENTAL (k_roi_corr16)
 
 #ifdef FPM_EXPERIMENTAL   // measurement-only kernel (scripts/fused_bench.hip); the product Makefile never defines it
 // ---- K6+K7 fused (templates too large for k_roi_small): the ROI never leaves the CU.  A work unit is one ROI and
@@ -3966,8 +3988,15 @@ struct SmallLayout {
 // diagonal D (+ the sampling margins and alignment of k_roi_small: width <= D + 14, height <= D + 4), so where that
 // box is smaller than the per-wave tile buffers U is sized to it and the tile path is never taken (it then reads
 // its taps from global memory, should it be).  nw = waves per workgroup.
+// (integer arithmetic only: host and device must size the LDS regions identically, so no sqrtf whose rounding could
+// differ between the two compilations; isqrt_ceil = the smallest d with d * d >= n)
+__host__ __device__ inline int isqrt_ceil(int n) {
+    int d = 0;
+    while ((d + 1) * (d + 1) <= n) ++d;   // floor(sqrt(n)) (n < 2^21 here: a ROI diagonal, at most ~1500 steps)
+    return d * d == n ? d : d + 1;
+}
 __host__ __device__ inline int small_footprint_bound(int rw, int rh) {
-    const int d = (int)ceilf(sqrtf((float)((rw - 1) * (rw - 1) + (rh - 1) * (rh - 1)))) + 2;
+    const int d = isqrt_ceil((rw - 1) * (rw - 1) + (rh - 1) * (rh - 1)) + 2;
     return ((d + 16) * (d + 6) + 15) & ~15;
 }
 __host__ __device__ inline SmallLayout small_layout(int tw, int th, int nw = 4) {
@@ -4615,7 +4644,21 @@ constexpr int kWarpFootBatch = 12, kWarpWaves = 8;
 // uncapped grids of round 4), unset: the defaults at each launch below.
 static int grid_cap_env(const char* v, int dflt) { return v ? (atoi(v) > 0 ? atoi(v) : 0) : dflt; }
 static int capped(int grid, int cap) { return cap > 0 && grid > cap ? cap : grid; }
-constexpr int kCUs = 256;   // MI355X
+// the device's compute units (hipDeviceProp_t::multiProcessorCount, read once per device; 256 on MI355X): the
+// persistent grids and the lone-search rules below scale with it
+static int device_cus() {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    static std::mutex mu;
+    static std::map<int, int> cus;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cus.find(dev);
+    if (it != cus.end()) return it->second;
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+    return n;
+}
 void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0 || a.equal1) return;
     const long tiles = (long)a.slot_cap * ((a.th + 6 + ROI_T - 1) / ROI_T) * ((a.tw + 6 + ROI_T - 1) / ROI_T);
@@ -4636,7 +4679,7 @@ void launch_roi_warp(const RoiArgs& a, hipStream_t st) {
         // 15.1 us (profiles/r05m vs r05_end lat_*.txt); larger batches keep the full grid (its dynamic balance beats the
         // persistent grid's static task ranges, r05j)
         const int srcs = a.slot_cap / std::max(1, a.per_source * a.n3);
-        const int dflt_cap = srcs <= 2 ? 7 * kCUs : 0;
+        const int dflt_cap = srcs <= 2 ? 7 * device_cus() : 0;
         hipLaunchKernelGGL((k_roi_warp3<7, kFtPitch, 0>), dim3(capped((int)(want3 < 16384 ? want3 : 16384), grid_cap_env(getenv("FPM_GRID_WARP"), dflt_cap))),
                            dim3(256), 0, st, a);
         return;
@@ -4650,7 +4693,6 @@ constexpr int kCorrWaves = 3;
 // register-A form at 13-16 k-steps: 2 waves per SIMD (A fragments + prefetched rows: 221 VGPRs), one workgroup per
 // resident slot (MI355X: 256 CUs)
 constexpr int kCorrRunWaves = 2;
-constexpr int kCorrRunWGs = 256 * kCorrRunWaves;
 template <int NK>
 static void launch_corr_regs(const RoiArgs& a, long items, size_t lds, hipStream_t st) {
     if constexpr (NK <= 12) {
@@ -4661,7 +4703,7 @@ static void launch_corr_regs(const RoiArgs& a, long items, size_t lds, hipStream
         // ... and at 8 k-steps since the load addressing is scalar (136 VGPRs at 3 waves, 4 spilled at 4 waves: Src7
         // layer 1 107.7 -> 99.4 us per 43-source microbenchmark launch, profiles/r03_y)
         if (NK == 4 && lds * 4 <= kLdsPerCu) {
-            const int grid = capped((int)(items < 256 * 4 ? items : 256 * 4), grid_cap_env(getenv("FPM_GRID_CORR"), 0));
+            const int grid = capped((int)std::min<long>(items, 4L * device_cus()), grid_cap_env(getenv("FPM_GRID_CORR"), 0));
             hipLaunchKernelGGL((k_roi_corr<0, true, 4, NK, false, 1, true>), dim3(grid), dim3(256), lds, st, a);
             return;
         }
@@ -4669,19 +4711,20 @@ static void launch_corr_regs(const RoiArgs& a, long items, size_t lds, hipStream
         // (43 Src7 sources: layer 0 269.8 -> 241.1 us, profiles/r04/mb_r04e.txt; layer 1 103.0 -> 93.5 us,
         // profiles/r04/mbl1_r04g.txt; host-checked)
         if ((NK == 8 || NK == 12) && lds * 4 <= kLdsPerCu) {
-            const int grid = capped((int)(items < 256 * 4 ? items : 256 * 4), grid_cap_env(getenv("FPM_GRID_CORR"), 0));
+            const int grid = capped((int)std::min<long>(items, 4L * device_cus()), grid_cap_env(getenv("FPM_GRID_CORR"), 0));
             hipLaunchKernelGGL((k_roi_corr<0, true, 4, NK, false, 1, true, true>), dim3(grid), dim3(256), lds, st, a);
             return;
         }
         // row results staged in LDS and flushed during the next item's staging (SE; Src7 microbenchmark at 43 sources:
         // layer 0 293.6 -> 264.4 us, layer 1 124.2 -> 115.4, bit-identical)
-        const int grid = capped((int)(items < 256 * kCorrWaves ? items : 256 * kCorrWaves), grid_cap_env(getenv("FPM_GRID_CORR"), 0));
+        const int grid = capped((int)std::min<long>(items, (long)kCorrWaves * device_cus()), grid_cap_env(getenv("FPM_GRID_CORR"), 0));
         hipLaunchKernelGGL((k_roi_corr<0, true, kCorrWaves, NK, false, 1, true>), dim3(grid), dim3(256), lds, st, a);
     } else {
-        const int grid = (int)(items < kCorrRunWGs ? items : kCorrRunWGs);
+        const int grid = (int)std::min<long>(items, (long)kCorrRunWaves * device_cus());
         hipLaunchKernelGGL((k_roi_corr<0, true, kCorrRunWaves, NK>), dim3(grid), dim3(256), lds, st, a);
     }
 }
+#ifdef FPM_EXPERIMENTAL
 // k_roi_corr16 (16-row items, 2-wave workgroups): as many workgroups as the LDS holds per CU, persistent
 bool launch_roi_corr16(const RoiArgs& a, hipStream_t st) {
     if (a.nk > 12 || (a.roi_pitch >> 4) > 64) return false;
@@ -4689,18 +4732,17 @@ bool launch_roi_corr16(const RoiArgs& a, hipStream_t st) {
     const int per_cu = (int)std::min<size_t>(8, kLdsPerCu / lds);
     if (per_cu < 1) return false;
     const long items = (long)a.slot_cap * ((a.th + kB16Rows - 1) / kB16Rows);
-    const int grid = capped((int)std::min<long>(items, (long)per_cu * kCUs), grid_cap_env(getenv("FPM_GRID_CORR"), 0));
+    const int grid = capped((int)std::min<long>(items, (long)per_cu * device_cus()), grid_cap_env(getenv("FPM_GRID_CORR"), 0));
     if (a.nk <= 4) hipLaunchKernelGGL((k_roi_corr16<4, 4>), dim3(grid), dim3(128), lds, st, a);
     else if (a.nk <= 8) hipLaunchKernelGGL((k_roi_corr16<8, 4>), dim3(grid), dim3(128), lds, st, a);
     else hipLaunchKernelGGL((k_roi_corr16<12, 4>), dim3(grid), dim3(128), lds, st, a);
     return true;
 }
 
+#endif
+
 void launch_roi_corr(const RoiArgs& a, hipStream_t st) {
     if (a.slot_cap <= 0 || a.equal1) return;
-    // FPM_CORR16=1: the 16-row-item form (measurement switch while it is evaluated; read when a search is recorded)
-    const char* c16 = getenv("FPM_CORR16");
-    if (c16 && atoi(c16) == 1 && launch_roi_corr16(a, st)) return;
     const size_t lds = roi_corr_lds(a.roi_pitch, a.tw, a.rc, kCorrGlobalA);
     // register-A form where its staged rows fit one 64-lane pass and A fits 16 k-steps (templates <= 1024 wide);
     // the slot-major form below serves wider templates
@@ -4759,6 +4801,7 @@ void launch_roi_small(const RoiArgs& a, hipStream_t st) {
     // thousands of candidates (Src10 +-180, TargetNum 100: 14.8 K), whose ROIs need the residency of the smaller forms.
     // FPM_SMALL_NT=512 forces them, another value keeps them off.
     const int srcs = a.slot_cap / std::max(1, a.per_source * a.n3);
+    const int kCUs = device_cus();
     if (nte ? atoi(nte) == 512 : (srcs <= 2 && a.slot_cap <= 4 * kCUs)) {
         const size_t lds8 = (size_t)small_layout(a.tw, a.th, 8).total;
         const int grid = capped(a.slot_cap < 8192 ? a.slot_cap : 8192, grid_cap_env(getenv("FPM_GRID_SMALL"), kCUs));
@@ -4822,6 +4865,258 @@ void launch_cand_step(const RoiArgs& a, int max_items, hipStream_t st) {
     hipLaunchKernelGGL(k_cand_step, dim3(grid), dim3(256), 0, st, a);
 }
 
+// ============================================================================================== K2-K5 on the matrix cores
+// The top layer of a search whose canvases or angle count are large (BASELINE configs[3] at 1 deg: 361 angles of
+// ~150 x 150 maps per source; configs[2] at +-180: 47 maps of ~1150 x 1150), TemplateMatcher.cpp:162-211.  One kernel
+// per search does, for every (source, angle) job, the rotated canvas (cv::warpAffine, the same fixed-point tables and
+// taps as k_warp), TM_CCORR and CCOEFF_Denominator (the exact integer correlation rounded once to f32, the f64
+// normalisation of k_ncc_tile), without writing the canvas or the map: the only pixels the peak loop can ever take are
+// those with a score >= the top-layer score (k_nms_greedy's argument), so the kernel lists those (index, score) per
+// job and k_nms_greedy (plain or s_BlockMax key) takes the peaks from the list.  A job whose list overflows (or that the
+// greedy form cannot take) gets its full map from a second launch of this kernel (mode 1) and the split peak kernels.
+//
+// Work unit: one job's strip of sw output columns, walked down in bands of 16 output rows.  Per band:
+//   sampling  the band's new canvas rows (sw + tw - 1 columns) into an LDS ring as i8 (x ^ 0x80), one word of four
+//             pixels per item, taps from the source level in global memory (L1/L2-resident: the top level is small);
+//   H2        per new canvas row and output column, the sum of I^2 over the template width (sliding, exact u32);
+//   MFMA      per 16 x 16 output tile and wave: D += A B on v_mfma_i32_16x16x64_i8 with A = canvas rows (the 16 output
+//             rows; K = 64 = two template rows x 32 columns, or one row x 64 columns for templates 18-49 wide) and B =
+//             the template row Toeplitz-banded over the 16 output columns (B[c][n] = T'[r][c - n], zero outside
+//             0 <= c - n < tw), so sum_slots D = sum T'I' exactly; a second MFMA with B = the band of ones gives
+//             sum I' over the window.  Exact: sum T I = sum T'I' + 128 (sum I + sum T) - 16384 area;
+//   epilogue  sum I^2 over the window from th + 3 H2 rows per lane (sliding over the lane's 4 output rows), then a
+//             conservative f32 bound (nf^2 >= thr^2 norm^2 area df, nf = area ccorr - sum I sum T, df = area sum I^2 -
+//             (sum I)^2, with an absolute slack E on the two f32 terms) and, where it passes, the exact f64 score.
+// Exactness of the bound (prefilter): for area <= 258 every integer term is < 2^24 (exact in f32); the two products
+// carry at most 512 of rounding each (E = 1024), and thrK includes a 1e-5 relative margin over the f64 evaluation's
+// and the f32 score rounding's relative errors (<= 1e-6), so no output with (double)score >= thr is ever rejected.
+constexpr int TM_BH = 16;            // output rows per band (one MFMA M block)
+
+bool top_mma_fits(int tw, int th) { return tw >= 1 && th >= 1 && ((tw <= 17 && th <= 32) || (tw <= 49 && th <= 16)); }
+
+void top_mma_layout(TopMmaArgs& a, int sw, int max_rows) {
+    a.sw = sw;
+    a.R = a.tw <= 17 ? 2 : 1;
+    a.nq = a.R == 2 ? (a.th + 1) / 2 : a.th;
+    a.cp = sw + 64;                                  // A fragments read <= sw + 47, H2 runs <= sw + tw + 6
+    int rr = 1;
+    while (rr < TM_BH + a.th - 1) rr <<= 1;
+    a.rr = rr;
+    a.hp = sw + 4;                                   // (4g-row groups of a wave land 16 banks apart)
+    a.ct = sw + 64;
+    a.rt = max_rows + a.th + TM_BH;
+    a.o_h2 = a.rr * a.cp;
+    a.o_colt = a.o_h2 + 4 * a.rr * a.hp;
+    a.o_rowt = a.o_colt + 8 * a.ct;
+    a.o_bf = (a.o_rowt + 8 * a.rt + 15) & ~15;
+}
+size_t top_mma_lds(const TopMmaArgs& a) { return (size_t)a.o_bf + 1024 * (size_t)a.nq; }
+
+__global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t tm_lds[];
+    uint8_t* const ring = tm_lds;
+    uint32_t* const h2 = (uint32_t*)(tm_lds + a.o_h2);
+    int32_t* const cad = (int32_t*)(tm_lds + a.o_colt);   // adelta [ct], bdelta [ct] of the unit's canvas columns
+    int32_t* const rxy = (int32_t*)(tm_lds + a.o_rowt);   // X0 [rt], Y0 [rt] of its canvas rows
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int ln = lane & 15, lg = lane >> 4;
+    const int tw = a.tw, th = a.th, mask = a.rr - 1, cp = a.cp, hp = a.hp;
+    // the B fragments (correlation) staged once into LDS; the band of ones (window sum of I') in registers: byte i of
+    // lane (n, g) is k = 16 g + i
+    fpm_v4i* const bl = (fpm_v4i*)(tm_lds + a.o_bf);
+    for (int i = tid; i < a.nq * 64; i += 256) bl[i] = *(const fpm_v4i*)(a.bfrag + (size_t)i * 16);
+    fpm_v4i ones;
+    {
+        const int c0 = a.R == 2 ? 16 * (lg & 1) : 16 * lg;
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (int i = 0; i < 16; ++i) {
+            const int c = c0 + i - ln;
+            if (c >= 0 && c < tw) w[i >> 2] |= 1u << (8 * (i & 3));
+        }
+        ones = fpm_v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
+    }
+    const fpm_v4i zero4 = {0, 0, 0, 0};
+    const uint32_t area = (uint32_t)a.area;
+    const float areaf = (float)a.area, tsumf = (float)a.tsum;
+    for (int u = blockIdx.x; u < a.nunits; u += gridDim.x) {
+        const TopUnit U = a.units[u];
+        if (a.mode == 1 && a.cand_cnt[U.job] < 0) continue;   // (uniform) taken from its list: no map needed
+        const WarpJob& W = a.wjobs[U.job];
+        const NccJob& NJ = a.njobs[U.job];
+        const int mw = NJ.ow;
+        const int swu = min(a.sw, mw - U.x0);                 // output columns of this strip
+        const int ncols = swu + tw - 1;                       // canvas columns it reads (<= dw - x0)
+        const int nrows = min(U.y1 + th - 1, W.dh) - U.y0;    // canvas rows of the unit
+        const uint8_t* src = W.src;
+        const int sw = W.sw, sh = W.sh, sp = W.sp, border = W.border;
+        __syncthreads();   // the previous unit is done with the LDS
+        for (int i = tid; i < ncols; i += 256) {
+            const int x = U.x0 + i;
+            cad[i] = rint_i(W.M[0] * x * kAbScale);
+            cad[a.ct + i] = rint_i(W.M[3] * x * kAbScale);
+        }
+        for (int i = tid; i < nrows; i += 256) {
+            const int y = U.y0 + i;
+            rxy[i] = rint_i((W.M[1] * y + W.M[2]) * kAbScale) + kRoundDelta;
+            rxy[a.rt + i] = rint_i((W.M[4] * y + W.M[5]) * kAbScale) + kRoundDelta;
+        }
+        const int ncw = (ncols + 3) >> 2, nruns = (swu + 7) >> 3, nbu = (swu + 15) >> 4;
+        for (int yb = U.y0; yb < U.y1; yb += TM_BH) {
+            const int rs = yb == U.y0 ? yb : yb + th - 1;
+            const int re = min(yb + TM_BH + th - 1, U.y0 + nrows);
+            __syncthreads();   // tables ready / the previous band's tiles are done with the ring rows replaced now
+            // ---- the band's new canvas rows (cv::warpAffine, k_warp's integers), flipped to i8
+            for (int it = tid; it < (re - rs) * ncw; it += 256) {
+                const int r = it / ncw, k = it - r * ncw;
+                const int y = rs + r, ry = y - U.y0;
+                const int X0 = rxy[ry], Y0 = rxy[a.rt + ry];
+                uint32_t word = 0;
+#pragma unroll 1
+                for (int b = 0; b < 4; ++b) {
+                    const int x = 4 * k + b;
+                    if (x < ncols) {
+                        const int X = (X0 + cad[x]) >> (kAbBits - kInterBits);
+                        const int Y = (Y0 + cad[a.ct + x]) >> (kAbBits - kInterBits);
+                        word |= (uint32_t)warp_tap(src, sw, sh, sp, X, Y, border) << (8 * b);
+                    }
+                }
+                *(uint32_t*)(ring + (size_t)(y & mask) * cp + 4 * k) = word ^ kRoiFlip;
+            }
+            __syncthreads();
+            // ---- H2: per new row, sum of I^2 over [x, x + tw) for the strip's output columns, 8 per item (sliding)
+            for (int it = tid; it < (re - rs) * nruns; it += 256) {
+                const int r = it / nruns, k = it - r * nruns;
+                const int y = rs + r;
+                const uint8_t* row = ring + (size_t)(y & mask) * cp + 8 * k;
+                uint32_t h = 0;
+                int jx = 0;
+                for (; jx + 4 <= tw; jx += 4) {
+                    const uint32_t w = *(const uint32_t*)(row + jx) ^ kRoiFlip;
+                    h = __builtin_amdgcn_udot4(w, w, h, false);
+                }
+                for (; jx < tw; ++jx) {
+                    const uint32_t b = row[jx] ^ 0x80u;
+                    h += b * b;
+                }
+                uint32_t o[8];
+                o[0] = h;
+#pragma unroll
+                for (int i = 1; i < 8; ++i) {
+                    const uint32_t bn = row[i + tw - 1] ^ 0x80u, bo = row[i - 1] ^ 0x80u;
+                    h = h + bn * bn - bo * bo;
+                    o[i] = h;
+                }
+                uint32_t* hd = h2 + (size_t)(y & mask) * hp + 8 * k;
+                *(uint4*)hd = make_uint4(o[0], o[1], o[2], o[3]);
+                *(uint4*)(hd + 4) = make_uint4(o[4], o[5], o[6], o[7]);
+            }
+            __syncthreads();
+            // ---- the band's 16 x 16 output tiles, one wave each
+            for (int nb = wv; nb < nbu; nb += 4) {
+                fpm_v4i acc = zero4, acc1 = zero4;
+                const int co = a.R == 2 ? 16 * (lg & 1) : 16 * lg;
+                const int rstep = a.R == 2 ? 2 : 1;
+                int ro = a.R == 2 ? (lg >> 1) : 0;
+                for (int q = 0; q < a.nq; ++q, ro += rstep) {
+                    const fpm_v4i av = *(const fpm_v4i*)(ring + (size_t)((yb + ln + ro) & mask) * cp + 16 * nb + co);
+                    const fpm_v4i bv = bl[q * 64 + lane];
+                    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv, acc, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, ro < th ? ones : zero4, acc1, 0, 0, 0);
+                }
+                // D: column ln = output column 16 nb + ln, rows 4 lg + i = output rows yb + 4 lg + i
+                const int xo = 16 * nb + ln, yo0 = yb + 4 * lg;
+                const uint32_t* hc = h2 + xo;
+                uint32_t hs = 0;
+                for (int k = 0; k < th; ++k) hs += hc[(size_t)((yo0 + k) & mask) * hp];
+                uint32_t wq[4];
+                wq[0] = hs;
+#pragma unroll
+                for (int i = 1; i < 4; ++i) {
+                    hs += hc[(size_t)((yo0 + th - 1 + i) & mask) * hp] - hc[(size_t)((yo0 + i - 1) & mask) * hp];
+                    wq[i] = hs;
+                }
+                // the cheap part for the lane's 4 outputs: exact integer sums and the prefilter
+                uint32_t ccv[4], wsv[4];
+                uint32_t pm = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    wsv[i] = (uint32_t)acc1[i] + 128u * area;
+                    ccv[i] = (uint32_t)acc[i] + 128u * (wsv[i] + a.tsum) - 16384u * area;
+                    bool pass = yo0 + i < U.y1 && xo < swu;
+                    if (pass && a.mode == 0 && a.prefilter) {
+                        const float wsf = (float)wsv[i];
+                        const float nf = __builtin_fmaf(areaf, (float)ccv[i], -(wsf * tsumf));
+                        const float df = __builtin_fmaf(areaf, (float)wq[i], -(wsf * wsf));
+                        const float nfp = nf + a.E;
+                        pass = nfp > 0.f && nfp * nfp >= a.thrK * (df - a.E);
+                    }
+                    pm |= pass ? 1u << i : 0u;
+                }
+                // the exact f64 score where the bound passed (rare in mode 0; every valid output in mode 1), one
+                // instance of ccoeff in a data-dependent loop (the register budget of the MFMA loop stays small)
+                float sv0 = 0.f, sv1 = 0.f, sv2 = 0.f, sv3 = 0.f;
+                uint32_t tk = 0;
+                while (pm) {
+                    const int i = __builtin_ctz(pm);
+                    pm &= pm - 1;
+                    const uint32_t cc = i == 0 ? ccv[0] : i == 1 ? ccv[1] : i == 2 ? ccv[2] : ccv[3];
+                    const uint32_t ws = i == 0 ? wsv[0] : i == 1 ? wsv[1] : i == 2 ? wsv[2] : wsv[3];
+                    const uint32_t qs = i == 0 ? wq[0] : i == 1 ? wq[1] : i == 2 ? wq[2] : wq[3];
+                    const double num = (double)(float)(double)cc;   // TM_CCORR's f32 result
+                    const float sc = ccoeff(num, (double)ws, (double)qs, a.mean, a.norm, a.inv_area);
+                    if (a.mode == 1) {
+                        NJ.out[(size_t)(yo0 + i) * mw + U.x0 + xo] = sc;
+                    } else if ((double)sc >= a.thr) {
+                        tk |= 1u << i;
+                        if (i == 0) sv0 = sc; else if (i == 1) sv1 = sc; else if (i == 2) sv2 = sc; else sv3 = sc;
+                    }
+                }
+                if (a.mode == 0) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const bool take = (tk >> i) & 1u;
+                        const uint64_t mk = __ballot(take);
+                        if (mk) {   // (wave-uniform; rare) one atomic per wave and output row
+                            int base = 0;
+                            if (lane == 0) base = atomicAdd(&a.cand_cnt[U.job], __popcll(mk));
+                            base = __shfl(base, 0);
+                            if (take) {
+                                const int pos = base + __popcll(mk & ((1ull << lane) - 1));
+                                if (pos < a.cand_cap) {
+                                    a.cand[(size_t)U.job * a.cand_cap + pos] = (yo0 + i) * mw + U.x0 + xo;
+                                    a.cand_val[(size_t)U.job * a.cand_cap + pos] =
+                                        i == 0 ? sv0 : i == 1 ? sv1 : i == 2 ? sv2 : sv3;
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+void launch_top_mma(const TopMmaArgs& a, hipStream_t st) {
+    if (a.nunits <= 0) return;
+    const size_t lds = top_mma_lds(a);
+    // mode 1 touches only the jobs left by the greedy form (usually none): a small grid walks the unit list
+    const int grid = a.mode == 1 ? std::min(a.nunits, 4 * device_cus()) : a.nunits;
+    ensure_lds_attr((const void*)k_top_mma, lds);
+    hipLaunchKernelGGL(k_top_mma, dim3(grid), dim3(256), lds, st, a);
+}
+
+void launch_top_greedy(const NmsArgs& a0, int njobs, int max_cells, hipStream_t st, const CandInitArgs* ci) {
+    if (njobs <= 0) return;
+    NmsArgs a = a0;
+    a.lds_blocks = max_cells;
+    CandInitArgs cz{};
+    const bool fuse = ci && !a.by_block && a.cap <= kNmsInitCap;
+    const int mode = !fuse ? 0 : (ci->refine == 0 ? 1 : (ci->refine == 2 ? 3 : 2));
+    const size_t lds = nms_greedy_lds(max_cells);
+    ensure_lds_attr((const void*)k_nms_greedy, lds);
+    hipLaunchKernelGGL(k_nms_greedy, dim3(njobs), dim3(256), lds, st, a, fuse ? *ci : cz, mode);
+}
+
 // ============================================================================================== pack
 __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
     const int tid = blockIdx.x * 256 + threadIdx.x, nthr = gridDim.x * 256;
@@ -4830,7 +5125,7 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
     // only the slots below each job's peak count (the host reads no others): at Src7's top layer ~1 slot in 10, the
     // rest of the 16-byte slots need not cross PCIe
     int4* hp = (int4*)(a.host + a.o_peaks);
-    const int cap = a.J > 0 ? a.C / a.J : 1;
+    const int cap = a.cap;   // peak slots per job (P.cap; the host checks C == J * cap before the launch)
     for (int i = tid; i < a.C; i += nthr) {
         const int job = i / cap;
         if (i - job * cap < a.counts[job]) hp[i] = *(const int4*)(a.peaks + i);
@@ -4853,7 +5148,12 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
             hr[i] = ((const uint32_t*)(a.rec + (size_t)a.live0[li] * a.n3 + j))[w];
         }
     }
-    __threadfence_system();
+    // The one visibility rule for the kernels that write mapped pinned host memory (k_pack, k_overlap_pairs): plain
+    // stores, no fence in the kernel; the host reads the buffer only after hipStreamSynchronize on the kernel's stream,
+    // which (HIP's synchronisation semantics for host-pinned memory) makes the completed kernel's stores visible to it.
+    // (A system-scope fence per workgroup writes its XCD's L2 back each time: +80 us on the Src10 +-180 tail when
+    // k_overlap_pairs had one, profiles/r05b.)  tests/test_gpu_overlap.py::test_device_filter_twice_in_one_context
+    // and every search's results (read through this buffer) check it.
 }
 
 void launch_pack(const PackArgs& a, hipStream_t st) {
@@ -4947,10 +5247,8 @@ __global__ __launch_bounds__(256) void k_overlap_pairs(const OvRect* __restrict_
         }
         if (lane == 0) { offcnt[2 * i] = base; offcnt[2 * i + 1] = nd; }
     }
-    // lists / offcnt live in mapped pinned host memory: the host reads them only after the stream's next copy and
-    // hipStreamSynchronize, which make the kernel's stores visible to it (HIP's stream-order and synchronisation
-    // semantics for host-pinned memory).  A system-scope fence here in every workgroup (round 4) wrote the L2 back once
-    // per workgroup: +80 us on the Src10 +-180 tail (0.28 -> 0.36 ms, scripts/gpu_tail_ab.sh, profiles/r05b)
+    // lists / offcnt live in mapped pinned host memory: k_pack's visibility rule (no fence; the host reads after
+    // hipStreamSynchronize)
 }
 
 void launch_overlap_pairs(const OvRect* r, const float4* box, int n, double max_overlap, int32_t* lists, int list_cap,

@@ -223,8 +223,8 @@ int fpm_search_bytes(const fpm_ctx* ctx, int64_t* b_pyr, int64_t* b_top, int64_t
  * scratch of this design is not counted).  One index per kernel. */
 #define FPM_K_PYR 0         /* k_pyr_down     K1 pyrDown                                          */
 #define FPM_K_TOP_WARP 1    /* k_warp         K2 top-layer rotation                               */
-#define FPM_K_TOP_NCC 2     /* k_ncc_tile / k_ncc_map  K3+K4 top-layer CCORR + normalisation      */
-#define FPM_K_TOP_NMS 3     /* k_nms          K5 peak extraction                                  */
+#define FPM_K_TOP_NCC 2     /* k_top_mma / k_ncc_tile / k_ncc_map  K2-K4 top-layer CCORR + norm.  */
+#define FPM_K_TOP_NMS 3     /* k_nms / k_nms_greedy  K5 peak extraction                           */
 #define FPM_K_CAND_INIT 4   /* k_cand_init    candidates from the top-layer peaks                 */
 #define FPM_K_ROI_TABLES 5  /* k_roi_tables   K6a refinement warp tables + tile descriptors       */
 #define FPM_K_ROI_WARP 6    /* k_roi_warp     K6b refinement ROI sampling                         */
@@ -232,7 +232,8 @@ int fpm_search_bytes(const fpm_ctx* ctx, int64_t* b_pyr, int64_t* b_top, int64_t
 #define FPM_K_ROI_EVAL 8    /* k_roi_eval     K8 row fold, CCOEFF, argmax, 3x3, candidate step    */
 #define FPM_K_ROI_SMALL 9   /* k_roi_small    K6-K8 in one kernel for small templates             */
 #define FPM_K_CAND_STEP 10  /* k_cand_step    candidate step after k_roi_small                    */
-#define FPM_K_COUNT 11
+#define FPM_K_TOP_MAP 11    /* k_top_mma mode 1: full maps of the jobs the list path left (fallback) */
+#define FPM_K_COUNT 12
 int fpm_profile_enable(fpm_ctx* ctx, int32_t enable);
 int fpm_profile_reset(fpm_ctx* ctx);
 int fpm_profile_get(const fpm_ctx* ctx, int32_t kernel, double* total_ms, int64_t* launches,

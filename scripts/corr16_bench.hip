@@ -5,6 +5,7 @@
 // row dot products and window-sum partials (k_roi_eval's inputs) and the records k_roi_eval makes of them are
 // identical, then times both.
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off scripts/corr16_bench.hip -o build/corr16_bench
+#define FPM_EXPERIMENTAL   // k_roi_corr16 is compiled only into this harness
 #include "../fastest_image_pattern_matching_amd/csrc/fpm_kernels.hip"
 
 #include <cstdio>

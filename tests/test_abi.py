@@ -73,12 +73,13 @@ def _kernel_symbols():
 
 
 def test_product_library_holds_no_measurement_kernels():
-    """The product library carries only result-path kernels: no fused K6+K7 experiment (FPM_EXPERIMENTAL builds
-    only, scripts/fused_bench.hip), and every ablation template parameter of k_roi_corr / k_roi_small (MODE) and
+    """The product library carries only result-path kernels: no fused K6+K7 experiment and no 16-row-item
+    correlation (FPM_EXPERIMENTAL builds only, scripts/fused_bench.hip / corr16_bench.hip), and every ablation template parameter of k_roi_corr / k_roi_small (MODE) and
     k_roi_warp (ABL) at its product value 0 -- the profiling instantiations exist only in scripts/*.hip."""
     ks = _kernel_symbols()
     assert any(k.startswith("fpm::k_roi_warp3") for k in ks) and any(k.startswith("fpm::k_roi_corr<") for k in ks)
     assert not [k for k in ks if "k_roi_fused" in k]
+    assert not [k for k in ks if "k_roi_corr16" in k]   # measured slower (round 5): scripts/corr16_bench.hip only
     for k in ks:
         args = k[k.index("<") + 1:-1].split(", ") if "<" in k else []
         if k.startswith(("fpm::k_roi_corr<", "fpm::k_roi_small<", "fpm::k_pyr_down<")):
@@ -101,4 +102,5 @@ def test_product_switches_are_result_neutral():
             names |= set(re.findall(r'getenv\("(FPM_[A-Z0-9_]+)"\)', open(os.path.join(csrc, f)).read()))
     assert names <= {"FPM_SCRATCH_MB", "FPM_TOP_FUSED", "FPM_OVERLAP_DEVICE_MIN", "FPM_TAIL_TIMES", "FPM_PYR_WGS",
                      "FPM_PYR_OH", "FPM_PYR2_OH", "FPM_STEP_PROLOGUE", "FPM_STEP_TABLES", "FPM_PYR2", "FPM_WARP3", "FPM_HOST_THREADS", "FPM_POOL_TRACE",
-                     "FPM_HOST_WARM", "FPM_GRID_WARP", "FPM_GRID_CORR", "FPM_GRID_SMALL", "FPM_GRID_TOP", "FPM_CORR16", "FPM_SMALL_NT"}, names
+                     "FPM_HOST_WARM", "FPM_GRID_WARP", "FPM_GRID_CORR", "FPM_GRID_SMALL", "FPM_GRID_TOP", "FPM_SMALL_NT",
+                     "FPM_TOP_MMA", "FPM_TOP_LIST_CAP"}, names

@@ -122,3 +122,20 @@ def test_overlap_adversarial(m):
     s_nan[3] = np.nan                                                # non-monotone scores: the rule compares again
     st = check(m, c, s_nan, 0.5)
     assert st[0] == 1
+
+
+def test_device_filter_twice_in_one_context(gpu_matcher_factory):
+    """k_overlap_pairs writes its pair lists to mapped pinned host memory with plain stores and no fence (the host
+    reads them after hipStreamSynchronize, the rule k_pack follows too): two device filters on different rectangle
+    sets back to back in ONE context, then the first set again -- a stale list from the previous call would change
+    the survivors.  Every call equals the oracle's sequential filter."""
+    mm = gpu_matcher_factory()
+    sets = []
+    for seed, (n, w, h) in enumerate([(420, 62.0, 41.0), (380, 40.0, 70.0)]):
+        rng = np.random.default_rng(700 + seed)
+        c = rects(rng.uniform(0, 450, n), rng.uniform(0, 380, n), w, h, rng.uniform(-180, 180, n))
+        sets.append((c, np.sort(rng.uniform(0.5, 1.0, n))[::-1].copy()))
+    for c, s in sets + sets[:1]:
+        exp = oracle.filter_rotated_rect(c, s, 0.3)
+        dev, dst = mm.overlap_filter(c, s, 0.3, device=True)
+        assert dst[0] == 1 and dev == exp

@@ -186,13 +186,12 @@ def test_src7_top_layer_forms(gpu_matcher_factory, templates, monkeypatch, top_f
                                       "FPM_GRID_CORR": "11"},
                                   {"FPM_GRID_TOP": "1000", "FPM_GRID_SMALL": "768", "FPM_GRID_WARP": "1536"},
                                   {"FPM_GRID_SMALL": "0", "FPM_GRID_WARP": "0"},
-                                  {"FPM_CORR16": "1"}, {"FPM_CORR16": "1", "FPM_GRID_CORR": "13"},
+                                  {"FPM_GRID_CORR": "13"},
                                   {"FPM_SMALL_NT": "256"}, {"FPM_SMALL_NT": "128"}, {"FPM_SMALL_NT": "512"},
                                   {"FPM_SMALL_NT": "128", "FPM_GRID_SMALL": "5"}])
 def test_src7_grid_caps(gpu_matcher_factory, templates, monkeypatch, caps):
     """The workgroup caps of the persistent forms (FPM_GRID_TOP / _SMALL / _WARP / _CORR; read when a fresh context
-    records its search; {} = the defaults, "0" = uncapped grids; FPM_CORR16 = the 16-row-item correlation;
-    FPM_SMALL_NT=256 / 128 / 512 = four- / two- / eight-wave workgroups for every small-template layer where they
+    records its search; {} = the defaults, "0" = uncapped grids; FPM_SMALL_NT=256 / 128 / 512 = four- / two- / eight-wave workgroups for every small-template layer where they
     apply; by default eight-wave ones for batches of at most two sources, two-wave ones for layers with more ROIs than
     the four-wave form holds at once): with tiny
     caps every workgroup of the fused top layer, the small-template refinement, the
@@ -209,6 +208,33 @@ def test_src7_grid_caps(gpu_matcher_factory, templates, monkeypatch, caps):
     o = oracle.OracleMatcher().set(max_pos=3, tolerance_angle=180.0, score=0.7)
     o.learnPattern(t)
     assert got == [o.match(s) for s in srcs]
+
+
+@pytest.mark.parametrize("nt", ["128", "256", "512"])
+@pytest.mark.parametrize("shape", ["wide", "tall"])
+def test_small_forms_wide_tall_templates(gpu_matcher_factory, templates, monkeypatch, nt, shape):
+    """The two- / four- / eight-wave small-template workgroups (FPM_SMALL_NT, forced wherever they apply) and a tight
+    correlation grid cap on a wide template (Dst6, 848 x 446) and a tall one (its transpose): every layer's footprint
+    region, table and band layout of k_roi_small on shapes other than Src7's; two sources at +-180 equal the oracle."""
+    monkeypatch.setenv("FPM_SMALL_NT", nt)
+    monkeypatch.setenv("FPM_GRID_CORR", "13")
+    t = np.ascontiguousarray(templates["Dst6"] if shape == "wide" else templates["Dst6"].T)
+    h, w = (1300, 1700) if shape == "wide" else (1700, 1300)
+    srcs = []
+    for i in range(2):
+        s = synth.noise(w, h, 128, 12, 77 + i)
+        synth.paste_rotated(s, t, w * 0.45, h * 0.5, 35.0 - 70.0 * i)
+        srcs.append(s)
+    kw = dict(max_pos=2, tolerance_angle=180.0, score=0.7)
+    m = gpu_matcher_factory(**kw)
+    assert m.learnPattern(t)
+    m.stage(srcs)
+    got = [[r.as_tuple() for r in rr] for rr in m.match_staged()]
+    o = oracle.OracleMatcher().set(**kw)
+    o.learnPattern(t)
+    exp = [o.match(s) for s in srcs]
+    assert got == exp
+    assert all(len(r) >= 1 for r in exp)
 
 
 def test_top_fused_lds_threshold(gpu_matcher_factory, templates, monkeypatch):
