@@ -380,6 +380,7 @@ int plan_top_mma(fpm_ctx* ctx, Plan& P, const TmplLevel& tt) {
     A = TopMmaArgs{};
     A.tw = tt.w; A.th = tt.h; A.area = tt.w * tt.h;
     top_mma_layout(A, sw, max_rows);
+    top_mma_source(A, ctx->src[L].w, ctx->src[L].h);
     if (top_mma_lds(A) > 160 * 1024 - 1024) return FPM_OK;
     uint32_t tsum = 0;
     for (uint8_t v : tt.px) tsum += v;
@@ -401,7 +402,7 @@ int plan_top_mma(fpm_ctx* ctx, Plan& P, const TmplLevel& tt) {
     HIP_TRY(hipMemcpyAsync(P.d_tmu.as<char>(ubytes), bf.data(), bf.size(), hipMemcpyHostToDevice, ctx->stream));
     // candidate lists: s_BlockMax maps share d_ncand with k_nms_blocks' fallback lists (kNmsCandCap per map); plain
     // maps need no more than the greedy form takes
-    P.tcand_cap = P.by_block ? kNmsCandCap : 4096;
+    P.tcand_cap = P.by_block ? kNmsCandCap : 512;
     // FPM_TOP_LIST_CAP=n (tests): lists of n entries, so every map with more candidates takes the fallback path
     if (const char* lc = getenv("FPM_TOP_LIST_CAP"))
         if (atoi(lc) > 0) P.tcand_cap = std::min(P.tcand_cap, atoi(lc));

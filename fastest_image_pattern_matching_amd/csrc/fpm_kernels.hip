@@ -1637,16 +1637,17 @@ __global__ __launch_bounds__(256) void k_nms_greedy(NmsArgs a, CandInitArgs ci, 
     g.init(mw, mh, tw, th, a.mfc);
     const int K = a.cand_cnt[blockIdx.x];
     const int cxn = (mw + tw - 1) / tw, cyn = (mh + th - 1) / th, ncell = cxn * cyn;
+    const int GC = a.greedy_cap > 0 ? a.greedy_cap : kGreedyMax;   // sort capacity of this launch's LDS (power of 2)
     if (!(mw > 0 && mh > 0 && (plain || (g.ncol > 0 && g.nrow > 0)) && rw > 0 && rh > 0 && a.thr > -1.0 && K >= 0 &&
-          K <= a.cand_cap && K <= kGreedyMax && ncell <= a.lds_blocks)) {
+          K <= a.cand_cap && K <= GC && ncell <= a.lds_blocks)) {
         if (a.reset_untaken && tid == 0 && K >= 0) a.cand_cnt[blockIdx.x] = 0;
         return;
     }
     int P = 64;
     while (P < K) P <<= 1;
-    float* sv = (float*)nms_lds;                       // [kGreedyMax] values
-    uint64_t* sk = (uint64_t*)(sv + kGreedyMax);       // [kGreedyMax] (block << 32) | (y << 16) | x
-    uint8_t* ccnt = (uint8_t*)(sk + kGreedyMax);       // [cells] taken rectangles per cell
+    uint64_t* sk = (uint64_t*)nms_lds;                 // [GC] (block << 32) | (y << 16) | x
+    float* sv = (float*)(sk + GC);                     // [GC] values
+    uint8_t* ccnt = (uint8_t*)(sv + GC);               // [cells] taken rectangles per cell
     uint8_t* cids = ccnt + a.lds_blocks;               // [cells][kCellIds]
     int* accx = (int*)(cids + (size_t)a.lds_blocks * kCellIds + 16 - ((a.lds_blocks * (1 + kCellIds)) & 15));
     int* accy = accx + 256;
@@ -1749,8 +1750,8 @@ __global__ __launch_bounds__(256) void k_nms_greedy(NmsArgs a, CandInitArgs ci, 
     }
 }
 
-static size_t nms_greedy_lds(int cells) {
-    return (size_t)12 * kGreedyMax + (size_t)cells * (1 + kCellIds) + 16 + 8 * 256;
+static size_t nms_greedy_lds(int cells, int gcap = kGreedyMax) {
+    return (size_t)12 * gcap + (size_t)cells * (1 + kCellIds) + 16 + 8 * 256;
 }
 
 // LDS bytes of k_nms_fast for a block capacity, peak capacity and candidate capacity
@@ -4891,6 +4892,9 @@ void launch_cand_step(const RoiArgs& a, int max_items, hipStream_t st) {
 // carry at most 512 of rounding each (E = 1024), and thrK includes a 1e-5 relative margin over the f64 evaluation's
 // and the f32 score rounding's relative errors (<= 1e-6), so no output with (double)score >= thr is ever rejected.
 constexpr int TM_BH = 16;            // output rows per band (one MFMA M block)
+#ifndef TOPMMA_ABL
+#define TOPMMA_ABL 0
+#endif
 
 bool top_mma_fits(int tw, int th) { return tw >= 1 && th >= 1 && ((tw <= 17 && th <= 32) || (tw <= 49 && th <= 16)); }
 
@@ -4909,8 +4913,16 @@ void top_mma_layout(TopMmaArgs& a, int sw, int max_rows) {
     a.o_colt = a.o_h2 + 4 * a.rr * a.hp;
     a.o_rowt = a.o_colt + 8 * a.ct;
     a.o_bf = (a.o_rowt + 8 * a.rt + 15) & ~15;
+    a.o_src = a.o_bf + 1024 * a.nq;
 }
-size_t top_mma_lds(const TopMmaArgs& a) { return (size_t)a.o_bf + 1024 * (size_t)a.nq; }
+size_t top_mma_lds(const TopMmaArgs& a) { return (size_t)a.o_src + (a.ssp > 0 ? (size_t)a.ssp * (a.ssh + 4) : 0); }
+// the source level staged into LDS (framed) when it takes at most kTopSrcLds bytes
+constexpr int kTopSrcLds = 20 * 1024;
+void top_mma_source(TopMmaArgs& a, int sw, int sh) {
+    const int ssp = (sw + 4 + 3) & ~3;
+    a.ssp = (size_t)ssp * (sh + 4) <= (size_t)kTopSrcLds ? ssp : 0;
+    a.ssh = sh;
+}
 
 __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t tm_lds[];
@@ -4938,6 +4950,8 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
     const fpm_v4i zero4 = {0, 0, 0, 0};
     const uint32_t area = (uint32_t)a.area;
     const float areaf = (float)a.area, tsumf = (float)a.tsum;
+    uint8_t* const sl = tm_lds + a.o_src;                  // the staged source level (a.ssp > 0)
+    const uint8_t* staged = nullptr;
     for (int u = blockIdx.x; u < a.nunits; u += gridDim.x) {
         const TopUnit U = a.units[u];
         if (a.mode == 1 && a.cand_cnt[U.job] < 0) continue;   // (uniform) taken from its list: no map needed
@@ -4950,6 +4964,21 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
         const uint8_t* src = W.src;
         const int sw = W.sw, sh = W.sh, sp = W.sp, border = W.border;
         __syncthreads();   // the previous unit is done with the LDS
+        if (a.ssp > 0 && src != staged) {   // (uniform) the source level, framed by 2 pixels of the border value
+            const int ssp = a.ssp, fw = sw + 4, fh = sh + 4;
+            for (int i = tid; i < fh * (ssp >> 2); i += 256) {
+                const int r = i / (ssp >> 2), c4 = (i - r * (ssp >> 2)) * 4;
+                uint32_t w = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const int x = c4 + b - 2, y = r - 2;
+                    const int v = (x >= 0 && x < sw && y >= 0 && y < sh) ? src[(size_t)y * sp + x] : border;
+                    w |= (uint32_t)v << (8 * b);
+                }
+                *(uint32_t*)(sl + r * ssp + c4) = c4 < fw ? w : 0u;
+            }
+            staged = src;
+        }
         for (int i = tid; i < ncols; i += 256) {
             const int x = U.x0 + i;
             cad[i] = rint_i(W.M[0] * x * kAbScale);
@@ -4965,18 +4994,36 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
             const int rs = yb == U.y0 ? yb : yb + th - 1;
             const int re = min(yb + TM_BH + th - 1, U.y0 + nrows);
             __syncthreads();   // tables ready / the previous band's tiles are done with the ring rows replaced now
-            // ---- the band's new canvas rows (cv::warpAffine, k_warp's integers), flipped to i8
-            for (int it = tid; it < (re - rs) * ncw; it += 256) {
+            // ---- the band's new canvas rows (cv::warpAffine, k_warp's integers), flipped to i8; four pixels per item,
+            // their taps issued together.  Source in LDS (a.ssp > 0): the level with a 2-pixel frame of the border value,
+            // tap coordinates clamped into the frame -- a tap outside the image then reads the border value exactly as
+            // warp_tap's per-tap rule does, and a fully outside one interpolates four border values to the border value
+            for (int it = tid; it < (TOPMMA_ABL == 1 ? 0 : (re - rs) * ncw); it += 256) {
                 const int r = it / ncw, k = it - r * ncw;
                 const int y = rs + r, ry = y - U.y0;
                 const int X0 = rxy[ry], Y0 = rxy[a.rt + ry];
+                const int4 ad4 = *(const int4*)(cad + 4 * k), bd4 = *(const int4*)(cad + a.ct + 4 * k);
+                const int adv[4] = {ad4.x, ad4.y, ad4.z, ad4.w}, bdv[4] = {bd4.x, bd4.y, bd4.z, bd4.w};
                 uint32_t word = 0;
-#pragma unroll 1
-                for (int b = 0; b < 4; ++b) {
-                    const int x = 4 * k + b;
-                    if (x < ncols) {
-                        const int X = (X0 + cad[x]) >> (kAbBits - kInterBits);
-                        const int Y = (Y0 + cad[a.ct + x]) >> (kAbBits - kInterBits);
+                if (a.ssp > 0) {
+                    const int ssp = a.ssp;
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        const int X = X0 + adv[b], Y = Y0 + bdv[b];
+                        const int fx = (X >> (kAbBits - kInterBits)) & (kInterTab - 1);
+                        const int fy = (Y >> (kAbBits - kInterBits)) & (kInterTab - 1);
+                        const int sx = min(max(X >> kAbBits, -2), sw), sy = min(max(Y >> kAbBits, -2), sh);
+                        const uint8_t* p = sl + (sy + 2) * ssp + (sx + 2);
+                        const int v0 = p[0], v1 = p[1], v2 = p[ssp], v3 = p[ssp + 1];
+                        const int h0 = v0 * kInterTab + fx * (v1 - v0), h1 = v2 * kInterTab + fx * (v3 - v2);
+                        const int v = (h0 * kInterTab + fy * (h1 - h0) + 512) >> 10;
+                        word |= (uint32_t)v << (8 * b);
+                    }
+                } else {
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        const int X = (X0 + adv[b]) >> (kAbBits - kInterBits);
+                        const int Y = (Y0 + bdv[b]) >> (kAbBits - kInterBits);
                         word |= (uint32_t)warp_tap(src, sw, sh, sp, X, Y, border) << (8 * b);
                     }
                 }
@@ -4984,7 +5031,7 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
             }
             __syncthreads();
             // ---- H2: per new row, sum of I^2 over [x, x + tw) for the strip's output columns, 8 per item (sliding)
-            for (int it = tid; it < (re - rs) * nruns; it += 256) {
+            for (int it = tid; it < (TOPMMA_ABL == 2 ? 0 : (re - rs) * nruns); it += 256) {
                 const int r = it / nruns, k = it - r * nruns;
                 const int y = rs + r;
                 const uint8_t* row = ring + (size_t)(y & mask) * cp + 8 * k;
@@ -5017,7 +5064,7 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
                 const int co = a.R == 2 ? 16 * (lg & 1) : 16 * lg;
                 const int rstep = a.R == 2 ? 2 : 1;
                 int ro = a.R == 2 ? (lg >> 1) : 0;
-                for (int q = 0; q < a.nq; ++q, ro += rstep) {
+                for (int q = 0; q < (TOPMMA_ABL == 3 ? 0 : a.nq); ++q, ro += rstep) {
                     const fpm_v4i av = *(const fpm_v4i*)(ring + (size_t)((yb + ln + ro) & mask) * cp + 16 * nb + co);
                     const fpm_v4i bv = bl[q * 64 + lane];
                     acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv, acc, 0, 0, 0);
@@ -5025,6 +5072,10 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
                 }
                 // D: column ln = output column 16 nb + ln, rows 4 lg + i = output rows yb + 4 lg + i
                 const int xo = 16 * nb + ln, yo0 = yb + 4 * lg;
+                if (TOPMMA_ABL == 4) {
+                    if (acc[0] == 0x12345 && acc1[1] == 0x777) a.cand_cnt[0] = acc[2] + acc1[3];
+                    continue;
+                }
                 const uint32_t* hc = h2 + xo;
                 uint32_t hs = 0;
                 for (int k = 0; k < th; ++k) hs += hc[(size_t)((yo0 + k) & mask) * hp];
@@ -5044,11 +5095,13 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
                     ccv[i] = (uint32_t)acc[i] + 128u * (wsv[i] + a.tsum) - 16384u * area;
                     bool pass = yo0 + i < U.y1 && xo < swu;
                     if (pass && a.mode == 0 && a.prefilter) {
+                        // df = area sum I^2 - (sum I)^2 exactly (mod 2^32: its value is < 2^32 for area <= 257); 0 is a
+                        // flat window, whose score is 0 (CCOEFF's t = 0 branch)
+                        const uint32_t dfi = area * wq[i] - wsv[i] * wsv[i];
                         const float wsf = (float)wsv[i];
                         const float nf = __builtin_fmaf(areaf, (float)ccv[i], -(wsf * tsumf));
-                        const float df = __builtin_fmaf(areaf, (float)wq[i], -(wsf * wsf));
                         const float nfp = nf + a.E;
-                        pass = nfp > 0.f && nfp * nfp >= a.thrK * (df - a.E);
+                        pass = dfi != 0u && nfp > 0.f && nfp * nfp >= a.thrK * (float)dfi;
                     }
                     pm |= pass ? 1u << i : 0u;
                 }
@@ -5112,7 +5165,12 @@ void launch_top_greedy(const NmsArgs& a0, int njobs, int max_cells, hipStream_t 
     CandInitArgs cz{};
     const bool fuse = ci && !a.by_block && a.cap <= kNmsInitCap;
     const int mode = !fuse ? 0 : (ci->refine == 0 ? 1 : (ci->refine == 2 ? 3 : 2));
-    const size_t lds = nms_greedy_lds(max_cells);
+    // sort capacity: the lists' capacity (a power of 2, at most kGreedyMax), so short lists need little LDS and many
+    // workgroups fit a CU (most of them end after reading their count)
+    int gc = 64;
+    while (gc < a.cand_cap && gc < kGreedyMax) gc <<= 1;
+    a.greedy_cap = gc;
+    const size_t lds = nms_greedy_lds(max_cells, gc);
     ensure_lds_attr((const void*)k_nms_greedy, lds);
     hipLaunchKernelGGL(k_nms_greedy, dim3(njobs), dim3(256), lds, st, a, fuse ? *ci : cz, mode);
 }

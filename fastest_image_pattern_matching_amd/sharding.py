@@ -188,6 +188,42 @@ def gather_candidates(local: np.ndarray, group=None, device=None) -> np.ndarray:
     return np.concatenate(out) if out else np.zeros(0, CANDIDATE_DTYPE)
 
 
+def gather_candidates_batch(local: Sequence[np.ndarray], group=None, device=None) -> List[np.ndarray]:
+    """gather_candidates for a batch of sources searched by angle shard on every rank (the same sources on every
+    rank, each rank its angle block): per source, the rank-order concatenation of every rank's records -- that
+    source's push order (TemplateMatcher.cpp:157-211).  Two collectives for the whole batch: the [sources] record
+    counts, then every source's records back to back as bytes, padded to the largest total."""
+    import torch
+    import torch.distributed as dist
+
+    from .matcher import CANDIDATE_DTYPE
+
+    recs = [np.ascontiguousarray(x, CANDIDATE_DTYPE) for x in local]
+    world = dist.get_world_size(group)
+    n_src = len(recs)
+    cnt = torch.tensor([len(x) for x in recs], dtype=torch.int64)
+    if device is not None:
+        cnt = cnt.to(device)
+    counts = [torch.empty_like(cnt) for _ in range(world)]
+    dist.all_gather(counts, cnt, group=group)
+    counts = np.stack([c.cpu().numpy() for c in counts])            # [world, sources]
+    item = CANDIDATE_DTYPE.itemsize
+    width = max(int(counts.sum(1).max()), 1) * item
+    buf = np.zeros(width, np.uint8)
+    raw = np.concatenate([x.view(np.uint8) for x in recs]) if n_src else np.zeros(0, np.uint8)
+    buf[:raw.size] = raw
+    mine = torch.from_numpy(buf)
+    if device is not None:
+        mine = mine.to(device)
+    parts = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(parts, mine, group=group)
+    per_rank = []
+    for k in range(world):
+        blob = parts[k].cpu().numpy()[:int(counts[k].sum()) * item].view(CANDIDATE_DTYPE)
+        per_rank.append(np.split(blob, np.cumsum(counts[k])[:-1]) if n_src else [])
+    return [np.concatenate([per_rank[k][s] for k in range(world)]) for s in range(n_src)]
+
+
 def merge_gathered(params, tmpl_w: int, tmpl_h: int, cands: np.ndarray):
     """fpm_merge_candidates over gathered records (host only): the search's final s_SingleTargetMatch list."""
     from .matcher import merge_candidates

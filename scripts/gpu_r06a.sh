@@ -17,6 +17,6 @@ for f in ("bench_c3_$T.json", "bench_c3_split_$T.json"):
     k = d["kernels"]
     print(f, d["value"], d["ms_per_step"], {n: (round(v["ms_total"] / max(v["launches"], 1) * 1000, 1), v["launches"]) for n, v in k.items()})
 PY
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$T -o kp -- python3 bench.py --workload config3 --kernel-pass-only --steps 2 --warmup 1 --cpu-budget 0 > gpurun_out/kp_$T.log 2>&1 || { tail -20 gpurun_out/kp_$T.log; exit 1; }
-find gpurun_out/prof_$T -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} gpurun_out/kernel_stats_$T.csv
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_$T -o kp --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --workload config3 --kernel-pass-only --steps 2 --warmup 1 --cpu-budget 0 > $GRAFT_REPO_ROOT/gpurun_out/kp_$T.log 2>&1 || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/kp_$T.log; exit 1; }
+cd $GRAFT_REPO_ROOT && find gpurun_out/prof_$T -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} gpurun_out/kernel_stats_$T.csv
 head -20 gpurun_out/kernel_stats_$T.csv | cut -c1-160

@@ -167,3 +167,52 @@ def test_merge_large_fixture_threads(threads):
                          env=env, capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     assert out.stdout.strip().endswith("SAME"), out.stdout + out.stderr
+
+
+def _batch_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        srcs, t = synth.src5_set()
+        prm = dict(max_pos=1, tolerance_angle=180.0, subpixel=1)
+        local, full_res = [], []
+        for s in srcs:
+            o = oracle.OracleMatcher().set(**prm)
+            assert o.learnPattern(t)
+            full_res.append(o.match(s))
+            c = o.candidates()
+            a0, a1 = sharding.angle_block(o.stats()[0], rank, world)
+            local.append(c[(c["angle_index"] >= a0) & (c["angle_index"] < a1)])
+        full = sharding.gather_candidates_batch(local)
+        merged = [_tuples(merge_candidates(o.params, t.shape[1], t.shape[0], c)) for c in full]
+        q.put((rank, merged == full_res, [len(c) for c in full], [len(c) for c in local]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_candidates_batch_config4_gloo():
+    """bench.py --workload config4's per-step exchange (world 2, gloo): every rank holds its angle block's candidate
+    records of each of the 8 Src5 images (oracle records); one batched all_gather (counts, then all records) gives
+    every image's rank-order concatenation, whose merge equals the oracle's unsharded search of that image."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    procs = [ctx.Process(target=_batch_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok, n_full, n_local in got:
+        assert ok, rank
+        assert len(n_full) == 8 and all(n > 0 for n in n_full)
+    # the ranks' blocks partition each image's records
+    by_rank = {r: nl for r, _, _, nl in got}
+    assert [a + b for a, b in zip(by_rank[0], by_rank[1])] == got[0][2]

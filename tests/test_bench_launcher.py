@@ -80,3 +80,14 @@ def test_search_macs_follow_survey_formula():
     mt, mr = b.search_macs(Ctx(), src_wh, tmpl_wh, S)
     assert mt == S * sum(w * h for w, h in maps) * tm[L][0] * tm[L][1]
     assert mr == [n * n3 * 49 * w * h for n, (w, h) in zip(live, layers)]
+
+
+def test_config4_shards_angles_over_ranks():
+    """--workload config4 (BASELINE.json configs[4]): the 8-image Src5 set searched on every rank, each rank its block
+    of the top-layer angle list (angle shard rank / world)."""
+    out = subprocess.run([sys.executable, BENCH, "--workload", "config4", "--gpus", "2", "--dry-run"],
+                         capture_output=True, text=True, timeout=240, env=_env())
+    assert out.returncode == 0, out.stderr
+    ranks = sorted((r["rank"], r["world"], r["workload"], tuple(r["angle_shard"]))
+                   for r in (json.loads(m) for m in re.findall(r"\{[^{}]*\}", out.stdout)))
+    assert ranks == [(0, 2, "config4", (0, 2)), (1, 2, "config4", (1, 2))]
