@@ -380,7 +380,6 @@ int plan_top_mma(fpm_ctx* ctx, Plan& P, const TmplLevel& tt) {
     A = TopMmaArgs{};
     A.tw = tt.w; A.th = tt.h; A.area = tt.w * tt.h;
     top_mma_layout(A, sw, max_rows);
-    top_mma_source(A, ctx->src[L].w, ctx->src[L].h);
     if (top_mma_lds(A) > 160 * 1024 - 1024) return FPM_OK;
     uint32_t tsum = 0;
     for (uint8_t v : tt.px) tsum += v;

@@ -235,8 +235,8 @@ struct TopMmaArgs {
     int32_t rr;              // ring rows (power of two >= 16 + th - 1): canvas bytes and H2 rows
     int32_t hp;              // H2 ring row pitch (u32)
     int32_t ct, rt;          // column / row table capacity (entries)
-    int32_t o_h2, o_colt, o_rowt, o_bf, o_src;   // dynamic LDS offsets (bytes)
-    int32_t ssp, ssh;        // staged source level: LDS row pitch (0 = taps from global memory), level height
+    int32_t o_h2, o_colt, o_rowt, o_bf, o_ft;   // dynamic LDS offsets (bytes)
+    int32_t nqm;             // B slots staged in LDS (the kernel form's unrolled slot count; zero past nq)
     int32_t mode;            // 0: candidate lists, 1: full maps of the jobs with cand_cnt >= 0 (fallback)
     int32_t prefilter;       // 1: f32 bound before the exact f64 score (area <= 258, thr > 0)
     float thrK, E;           // prefilter: (thr (1 - 1e-5))^2 * norm^2 * area, absolute slack of the f32 terms
@@ -249,7 +249,6 @@ struct TopMmaArgs {
 size_t top_mma_lds(const TopMmaArgs& a);
 // fills the layout fields of `a` (sw, cp, rr, hp, ct, rt, o_*) for a strip width and the largest unit height
 void top_mma_layout(TopMmaArgs& a, int sw, int max_rows);
-void top_mma_source(TopMmaArgs& a, int src_w, int src_h);   // after top_mma_layout: stage the level in LDS if small
 bool top_mma_fits(int tw, int th);   // template shapes the kernel takes (R = 2 up to 17 wide, R = 1 up to 49)
 void launch_top_mma(const TopMmaArgs& a, hipStream_t st);
 // k_nms_greedy over k_top_mma's lists (a.cand_val set): plain getNextMaxLoc key (by_block 0) or s_BlockMax key; with ci

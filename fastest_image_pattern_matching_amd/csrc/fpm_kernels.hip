@@ -4892,11 +4892,18 @@ void launch_cand_step(const RoiArgs& a, int max_items, hipStream_t st) {
 // carry at most 512 of rounding each (E = 1024), and thrK includes a 1e-5 relative margin over the f64 evaluation's
 // and the f32 score rounding's relative errors (<= 1e-6), so no output with (double)score >= thr is ever rejected.
 constexpr int TM_BH = 16;            // output rows per band (one MFMA M block)
+constexpr int TM_FTP = 48;           // sampling footprint buffer: row pitch (bytes) and size per wave
+constexpr int TM_FTB = 48 * 40;      // (a 16 x 32 tile of a rotation covers at most 37 x 37 source pixels + taps)
 #ifndef TOPMMA_ABL
 #define TOPMMA_ABL 0
 #endif
 
 bool top_mma_fits(int tw, int th) { return tw >= 1 && th >= 1 && ((tw <= 17 && th <= 32) || (tw <= 49 && th <= 16)); }
+
+// the loop bounds every lane runs unrolled (NQM MFMA slots, THM H2 rows, TWW template words; a slot, row or word
+// beyond the template is masked, not branched around, so all of a loop's LDS reads are issued before the first use):
+// <8, 16, 5> for templates up to 17 x 16 (BASELINE configs[2] and [3]), <16, 32, 13> for every other shape
+static bool top_mma_small(const TopMmaArgs& a) { return a.R == 2 && a.th <= 16; }
 
 void top_mma_layout(TopMmaArgs& a, int sw, int max_rows) {
     a.sw = sw;
@@ -4913,17 +4920,14 @@ void top_mma_layout(TopMmaArgs& a, int sw, int max_rows) {
     a.o_colt = a.o_h2 + 4 * a.rr * a.hp;
     a.o_rowt = a.o_colt + 8 * a.ct;
     a.o_bf = (a.o_rowt + 8 * a.rt + 15) & ~15;
-    a.o_src = a.o_bf + 1024 * a.nq;
+    a.nqm = top_mma_small(a) ? 8 : 16;               // B slots in LDS (zero beyond nq)
+    a.o_ft = a.o_bf + 1024 * a.nqm;                  // the 4 waves' sampling footprint buffers
 }
-size_t top_mma_lds(const TopMmaArgs& a) { return (size_t)a.o_src + (a.ssp > 0 ? (size_t)a.ssp * (a.ssh + 4) : 0); }
-// the source level staged into LDS (framed) when it takes at most kTopSrcLds bytes
-constexpr int kTopSrcLds = 20 * 1024;
-void top_mma_source(TopMmaArgs& a, int sw, int sh) {
-    const int ssp = (sw + 4 + 3) & ~3;
-    a.ssp = (size_t)ssp * (sh + 4) <= (size_t)kTopSrcLds ? ssp : 0;
-    a.ssh = sh;
-}
+size_t top_mma_lds(const TopMmaArgs& a) { return (size_t)a.o_ft + 4 * TM_FTB; }
 
+// TH > 0: the template height as a compile-time constant (two-row slots, NQM = (TH + 1) / 2, every slot and H2 row
+// exact: no masks); TH == 0: any height up to the form's bounds, rows past th masked
+template <int NQM, int THM, int TWW, int TH = 0>
 __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t tm_lds[];
     uint8_t* const ring = tm_lds;
@@ -4932,11 +4936,13 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
     int32_t* const rxy = (int32_t*)(tm_lds + a.o_rowt);   // X0 [rt], Y0 [rt] of its canvas rows
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int ln = lane & 15, lg = lane >> 4;
-    const int tw = a.tw, th = a.th, mask = a.rr - 1, cp = a.cp, hp = a.hp;
-    // the B fragments (correlation) staged once into LDS; the band of ones (window sum of I') in registers: byte i of
-    // lane (n, g) is k = 16 g + i
+    const int tw = a.tw, th = TH > 0 ? TH : a.th, mask = a.rr - 1, cp = a.cp, hp = a.hp;
+    // the B fragments (correlation) staged once into LDS, zero past slot nq; the band of ones (window sum of I') in
+    // registers: byte i of lane (n, g) is k = 16 g + i
     fpm_v4i* const bl = (fpm_v4i*)(tm_lds + a.o_bf);
-    for (int i = tid; i < a.nq * 64; i += 256) bl[i] = *(const fpm_v4i*)(a.bfrag + (size_t)i * 16);
+    uint8_t* const ftb = tm_lds + a.o_ft;
+    for (int i = tid; i < NQM * 64; i += 256)
+        bl[i] = i < a.nq * 64 ? *(const fpm_v4i*)(a.bfrag + (size_t)i * 16) : fpm_v4i{0, 0, 0, 0};
     fpm_v4i ones;
     {
         const int c0 = a.R == 2 ? 16 * (lg & 1) : 16 * lg;
@@ -4947,11 +4953,17 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
         }
         ones = fpm_v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
     }
+    // byte masks of the template width for the H2 window's words
+    uint32_t tmask[TWW];
+#pragma unroll
+    for (int k = 0; k < TWW; ++k) {
+        const int n = tw - 4 * k;
+        tmask[k] = n >= 4 ? 0xffffffffu : n <= 0 ? 0u : (0xffffffffu >> (8 * (4 - n)));
+    }
     const fpm_v4i zero4 = {0, 0, 0, 0};
     const uint32_t area = (uint32_t)a.area;
     const float areaf = (float)a.area, tsumf = (float)a.tsum;
-    uint8_t* const sl = tm_lds + a.o_src;                  // the staged source level (a.ssp > 0)
-    const uint8_t* staged = nullptr;
+    const int co = a.R == 2 ? 16 * (lg & 1) : 16 * lg;   // the lane's A / B column offset in a slot
     for (int u = blockIdx.x; u < a.nunits; u += gridDim.x) {
         const TopUnit U = a.units[u];
         if (a.mode == 1 && a.cand_cnt[U.job] < 0) continue;   // (uniform) taken from its list: no map needed
@@ -4964,21 +4976,6 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
         const uint8_t* src = W.src;
         const int sw = W.sw, sh = W.sh, sp = W.sp, border = W.border;
         __syncthreads();   // the previous unit is done with the LDS
-        if (a.ssp > 0 && src != staged) {   // (uniform) the source level, framed by 2 pixels of the border value
-            const int ssp = a.ssp, fw = sw + 4, fh = sh + 4;
-            for (int i = tid; i < fh * (ssp >> 2); i += 256) {
-                const int r = i / (ssp >> 2), c4 = (i - r * (ssp >> 2)) * 4;
-                uint32_t w = 0;
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const int x = c4 + b - 2, y = r - 2;
-                    const int v = (x >= 0 && x < sw && y >= 0 && y < sh) ? src[(size_t)y * sp + x] : border;
-                    w |= (uint32_t)v << (8 * b);
-                }
-                *(uint32_t*)(sl + r * ssp + c4) = c4 < fw ? w : 0u;
-            }
-            staged = src;
-        }
         for (int i = tid; i < ncols; i += 256) {
             const int x = U.x0 + i;
             cad[i] = rint_i(W.M[0] * x * kAbScale);
@@ -4994,40 +4991,111 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
             const int rs = yb == U.y0 ? yb : yb + th - 1;
             const int re = min(yb + TM_BH + th - 1, U.y0 + nrows);
             __syncthreads();   // tables ready / the previous band's tiles are done with the ring rows replaced now
-            // ---- the band's new canvas rows (cv::warpAffine, k_warp's integers), flipped to i8; four pixels per item,
-            // their taps issued together.  Source in LDS (a.ssp > 0): the level with a 2-pixel frame of the border value,
-            // tap coordinates clamped into the frame -- a tap outside the image then reads the border value exactly as
-            // warp_tap's per-tap rule does, and a fully outside one interpolates four border values to the border value
-            for (int it = tid; it < (TOPMMA_ABL == 1 ? 0 : (re - rs) * ncw); it += 256) {
-                const int r = it / ncw, k = it - r * ncw;
-                const int y = rs + r, ry = y - U.y0;
-                const int X0 = rxy[ry], Y0 = rxy[a.rt + ry];
-                const int4 ad4 = *(const int4*)(cad + 4 * k), bd4 = *(const int4*)(cad + a.ct + 4 * k);
-                const int adv[4] = {ad4.x, ad4.y, ad4.z, ad4.w}, bdv[4] = {bd4.x, bd4.y, bd4.z, bd4.w};
-                uint32_t word = 0;
-                if (a.ssp > 0) {
-                    const int ssp = a.ssp;
-#pragma unroll
-                    for (int b = 0; b < 4; ++b) {
-                        const int X = X0 + adv[b], Y = Y0 + bdv[b];
-                        const int fx = (X >> (kAbBits - kInterBits)) & (kInterTab - 1);
-                        const int fy = (Y >> (kAbBits - kInterBits)) & (kInterTab - 1);
-                        const int sx = min(max(X >> kAbBits, -2), sw), sy = min(max(Y >> kAbBits, -2), sh);
-                        const uint8_t* p = sl + (sy + 2) * ssp + (sx + 2);
-                        const int v0 = p[0], v1 = p[1], v2 = p[ssp], v3 = p[ssp + 1];
-                        const int h0 = v0 * kInterTab + fx * (v1 - v0), h1 = v2 * kInterTab + fx * (v3 - v2);
-                        const int v = (h0 * kInterTab + fy * (h1 - h0) + 512) >> 10;
-                        word |= (uint32_t)v << (8 * b);
+            // ---- the band's new canvas rows (cv::warpAffine with k_warp's integers), flipped to i8.  One wave per
+            // sampling tile of 16 rows x 32 columns: the tile's source footprint (the box of its clamped tap coordinates:
+            // the fixed-point coordinates are monotone in x and y, so the corners bound it; coordinates clamped into
+            // [-2, w] x [-2, h], where every tap outside the level reads the border value) is staged from the level into
+            // the wave's LDS buffer, the border value filling what lies outside, and the 4 taps of each pixel are read
+            // from there (a clamped tap outside the image reads the border value exactly as warp_tap's per-tap rule
+            // does, and four border values interpolate to the border value)
+            {
+                const int nrw = re - rs, ntc = (ncols + 31) >> 5, ntr = (nrw + 15) >> 4;
+                uint8_t* const ft = ftb + wv * TM_FTB;
+                for (int t = wv; t < (TOPMMA_ABL == 1 ? 0 : ntr * ntc); t += 4) {
+                    const int tr = t / ntc, tc = t - tr * ntc;
+                    const int ty0 = rs + 16 * tr, ty1 = min(ty0 + 16, re), tx0 = 32 * tc, tx1 = min(tx0 + 32, ncols);
+                    const int r0 = ty0 - U.y0, r1 = ty1 - 1 - U.y0;
+                    const int Xa = rxy[r0] + cad[tx0], Xb = rxy[r0] + cad[tx1 - 1];
+                    const int Xc = rxy[r1] + cad[tx0], Xd = rxy[r1] + cad[tx1 - 1];
+                    const int Ya = rxy[a.rt + r0] + cad[a.ct + tx0], Yb = rxy[a.rt + r0] + cad[a.ct + tx1 - 1];
+                    const int Yc = rxy[a.rt + r1] + cad[a.ct + tx0], Yd = rxy[a.rt + r1] + cad[a.ct + tx1 - 1];
+                    // the tile's raw tap box (wave-uniform): wholly outside the level (every tap reads the border
+                    // value), wholly inside (no clamping, no border), or across the edge (clamped into the frame)
+                    const int rx0 = __builtin_amdgcn_readfirstlane(min(min(Xa, Xb), min(Xc, Xd)) >> kAbBits);
+                    const int rx1 = __builtin_amdgcn_readfirstlane(max(max(Xa, Xb), max(Xc, Xd)) >> kAbBits);
+                    const int ry0 = __builtin_amdgcn_readfirstlane(min(min(Ya, Yb), min(Yc, Yd)) >> kAbBits);
+                    const int ry1 = __builtin_amdgcn_readfirstlane(max(max(Ya, Yb), max(Yc, Yd)) >> kAbBits);
+                    const int y = ty0 + (lane >> 2), xq = tx0 + 8 * (lane & 3);   // this lane's 8 pixels
+                    const bool mine = y < ty1 && xq < tx1;
+                    if (rx1 + 1 < 0 || rx0 >= sw || ry1 + 1 < 0 || ry0 >= sh) {
+                        if (mine) {
+                            const uint32_t bw = (0x01010101u * (uint32_t)border) ^ kRoiFlip;
+                            *(uint2*)(ring + (size_t)(y & mask) * cp + xq) = make_uint2(bw, bw);
+                        }
+                        continue;   // (uniform; the buffer was not touched)
                     }
-                } else {
+                    const bool inner = rx0 >= 0 && rx1 + 1 < sw && ry0 >= 0 && ry1 + 1 < sh;
+                    const int bx0 = min(max(rx0, -2), sw), bx1 = min(max(rx1, -2), sw) + 1;
+                    const int by0 = min(max(ry0, -2), sh), by1 = min(max(ry1, -2), sh) + 1;
+                    // staged columns: the aligned words of source columns [bx0 & ~3, bx1] (the box's first column sits
+                    // at byte bx0 & 3 of the buffer row)
+                    const int cx0 = bx0 & ~3, nwd = ((bx1 - cx0) >> 2) + 1, nr = by1 - by0 + 1;
+                    // (a pure rotation of a 16 x 32 tile covers at most 35 x 35 source pixels + the tap neighbours and the
+                    // word alignment: nr <= 37 <= TM_FTB / TM_FTP, nwd <= 10 <= TM_FTP / 4 -- top_mma_fits' matrices)
+                    {
+                        // lane -> word column lane & 15 (< nwd) of rows (lane >> 4) + 4 i: every load of the box in flight
+                        // at once (<= 10 per lane), no division; an inner box's words are all inside the level's rows
+                        // (whose pitch holds >= 4 bytes past the width)
+                        const uint32_t bw4 = 0x01010101u * (uint32_t)border;
+                        const int wc = lane & 15, c = cx0 + 4 * wc;
+                        const bool col_in = wc < nwd, full = inner || (c >= 0 && c + 4 <= sw);
+                        uint32_t wds[TM_FTB / TM_FTP / 4];
 #pragma unroll
-                    for (int b = 0; b < 4; ++b) {
-                        const int X = (X0 + adv[b]) >> (kAbBits - kInterBits);
-                        const int Y = (Y0 + bdv[b]) >> (kAbBits - kInterBits);
-                        word |= (uint32_t)warp_tap(src, sw, sh, sp, X, Y, border) << (8 * b);
+                        for (int u = 0; u < TM_FTB / TM_FTP / 4; ++u) {
+                            const int r = (lane >> 4) + 4 * u, yy = by0 + r;
+                            const bool in = col_in && r < nr && full && (inner || (yy >= 0 && yy < sh));
+                            wds[u] = in ? *(const uint32_t*)(src + (size_t)yy * sp + c) : bw4;
+                        }
+#pragma unroll
+                        for (int u = 0; u < TM_FTB / TM_FTP / 4; ++u) {
+                            const int r = (lane >> 4) + 4 * u, yy = by0 + r;
+                            if (col_in && r < nr) {
+                                uint32_t w = wds[u];
+                                if (!full && yy >= 0 && yy < sh) {   // a word the level's edge cuts (boundary tiles)
+#pragma unroll
+                                    for (int b = 0; b < 4; ++b) {
+                                        const int x = c + b;
+                                        const uint32_t v = (x >= 0 && x < sw) ? src[(size_t)yy * sp + x] : (uint32_t)border;
+                                        w = (w & ~(0xffu << (8 * b))) | (v << (8 * b));
+                                    }
+                                }
+                                *(uint32_t*)(ft + r * TM_FTP + 4 * wc) = w;
+                            }
+                        }
+                        wave_sync();
                     }
+                    if (mine) {
+                        const int ry = y - U.y0;
+                        // the footprint origin folded into the row's fixed-point start (exact: a whole-pixel shift)
+                        const int X0 = rxy[ry] - (cx0 << kAbBits), Y0 = rxy[a.rt + ry] - (by0 << kAbBits);
+                        const int4 a0 = *(const int4*)(cad + xq), a1 = *(const int4*)(cad + xq + 4);
+                        const int4 b0 = *(const int4*)(cad + a.ct + xq), b1 = *(const int4*)(cad + a.ct + xq + 4);
+                        const int adv[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+                        const int bdv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+                        const int xlo = -2 - cx0, xhi = sw - cx0, ylo = -2 - by0, yhi = sh - by0;
+                        uint32_t wlo = 0, whi = 0;
+#pragma unroll
+                        for (int b = 0; b < 8; ++b) {
+                            const int X = X0 + adv[b], Y = Y0 + bdv[b];
+                            const int fx = (X >> (kAbBits - kInterBits)) & (kInterTab - 1);
+                            const int fy = (Y >> (kAbBits - kInterBits)) & (kInterTab - 1);
+                            int sx = X >> kAbBits, sy = Y >> kAbBits;
+                            if (!inner) {
+                                sx = min(max(sx, xlo), xhi);
+                                sy = min(max(sy, ylo), yhi);
+                            }
+                            const uint8_t* p = ft + __mul24(sy, TM_FTP) + sx;
+                            const int v0 = p[0], v1 = p[1], v2 = p[TM_FTP], v3 = p[TM_FTP + 1];
+                            const int h0 = __mul24(v1 - v0, fx) + (v0 << kInterBits);
+                            const int h1 = __mul24(v3 - v2, fx) + (v2 << kInterBits);
+                            const int v = (__mul24(h1 - h0, fy) + (h0 << kInterBits) + 512) >> 10;
+                            if (b < 4) wlo |= (uint32_t)v << (8 * b);
+                            else whi |= (uint32_t)v << (8 * (b - 4));
+                        }
+                        *(uint2*)(ring + (size_t)(y & mask) * cp + xq) = make_uint2(wlo ^ kRoiFlip, whi ^ kRoiFlip);
+                    }
+                    wave_sync();   // the buffer is reused by the wave's next tile
                 }
-                *(uint32_t*)(ring + (size_t)(y & mask) * cp + 4 * k) = word ^ kRoiFlip;
             }
             __syncthreads();
             // ---- H2: per new row, sum of I^2 over [x, x + tw) for the strip's output columns, 8 per item (sliding)
@@ -5035,22 +5103,24 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
                 const int r = it / nruns, k = it - r * nruns;
                 const int y = rs + r;
                 const uint8_t* row = ring + (size_t)(y & mask) * cp + 8 * k;
+                uint32_t wv_[TWW];
+#pragma unroll
+                for (int q = 0; q < TWW; ++q) wv_[q] = *(const uint32_t*)(row + 4 * q);
                 uint32_t h = 0;
-                int jx = 0;
-                for (; jx + 4 <= tw; jx += 4) {
-                    const uint32_t w = *(const uint32_t*)(row + jx) ^ kRoiFlip;
+#pragma unroll
+                for (int q = 0; q < TWW; ++q) {
+                    const uint32_t w = (wv_[q] ^ kRoiFlip) & tmask[q];
                     h = __builtin_amdgcn_udot4(w, w, h, false);
                 }
-                for (; jx < tw; ++jx) {
-                    const uint32_t b = row[jx] ^ 0x80u;
-                    h += b * b;
-                }
+                uint32_t bn[7], bo[7];
+#pragma unroll
+                for (int i = 1; i < 8; ++i) { bn[i - 1] = row[i + tw - 1]; bo[i - 1] = row[i - 1]; }
                 uint32_t o[8];
                 o[0] = h;
 #pragma unroll
                 for (int i = 1; i < 8; ++i) {
-                    const uint32_t bn = row[i + tw - 1] ^ 0x80u, bo = row[i - 1] ^ 0x80u;
-                    h = h + bn * bn - bo * bo;
+                    const uint32_t n_ = bn[i - 1] ^ 0x80u, o_ = bo[i - 1] ^ 0x80u;
+                    h = h + n_ * n_ - o_ * o_;
                     o[i] = h;
                 }
                 uint32_t* hd = h2 + (size_t)(y & mask) * hp + 8 * k;
@@ -5058,34 +5128,59 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
                 *(uint4*)(hd + 4) = make_uint4(o[4], o[5], o[6], o[7]);
             }
             __syncthreads();
-            // ---- the band's 16 x 16 output tiles, one wave each
+            // ---- the band's 16 x 16 output tiles, one wave each: NQM slots unrolled (A and B of every slot requested
+            // before the first MFMA; slots >= nq read zero B)
             for (int nb = wv; nb < nbu; nb += 4) {
                 fpm_v4i acc = zero4, acc1 = zero4;
-                const int co = a.R == 2 ? 16 * (lg & 1) : 16 * lg;
-                const int rstep = a.R == 2 ? 2 : 1;
-                int ro = a.R == 2 ? (lg >> 1) : 0;
-                for (int q = 0; q < (TOPMMA_ABL == 3 ? 0 : a.nq); ++q, ro += rstep) {
-                    const fpm_v4i av = *(const fpm_v4i*)(ring + (size_t)((yb + ln + ro) & mask) * cp + 16 * nb + co);
-                    const fpm_v4i bv = bl[q * 64 + lane];
-                    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv, acc, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, ro < th ? ones : zero4, acc1, 0, 0, 0);
+                if (TOPMMA_ABL != 3) {
+                    // slot q's fragments are requested two slots ahead of its MFMAs
+                    const uint8_t* abase = ring + 16 * nb + co;
+                    const int rstep = a.R == 2 ? 2 : 1, r0 = yb + ln + (a.R == 2 ? (lg >> 1) : 0);
+                    fpm_v4i av0 = *(const fpm_v4i*)(abase + (size_t)(r0 & mask) * cp), bv0 = bl[lane];
+                    fpm_v4i av1 = *(const fpm_v4i*)(abase + (size_t)((r0 + rstep) & mask) * cp), bv1 = bl[64 + lane];
+#pragma unroll
+                    for (int q = 0; q < NQM; ++q) {
+                        fpm_v4i av2 = zero4, bv2 = zero4;
+                        if (q + 2 < NQM) {
+                            av2 = *(const fpm_v4i*)(abase + (size_t)((r0 + (q + 2) * rstep) & mask) * cp);
+                            bv2 = bl[(q + 2) * 64 + lane];
+                        }
+                        // a template row past th (the odd row of the last two-row slot, or a slot past nq): its canvas
+                        // row enters neither sum (the correlation's B is zero there, the window sum's A is zeroed)
+                        if (TH == 0 && q >= a.nq - 1) {   // (uniform) only the last slot can hold such a row
+                            const int ro = a.R == 2 ? 2 * q + (lg >> 1) : q;
+                            if (ro >= th) av0 = zero4;
+                        }
+                        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(av0, bv0, acc, 0, 0, 0);
+                        acc1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av0, ones, acc1, 0, 0, 0);
+                        av0 = av1; bv0 = bv1; av1 = av2; bv1 = bv2;
+                    }
                 }
-                // D: column ln = output column 16 nb + ln, rows 4 lg + i = output rows yb + 4 lg + i
-                const int xo = 16 * nb + ln, yo0 = yb + 4 * lg;
                 if (TOPMMA_ABL == 4) {
                     if (acc[0] == 0x12345 && acc1[1] == 0x777) a.cand_cnt[0] = acc[2] + acc1[3];
                     continue;
                 }
+                // D: column ln = output column 16 nb + ln, rows 4 lg + i = output rows yb + 4 lg + i
+                const int xo = 16 * nb + ln, yo0 = yb + 4 * lg;
+                // sum of I^2 over the lane's 4 windows: rows yo0 .. yo0 + th - 1 of H2 (masked to th <= THM), then slid
+                // down by one row three times (the 3 entering rows read by their own offsets)
                 const uint32_t* hc = h2 + xo;
-                uint32_t hs = 0;
-                for (int k = 0; k < th; ++k) hs += hc[(size_t)((yo0 + k) & mask) * hp];
-                uint32_t wq[4];
-                wq[0] = hs;
+                uint32_t hv[THM], hn[3];
 #pragma unroll
-                for (int i = 1; i < 4; ++i) {
-                    hs += hc[(size_t)((yo0 + th - 1 + i) & mask) * hp] - hc[(size_t)((yo0 + i - 1) & mask) * hp];
-                    wq[i] = hs;
+                for (int k = 0; k < THM; ++k) hv[k] = hc[(size_t)((yo0 + k) & mask) * hp];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) hn[i] = hc[(size_t)((yo0 + th + i) & mask) * hp];
+                uint32_t wq[4];
+                wq[0] = 0;
+                if (TH > 0 || th == THM) {
+#pragma unroll
+                    for (int k = 0; k < THM; ++k) wq[0] += hv[k];
+                } else {
+#pragma unroll
+                    for (int k = 0; k < THM; ++k) wq[0] += k < th ? hv[k] : 0u;
                 }
+#pragma unroll
+                for (int i = 1; i < 4; ++i) wq[i] = wq[i - 1] + hn[i - 1] - hv[i - 1];
                 // the cheap part for the lane's 4 outputs: exact integer sums and the prefilter
                 uint32_t ccv[4], wsv[4];
                 uint32_t pm = 0;
@@ -5097,7 +5192,7 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
                     if (pass && a.mode == 0 && a.prefilter) {
                         // df = area sum I^2 - (sum I)^2 exactly (mod 2^32: its value is < 2^32 for area <= 257); 0 is a
                         // flat window, whose score is 0 (CCOEFF's t = 0 branch)
-                        const uint32_t dfi = area * wq[i] - wsv[i] * wsv[i];
+                        const uint32_t dfi = __umul24(area, wq[i]) - __umul24(wsv[i], wsv[i]);   // (24-bit factors)
                         const float wsf = (float)wsv[i];
                         const float nf = __builtin_fmaf(areaf, (float)ccv[i], -(wsf * tsumf));
                         const float nfp = nf + a.E;
@@ -5124,12 +5219,12 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
                         if (i == 0) sv0 = sc; else if (i == 1) sv1 = sc; else if (i == 2) sv2 = sc; else sv3 = sc;
                     }
                 }
-                if (a.mode == 0) {
+                if (a.mode == 0 && __ballot(tk != 0)) {   // (wave-uniform; rare)
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const bool take = (tk >> i) & 1u;
                         const uint64_t mk = __ballot(take);
-                        if (mk) {   // (wave-uniform; rare) one atomic per wave and output row
+                        if (mk) {   // one atomic per wave and output row
                             int base = 0;
                             if (lane == 0) base = atomicAdd(&a.cand_cnt[U.job], __popcll(mk));
                             base = __shfl(base, 0);
@@ -5154,8 +5249,21 @@ void launch_top_mma(const TopMmaArgs& a, hipStream_t st) {
     const size_t lds = top_mma_lds(a);
     // mode 1 touches only the jobs left by the greedy form (usually none): a small grid walks the unit list
     const int grid = a.mode == 1 ? std::min(a.nunits, 4 * device_cus()) : a.nunits;
-    ensure_lds_attr((const void*)k_top_mma, lds);
-    hipLaunchKernelGGL(k_top_mma, dim3(grid), dim3(256), lds, st, a);
+    // exact-height forms for the two-row layout's common top templates (16 rows: a square template at MinReduceArea
+    // 256, BASELINE configs[3]; 14: configs[2]), the masked small form for other heights up to 16
+    if (top_mma_small(a) && a.th == 16) {
+        ensure_lds_attr((const void*)k_top_mma<8, 16, 5, 16>, lds);
+        hipLaunchKernelGGL((k_top_mma<8, 16, 5, 16>), dim3(grid), dim3(256), lds, st, a);
+    } else if (top_mma_small(a) && a.th == 14) {
+        ensure_lds_attr((const void*)k_top_mma<7, 14, 5, 14>, lds);
+        hipLaunchKernelGGL((k_top_mma<7, 14, 5, 14>), dim3(grid), dim3(256), lds, st, a);
+    } else if (top_mma_small(a)) {
+        ensure_lds_attr((const void*)k_top_mma<8, 16, 5>, lds);
+        hipLaunchKernelGGL((k_top_mma<8, 16, 5>), dim3(grid), dim3(256), lds, st, a);
+    } else {
+        ensure_lds_attr((const void*)k_top_mma<16, 32, 13>, lds);
+        hipLaunchKernelGGL((k_top_mma<16, 32, 13>), dim3(grid), dim3(256), lds, st, a);
+    }
 }
 
 void launch_top_greedy(const NmsArgs& a0, int njobs, int max_cells, hipStream_t st, const CandInitArgs* ci) {
