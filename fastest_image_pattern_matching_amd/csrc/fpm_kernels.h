@@ -231,11 +231,10 @@ struct TopMmaArgs {
     int32_t tw, th, area;
     uint32_t tsum;           // sum of the template level's pixels
     int32_t sw;              // strip width (output columns, multiple of 16)
-    int32_t cp;              // canvas ring row pitch (bytes, multiple of 16)
-    int32_t rr;              // ring rows (power of two >= 16 + th - 1): canvas bytes and H2 rows
-    int32_t hp;              // H2 ring row pitch (u32)
+    int32_t cp;              // canvas ring row pitch (bytes; the kernel's compile-time TM_CP)
+    int32_t rr;              // ring rows per plane (power of two >= 16 + th - 1; the kernel form's RR)
     int32_t ct, rt;          // column / row table capacity (entries)
-    int32_t o_h2, o_colt, o_rowt, o_bf, o_ft;   // dynamic LDS offsets (bytes)
+    int32_t o_colt, o_rowt, o_bf, o_ft;   // dynamic LDS offsets (bytes)
     int32_t nqm;             // B slots staged in LDS (the kernel form's unrolled slot count; zero past nq)
     int32_t mode;            // 0: candidate lists, 1: full maps of the jobs with cand_cnt >= 0 (fallback)
     int32_t prefilter;       // 1: f32 bound before the exact f64 score (area <= 258, thr > 0)

@@ -24,6 +24,7 @@
 
 #include <map>
 #include <mutex>
+#include <type_traits>
 #include <utility>
 
 #include "fpm_kernels.h"
@@ -4877,47 +4878,47 @@ void launch_cand_step(const RoiArgs& a, int max_items, hipStream_t st) {
 // greedy form cannot take) gets its full map from a second launch of this kernel (mode 1) and the split peak kernels.
 //
 // Work unit: one job's strip of sw output columns, walked down in bands of 16 output rows.  Per band:
-//   sampling  the band's new canvas rows (sw + tw - 1 columns) into an LDS ring as i8 (x ^ 0x80), one word of four
-//             pixels per item, taps from the source level in global memory (L1/L2-resident: the top level is small);
-//   H2        per new canvas row and output column, the sum of I^2 over the template width (sliding, exact u32);
+//   sampling  the band's new canvas rows (sw + tw - 1 columns) into an LDS ring of three i8 planes: I' = I - 128,
+//             and the low (flipped) and high bytes of I'^2 (<= 16384), 8 pixels per lane, the taps from the wave's
+//             staged source footprint;
 //   MFMA      per 16 x 16 output tile and wave: D += A B on v_mfma_i32_16x16x64_i8 with A = canvas rows (the 16 output
 //             rows; K = 64 = two template rows x 32 columns, or one row x 64 columns for templates 18-49 wide) and B =
 //             the template row Toeplitz-banded over the 16 output columns (B[c][n] = T'[r][c - n], zero outside
-//             0 <= c - n < tw), so sum_slots D = sum T'I' exactly; a second MFMA with B = the band of ones gives
-//             sum I' over the window.  Exact: sum T I = sum T'I' + 128 (sum I + sum T) - 16384 area;
-//   epilogue  sum I^2 over the window from th + 3 H2 rows per lane (sliding over the lane's 4 output rows), then a
-//             conservative f32 bound (nf^2 >= thr^2 norm^2 area df, nf = area ccorr - sum I sum T, df = area sum I^2 -
+//             0 <= c - n < tw), so sum_slots D = sum T'I' exactly; three more MFMAs with B = the band of ones give the
+//             window sums of I' and of the two byte planes of I'^2.  Exact: sum T I = sum T'I' + 128 (sum I + sum T) -
+//             16384 area, sum I^2 = 256 (sum hi + sum I') + sum lo' + 16512 area;
+//   epilogue  a conservative f32 bound (nf^2 >= thr^2 norm^2 area df, nf = area ccorr - sum I sum T, df = area sum I^2 -
 //             (sum I)^2, with an absolute slack E on the two f32 terms) and, where it passes, the exact f64 score.
 // Exactness of the bound (prefilter): for area <= 258 every integer term is < 2^24 (exact in f32); the two products
 // carry at most 512 of rounding each (E = 1024), and thrK includes a 1e-5 relative margin over the f64 evaluation's
 // and the f32 score rounding's relative errors (<= 1e-6), so no output with (double)score >= thr is ever rejected.
 constexpr int TM_BH = 16;            // output rows per band (one MFMA M block)
-constexpr int TM_FTP = 48;           // sampling footprint buffer: row pitch (bytes) and size per wave
-constexpr int TM_FTB = 48 * 40;      // (a 16 x 32 tile of a rotation covers at most 37 x 37 source pixels + taps)
+constexpr int TM_CP = 288;           // ring row pitch (bytes >= kTopMmaMaxSw + 56; 72 words = 2 x 16 B mod 256 B: the
+                                     // 16 lanes of every ds_read_b128 lane group (8 rows x two 16-byte column blocks)
+                                     // and of every ds_write_b64 group (4 rows x 4 words) hit disjoint banks)
+constexpr int TM_FTP = 44;           // sampling footprint buffer: row pitch (bytes; an odd word count spreads the
+constexpr int TM_FTB = 44 * 40;      // taps over the banks) and size per wave (a 16 x 32 tile of a rotation covers at
+                                     // most 37 x 37 source pixels + taps)
 #ifndef TOPMMA_ABL
 #define TOPMMA_ABL 0
 #endif
 
 bool top_mma_fits(int tw, int th) { return tw >= 1 && th >= 1 && ((tw <= 17 && th <= 32) || (tw <= 49 && th <= 16)); }
 
-// the loop bounds every lane runs unrolled (NQM MFMA slots, THM H2 rows, TWW template words; a slot, row or word
-// beyond the template is masked, not branched around, so all of a loop's LDS reads are issued before the first use):
-// <8, 16, 5> for templates up to 17 x 16 (BASELINE configs[2] and [3]), <16, 32, 13> for every other shape
+// the loop bounds every lane runs unrolled (NQM MFMA slots; a slot beyond the template is masked, not branched
+// around, so all of the loop's LDS reads are issued before the first use) and the ring's rows (RR, a power of two
+// >= 16 + th - 1): <8, 32> for templates up to 17 x 16 (BASELINE configs[2] and [3]), <16, 64> for every other shape
 static bool top_mma_small(const TopMmaArgs& a) { return a.R == 2 && a.th <= 16; }
 
 void top_mma_layout(TopMmaArgs& a, int sw, int max_rows) {
     a.sw = sw;
     a.R = a.tw <= 17 ? 2 : 1;
     a.nq = a.R == 2 ? (a.th + 1) / 2 : a.th;
-    a.cp = sw + 64;                                  // A fragments read <= sw + 47, H2 runs <= sw + tw + 6
-    int rr = 1;
-    while (rr < TM_BH + a.th - 1) rr <<= 1;
-    a.rr = rr;
-    a.hp = sw + 4;                                   // (4g-row groups of a wave land 16 banks apart)
+    a.cp = TM_CP;                                    // A fragments read <= sw + 63, samples written <= sw + tw + 6
+    a.rr = top_mma_small(a) ? 32 : 64;
     a.ct = sw + 64;
     a.rt = max_rows + a.th + TM_BH;
-    a.o_h2 = a.rr * a.cp;
-    a.o_colt = a.o_h2 + 4 * a.rr * a.hp;
+    a.o_colt = 3 * a.rr * a.cp;                      // the ring's three planes
     a.o_rowt = a.o_colt + 8 * a.ct;
     a.o_bf = (a.o_rowt + 8 * a.rt + 15) & ~15;
     a.nqm = top_mma_small(a) ? 8 : 16;               // B slots in LDS (zero beyond nq)
@@ -4925,18 +4926,44 @@ void top_mma_layout(TopMmaArgs& a, int sw, int max_rows) {
 }
 size_t top_mma_lds(const TopMmaArgs& a) { return (size_t)a.o_ft + 4 * TM_FTB; }
 
-// TH > 0: the template height as a compile-time constant (two-row slots, NQM = (TH + 1) / 2, every slot and H2 row
-// exact: no masks); TH == 0: any height up to the form's bounds, rows past th masked
-template <int NQM, int THM, int TWW, int TH = 0>
+typedef short fpm_s2 __attribute__((ext_vector_type(2)));
+
+// 24-bit multiply-adds as single full-rate instructions (a plain int multiply whose operands the compiler cannot
+// bound becomes the quarter-rate v_mul_lo_u32, and it drops __mul24's sign extension when it proves it redundant)
+__device__ __forceinline__ int tm_mad_i24(int a, int b, int c) {
+    int r;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ int tm_mad_u24(int a, int b, int c) {
+    int r;
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(b), "v"(c));
+    return r;
+}
+
+// the three ring words of 4 canvas pixels from two pairs of 16-bit pixel values (p0 = pixels 0, 1; p1 = 2, 3):
+// I' (flipped bytes), the low bytes of I'^2 (flipped) and the high bytes (packed 16-bit squares, byte permutes)
+__device__ __forceinline__ void tm_planes(uint32_t p0, uint32_t p1, uint32_t& wi, uint32_t& wl, uint32_t& wh) {
+    const fpm_s2 k128 = {128, 128};
+    const fpm_s2 d0 = __builtin_bit_cast(fpm_s2, p0) - k128, d1 = __builtin_bit_cast(fpm_s2, p1) - k128;
+    const uint32_t q0 = __builtin_bit_cast(uint32_t, d0 * d0), q1 = __builtin_bit_cast(uint32_t, d1 * d1);
+    wi = __builtin_amdgcn_perm(p1, p0, 0x06040200u) ^ kRoiFlip;
+    wl = __builtin_amdgcn_perm(q1, q0, 0x06040200u) ^ kRoiFlip;
+    wh = __builtin_amdgcn_perm(q1, q0, 0x07050301u);
+}
+
+// TH > 0: the template height as a compile-time constant (two-row slots, NQM = (TH + 1) / 2, every slot exact: no
+// masks); TH == 0: any height up to the form's bounds, rows past th masked
+template <int NQM, int RR, int TH = 0>
 __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t tm_lds[];
+    constexpr int PS = RR * TM_CP;   // plane stride of the ring: I', lo(I'^2) ^ 0x80, hi(I'^2)
     uint8_t* const ring = tm_lds;
-    uint32_t* const h2 = (uint32_t*)(tm_lds + a.o_h2);
     int32_t* const cad = (int32_t*)(tm_lds + a.o_colt);   // adelta [ct], bdelta [ct] of the unit's canvas columns
     int32_t* const rxy = (int32_t*)(tm_lds + a.o_rowt);   // X0 [rt], Y0 [rt] of its canvas rows
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int ln = lane & 15, lg = lane >> 4;
-    const int tw = a.tw, th = TH > 0 ? TH : a.th, mask = a.rr - 1, cp = a.cp, hp = a.hp;
+    const int tw = a.tw, th = TH > 0 ? TH : a.th, mask = RR - 1;
     // the B fragments (correlation) staged once into LDS, zero past slot nq; the band of ones (window sum of I') in
     // registers: byte i of lane (n, g) is k = 16 g + i
     fpm_v4i* const bl = (fpm_v4i*)(tm_lds + a.o_bf);
@@ -4952,13 +4979,6 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
             if (c >= 0 && c < tw) w[i >> 2] |= 1u << (8 * (i & 3));
         }
         ones = fpm_v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
-    }
-    // byte masks of the template width for the H2 window's words
-    uint32_t tmask[TWW];
-#pragma unroll
-    for (int k = 0; k < TWW; ++k) {
-        const int n = tw - 4 * k;
-        tmask[k] = n >= 4 ? 0xffffffffu : n <= 0 ? 0u : (0xffffffffu >> (8 * (4 - n)));
     }
     const fpm_v4i zero4 = {0, 0, 0, 0};
     const uint32_t area = (uint32_t)a.area;
@@ -4986,7 +5006,7 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
             rxy[i] = rint_i((W.M[1] * y + W.M[2]) * kAbScale) + kRoundDelta;
             rxy[a.rt + i] = rint_i((W.M[4] * y + W.M[5]) * kAbScale) + kRoundDelta;
         }
-        const int ncw = (ncols + 3) >> 2, nruns = (swu + 7) >> 3, nbu = (swu + 15) >> 4;
+        const int nbu = (swu + 15) >> 4;
         for (int yb = U.y0; yb < U.y1; yb += TM_BH) {
             const int rs = yb == U.y0 ? yb : yb + th - 1;
             const int re = min(yb + TM_BH + th - 1, U.y0 + nrows);
@@ -5019,8 +5039,13 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
                     const bool mine = y < ty1 && xq < tx1;
                     if (rx1 + 1 < 0 || rx0 >= sw || ry1 + 1 < 0 || ry0 >= sh) {
                         if (mine) {
-                            const uint32_t bw = (0x01010101u * (uint32_t)border) ^ kRoiFlip;
-                            *(uint2*)(ring + (size_t)(y & mask) * cp + xq) = make_uint2(bw, bw);
+                            const uint32_t bp = (uint32_t)border * 0x10001u;
+                            uint32_t wi, wl, wh;
+                            tm_planes(bp, bp, wi, wl, wh);
+                            uint8_t* const rp = ring + (y & mask) * TM_CP + xq;
+                            *(uint2*)rp = make_uint2(wi, wi);
+                            *(uint2*)(rp + PS) = make_uint2(wl, wl);
+                            *(uint2*)(rp + 2 * PS) = make_uint2(wh, wh);
                         }
                         continue;   // (uniform; the buffer was not touched)
                     }
@@ -5044,7 +5069,7 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
                         for (int u = 0; u < TM_FTB / TM_FTP / 4; ++u) {
                             const int r = (lane >> 4) + 4 * u, yy = by0 + r;
                             const bool in = col_in && r < nr && full && (inner || (yy >= 0 && yy < sh));
-                            wds[u] = in ? *(const uint32_t*)(src + (size_t)yy * sp + c) : bw4;
+                            wds[u] = (in && TOPMMA_ABL != 5) ? *(const uint32_t*)(src + (size_t)yy * sp + c) : bw4;
                         }
 #pragma unroll
                         for (int u = 0; u < TM_FTB / TM_FTP / 4; ++u) {
@@ -5064,7 +5089,7 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
                         }
                         wave_sync();
                     }
-                    if (mine) {
+                    if (mine && TOPMMA_ABL != 6) {
                         const int ry = y - U.y0;
                         // the footprint origin folded into the row's fixed-point start (exact: a whole-pixel shift)
                         const int X0 = rxy[ry] - (cx0 << kAbBits), Y0 = rxy[a.rt + ry] - (by0 << kAbBits);
@@ -5073,132 +5098,116 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
                         const int adv[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
                         const int bdv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
                         const int xlo = -2 - cx0, xhi = sw - cx0, ylo = -2 - by0, yhi = sh - by0;
-                        uint32_t wlo = 0, whi = 0;
+                        uint32_t pv[4] = {0, 0, 0, 0};
+                        // (inner is wave-uniform: two copies of the loop, the inner one without the clamps)
+                        auto gather = [&](auto inner_c) {
 #pragma unroll
-                        for (int b = 0; b < 8; ++b) {
-                            const int X = X0 + adv[b], Y = Y0 + bdv[b];
-                            const int fx = (X >> (kAbBits - kInterBits)) & (kInterTab - 1);
-                            const int fy = (Y >> (kAbBits - kInterBits)) & (kInterTab - 1);
-                            int sx = X >> kAbBits, sy = Y >> kAbBits;
-                            if (!inner) {
-                                sx = min(max(sx, xlo), xhi);
-                                sy = min(max(sy, ylo), yhi);
+                            for (int b = 0; b < 8; ++b) {
+                                const int X = X0 + adv[b], Y = Y0 + bdv[b];
+                                const int fx = (X >> (kAbBits - kInterBits)) & (kInterTab - 1);
+                                const int fy = (Y >> (kAbBits - kInterBits)) & (kInterTab - 1);
+                                int sx = X >> kAbBits, sy = Y >> kAbBits;
+                                if (!decltype(inner_c)::value) {
+                                    sx = min(max(sx, xlo), xhi);
+                                    sy = min(max(sy, ylo), yhi);
+                                }
+                                const uint8_t* p = ft + tm_mad_u24(sy, TM_FTP, sx);   // (0 <= sy, sx < TM_FTP)
+                                const int v0 = p[0], v1 = p[1], v2 = p[TM_FTP], v3 = p[TM_FTP + 1];
+                                const int h0 = tm_mad_i24(v1 - v0, fx, v0 << kInterBits);
+                                const int h1 = tm_mad_i24(v3 - v2, fx, v2 << kInterBits);
+                                const int v = tm_mad_i24(h1 - h0, fy, (h0 << kInterBits) + 512) >> 10;
+                                pv[b >> 1] |= (uint32_t)v << (16 * (b & 1));
                             }
-                            const uint8_t* p = ft + __mul24(sy, TM_FTP) + sx;
-                            const int v0 = p[0], v1 = p[1], v2 = p[TM_FTP], v3 = p[TM_FTP + 1];
-                            const int h0 = __mul24(v1 - v0, fx) + (v0 << kInterBits);
-                            const int h1 = __mul24(v3 - v2, fx) + (v2 << kInterBits);
-                            const int v = (__mul24(h1 - h0, fy) + (h0 << kInterBits) + 512) >> 10;
-                            if (b < 4) wlo |= (uint32_t)v << (8 * b);
-                            else whi |= (uint32_t)v << (8 * (b - 4));
-                        }
-                        *(uint2*)(ring + (size_t)(y & mask) * cp + xq) = make_uint2(wlo ^ kRoiFlip, whi ^ kRoiFlip);
+                        };
+                        if (inner) gather(std::true_type{});
+                        else gather(std::false_type{});
+                        uint32_t wi0, wl0, wh0, wi1, wl1, wh1;
+                        tm_planes(pv[0], pv[1], wi0, wl0, wh0);
+                        tm_planes(pv[2], pv[3], wi1, wl1, wh1);
+                        uint8_t* const rp = ring + (y & mask) * TM_CP + xq;
+                        *(uint2*)rp = make_uint2(wi0, wi1);
+                        *(uint2*)(rp + PS) = make_uint2(wl0, wl1);
+                        *(uint2*)(rp + 2 * PS) = make_uint2(wh0, wh1);
                     }
                     wave_sync();   // the buffer is reused by the wave's next tile
                 }
             }
             __syncthreads();
-            // ---- H2: per new row, sum of I^2 over [x, x + tw) for the strip's output columns, 8 per item (sliding)
-            for (int it = tid; it < (TOPMMA_ABL == 2 ? 0 : (re - rs) * nruns); it += 256) {
-                const int r = it / nruns, k = it - r * nruns;
-                const int y = rs + r;
-                const uint8_t* row = ring + (size_t)(y & mask) * cp + 8 * k;
-                uint32_t wv_[TWW];
-#pragma unroll
-                for (int q = 0; q < TWW; ++q) wv_[q] = *(const uint32_t*)(row + 4 * q);
-                uint32_t h = 0;
-#pragma unroll
-                for (int q = 0; q < TWW; ++q) {
-                    const uint32_t w = (wv_[q] ^ kRoiFlip) & tmask[q];
-                    h = __builtin_amdgcn_udot4(w, w, h, false);
-                }
-                uint32_t bn[7], bo[7];
-#pragma unroll
-                for (int i = 1; i < 8; ++i) { bn[i - 1] = row[i + tw - 1]; bo[i - 1] = row[i - 1]; }
-                uint32_t o[8];
-                o[0] = h;
-#pragma unroll
-                for (int i = 1; i < 8; ++i) {
-                    const uint32_t n_ = bn[i - 1] ^ 0x80u, o_ = bo[i - 1] ^ 0x80u;
-                    h = h + n_ * n_ - o_ * o_;
-                    o[i] = h;
-                }
-                uint32_t* hd = h2 + (size_t)(y & mask) * hp + 8 * k;
-                *(uint4*)hd = make_uint4(o[0], o[1], o[2], o[3]);
-                *(uint4*)(hd + 4) = make_uint4(o[4], o[5], o[6], o[7]);
-            }
-            __syncthreads();
             // ---- the band's 16 x 16 output tiles, one wave each: NQM slots unrolled (A and B of every slot requested
             // before the first MFMA; slots >= nq read zero B)
             for (int nb = wv; nb < nbu; nb += 4) {
-                fpm_v4i acc = zero4, acc1 = zero4;
+                fpm_v4i acc = zero4, acc1 = zero4, accl = zero4, acch = zero4;
                 if (TOPMMA_ABL != 3) {
-                    // slot q's fragments are requested two slots ahead of its MFMAs
+                    // slot q's fragments (three planes) are requested two slots ahead of its MFMAs
                     const uint8_t* abase = ring + 16 * nb + co;
                     const int rstep = a.R == 2 ? 2 : 1, r0 = yb + ln + (a.R == 2 ? (lg >> 1) : 0);
-                    fpm_v4i av0 = *(const fpm_v4i*)(abase + (size_t)(r0 & mask) * cp), bv0 = bl[lane];
-                    fpm_v4i av1 = *(const fpm_v4i*)(abase + (size_t)((r0 + rstep) & mask) * cp), bv1 = bl[64 + lane];
+                    fpm_v4i av[3][3], bv[3];
+#pragma unroll
+                    for (int q = 0; q < 2; ++q) {
+                        const uint8_t* ap = abase + ((r0 + q * rstep) & mask) * TM_CP;
+#pragma unroll
+                        for (int pl = 0; pl < 3; ++pl) av[q][pl] = *(const fpm_v4i*)(ap + pl * PS);
+                        bv[q] = bl[q * 64 + lane];
+                    }
 #pragma unroll
                     for (int q = 0; q < NQM; ++q) {
-                        fpm_v4i av2 = zero4, bv2 = zero4;
                         if (q + 2 < NQM) {
-                            av2 = *(const fpm_v4i*)(abase + (size_t)((r0 + (q + 2) * rstep) & mask) * cp);
-                            bv2 = bl[(q + 2) * 64 + lane];
+                            const uint8_t* ap = abase + ((r0 + (q + 2) * rstep) & mask) * TM_CP;
+#pragma unroll
+                            for (int pl = 0; pl < 3; ++pl) av[(q + 2) % 3][pl] = *(const fpm_v4i*)(ap + pl * PS);
+                            bv[(q + 2) % 3] = bl[(q + 2) * 64 + lane];
                         }
+                        fpm_v4i* const A = av[q % 3];
                         // a template row past th (the odd row of the last two-row slot, or a slot past nq): its canvas
-                        // row enters neither sum (the correlation's B is zero there, the window sum's A is zeroed)
+                        // row enters no sum (the correlation's B is zero there, the window sums' A are zeroed)
                         if (TH == 0 && q >= a.nq - 1) {   // (uniform) only the last slot can hold such a row
                             const int ro = a.R == 2 ? 2 * q + (lg >> 1) : q;
-                            if (ro >= th) av0 = zero4;
+                            if (ro >= th) A[0] = A[1] = A[2] = zero4;
                         }
-                        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(av0, bv0, acc, 0, 0, 0);
-                        acc1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av0, ones, acc1, 0, 0, 0);
-                        av0 = av1; bv0 = bv1; av1 = av2; bv1 = bv2;
+                        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0], bv[q % 3], acc, 0, 0, 0);
+                        acc1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0], ones, acc1, 0, 0, 0);
+                        accl = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1], ones, accl, 0, 0, 0);
+                        acch = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[2], ones, acch, 0, 0, 0);
                     }
                 }
                 if (TOPMMA_ABL == 4) {
-                    if (acc[0] == 0x12345 && acc1[1] == 0x777) a.cand_cnt[0] = acc[2] + acc1[3];
+                    if (acc[0] == 0x12345 && acc1[1] == 0x777) a.cand_cnt[0] = acc[2] + acc1[3] + accl[0] + acch[1];
                     continue;
                 }
                 // D: column ln = output column 16 nb + ln, rows 4 lg + i = output rows yb + 4 lg + i
                 const int xo = 16 * nb + ln, yo0 = yb + 4 * lg;
-                // sum of I^2 over the lane's 4 windows: rows yo0 .. yo0 + th - 1 of H2 (masked to th <= THM), then slid
-                // down by one row three times (the 3 entering rows read by their own offsets)
-                const uint32_t* hc = h2 + xo;
-                uint32_t hv[THM], hn[3];
-#pragma unroll
-                for (int k = 0; k < THM; ++k) hv[k] = hc[(size_t)((yo0 + k) & mask) * hp];
-#pragma unroll
-                for (int i = 0; i < 3; ++i) hn[i] = hc[(size_t)((yo0 + th + i) & mask) * hp];
-                uint32_t wq[4];
-                wq[0] = 0;
-                if (TH > 0 || th == THM) {
-#pragma unroll
-                    for (int k = 0; k < THM; ++k) wq[0] += hv[k];
-                } else {
-#pragma unroll
-                    for (int k = 0; k < THM; ++k) wq[0] += k < th ? hv[k] : 0u;
-                }
-#pragma unroll
-                for (int i = 1; i < 4; ++i) wq[i] = wq[i - 1] + hn[i - 1] - hv[i - 1];
-                // the cheap part for the lane's 4 outputs: exact integer sums and the prefilter
-                uint32_t ccv[4], wsv[4];
-                uint32_t pm = 0;
+                // the cheap part for the lane's 4 outputs: exact integer sums and the prefilter (pairs of outputs in
+                // packed f32 lanes)
+                uint32_t ccv[4], wsv[4], wq[4], dfi[4];
+                const uint32_t ccofs = 128u * a.tsum - 16384u * area, qofs = 16512u * area;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     wsv[i] = (uint32_t)acc1[i] + 128u * area;
-                    ccv[i] = (uint32_t)acc[i] + 128u * (wsv[i] + a.tsum) - 16384u * area;
-                    bool pass = yo0 + i < U.y1 && xo < swu;
-                    if (pass && a.mode == 0 && a.prefilter) {
-                        // df = area sum I^2 - (sum I)^2 exactly (mod 2^32: its value is < 2^32 for area <= 257); 0 is a
-                        // flat window, whose score is 0 (CCOEFF's t = 0 branch)
-                        const uint32_t dfi = __umul24(area, wq[i]) - __umul24(wsv[i], wsv[i]);   // (24-bit factors)
-                        const float wsf = (float)wsv[i];
-                        const float nf = __builtin_fmaf(areaf, (float)ccv[i], -(wsf * tsumf));
-                        const float nfp = nf + a.E;
-                        pass = dfi != 0u && nfp > 0.f && nfp * nfp >= a.thrK * (float)dfi;
+                    ccv[i] = (uint32_t)acc[i] + (wsv[i] << 7) + ccofs;
+                    wq[i] = (((uint32_t)acch[i] + (uint32_t)acc1[i]) << 8) + (uint32_t)accl[i] + qofs;
+                    // df = area sum I^2 - (sum I)^2 exactly (mod 2^32: its value is < 2^32 for area <= 257; 24-bit
+                    // factors); 0 is a flat window, whose score is 0 (CCOEFF's t = 0 branch)
+                    dfi[i] = __umul24(area, wq[i]) - __umul24(wsv[i], wsv[i]);
+                }
+                uint32_t pm = 0;
+                const bool colok = xo < swu;
+                if (a.mode == 0 && a.prefilter) {
+                    typedef float f2_t __attribute__((ext_vector_type(2)));
+                    const f2_t ar2 = {areaf, areaf}, ts2 = {tsumf, tsumf}, e2 = {a.E, a.E}, k2 = {a.thrK, a.thrK};
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int i0 = 2 * h, i1 = 2 * h + 1;
+                        const f2_t ws = {(float)wsv[i0], (float)wsv[i1]}, cc = {(float)ccv[i0], (float)ccv[i1]};
+                        const f2_t df = {(float)dfi[i0], (float)dfi[i1]};
+                        const f2_t nfp = __builtin_elementwise_fma(ar2, cc, -(ws * ts2)) + e2;
+                        const f2_t lhs = nfp * nfp, rhs = k2 * df;
+                        if (colok && yo0 + i0 < U.y1 && dfi[i0] != 0u && nfp.x > 0.f && lhs.x >= rhs.x) pm |= 1u << i0;
+                        if (colok && yo0 + i1 < U.y1 && dfi[i1] != 0u && nfp.y > 0.f && lhs.y >= rhs.y) pm |= 1u << i1;
                     }
-                    pm |= pass ? 1u << i : 0u;
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (colok && yo0 + i < U.y1) pm |= 1u << i;
                 }
                 // the exact f64 score where the bound passed (rare in mode 0; every valid output in mode 1), one
                 // instance of ccoeff in a data-dependent loop (the register budget of the MFMA loop stays small)
@@ -5252,17 +5261,17 @@ void launch_top_mma(const TopMmaArgs& a, hipStream_t st) {
     // exact-height forms for the two-row layout's common top templates (16 rows: a square template at MinReduceArea
     // 256, BASELINE configs[3]; 14: configs[2]), the masked small form for other heights up to 16
     if (top_mma_small(a) && a.th == 16) {
-        ensure_lds_attr((const void*)k_top_mma<8, 16, 5, 16>, lds);
-        hipLaunchKernelGGL((k_top_mma<8, 16, 5, 16>), dim3(grid), dim3(256), lds, st, a);
+        ensure_lds_attr((const void*)k_top_mma<8, 32, 16>, lds);
+        hipLaunchKernelGGL((k_top_mma<8, 32, 16>), dim3(grid), dim3(256), lds, st, a);
     } else if (top_mma_small(a) && a.th == 14) {
-        ensure_lds_attr((const void*)k_top_mma<7, 14, 5, 14>, lds);
-        hipLaunchKernelGGL((k_top_mma<7, 14, 5, 14>), dim3(grid), dim3(256), lds, st, a);
+        ensure_lds_attr((const void*)k_top_mma<7, 32, 14>, lds);
+        hipLaunchKernelGGL((k_top_mma<7, 32, 14>), dim3(grid), dim3(256), lds, st, a);
     } else if (top_mma_small(a)) {
-        ensure_lds_attr((const void*)k_top_mma<8, 16, 5>, lds);
-        hipLaunchKernelGGL((k_top_mma<8, 16, 5>), dim3(grid), dim3(256), lds, st, a);
+        ensure_lds_attr((const void*)k_top_mma<8, 32>, lds);
+        hipLaunchKernelGGL((k_top_mma<8, 32>), dim3(grid), dim3(256), lds, st, a);
     } else {
-        ensure_lds_attr((const void*)k_top_mma<16, 32, 13>, lds);
-        hipLaunchKernelGGL((k_top_mma<16, 32, 13>), dim3(grid), dim3(256), lds, st, a);
+        ensure_lds_attr((const void*)k_top_mma<16, 64>, lds);
+        hipLaunchKernelGGL((k_top_mma<16, 64>), dim3(grid), dim3(256), lds, st, a);
     }
 }
 
