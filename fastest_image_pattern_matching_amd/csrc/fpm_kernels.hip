@@ -4893,9 +4893,11 @@ void launch_cand_step(const RoiArgs& a, int max_items, hipStream_t st) {
 // carry at most 512 of rounding each (E = 1024), and thrK includes a 1e-5 relative margin over the f64 evaluation's
 // and the f32 score rounding's relative errors (<= 1e-6), so no output with (double)score >= thr is ever rejected.
 constexpr int TM_BH = 16;            // output rows per band (one MFMA M block)
-constexpr int TM_CP = 288;           // ring row pitch (bytes >= kTopMmaMaxSw + 56; 72 words = 2 x 16 B mod 256 B: the
-                                     // 16 lanes of every ds_read_b128 lane group (8 rows x two 16-byte column blocks)
-                                     // and of every ds_write_b64 group (4 rows x 4 words) hit disjoint banks)
+// ring row pitch (bytes): the A fragments of the two-row layout read columns <= sw + 15 and the samples reach
+// sw + tw + 6 (<= 215); the one-row layout's reach sw + 63.  Both are +-2 x 16 B mod 256 B (56 / 72 words), so the 16
+// lanes of every ds_read_b128 lane group (rows ln at two 16-byte column blocks) and of every ds_write_b64 group (4
+// rows x 4 words) hit disjoint banks
+constexpr int TM_CP2 = 224, TM_CP1 = 288;
 constexpr int TM_FTP = 44;           // sampling footprint buffer: row pitch (bytes; an odd word count spreads the
 constexpr int TM_FTB = 44 * 40;      // taps over the banks) and size per wave (a 16 x 32 tile of a rotation covers at
                                      // most 37 x 37 source pixels + taps)
@@ -4914,10 +4916,10 @@ void top_mma_layout(TopMmaArgs& a, int sw, int max_rows) {
     a.sw = sw;
     a.R = a.tw <= 17 ? 2 : 1;
     a.nq = a.R == 2 ? (a.th + 1) / 2 : a.th;
-    a.cp = TM_CP;                                    // A fragments read <= sw + 63, samples written <= sw + tw + 6
+    a.cp = top_mma_small(a) ? TM_CP2 : TM_CP1;
     a.rr = top_mma_small(a) ? 32 : 64;
-    a.ct = sw + 64;
-    a.rt = max_rows + a.th + TM_BH;
+    a.ct = (sw + a.tw - 1 + 8 + 3) & ~3;             // canvas columns (+ the 8-pixel reads past the last one)
+    a.rt = max_rows + a.th;                          // canvas rows of the tallest unit
     a.o_colt = 3 * a.rr * a.cp;                      // the ring's three planes
     a.o_rowt = a.o_colt + 8 * a.ct;
     a.o_bf = (a.o_rowt + 8 * a.rt + 15) & ~15;
@@ -4954,8 +4956,11 @@ __device__ __forceinline__ void tm_planes(uint32_t p0, uint32_t p1, uint32_t& wi
 
 // TH > 0: the template height as a compile-time constant (two-row slots, NQM = (TH + 1) / 2, every slot exact: no
 // masks); TH == 0: any height up to the form's bounds, rows past th masked
-template <int NQM, int RR, int TH = 0>
-__global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
+// The exact-height two-row forms (<= 40 KB of LDS at the BASELINE shapes) are held to 128 registers: 4 workgroups
+// per CU.
+template <int NQM, int RR, int TM_CP, int TH = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RR == 32 && TH > 0 ? 4 : 1)))
+void k_top_mma(TopMmaArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t tm_lds[];
     constexpr int PS = RR * TM_CP;   // plane stride of the ring: I', lo(I'^2) ^ 0x80, hi(I'^2)
     uint8_t* const ring = tm_lds;
@@ -4984,7 +4989,14 @@ __global__ __launch_bounds__(256) void k_top_mma(TopMmaArgs a) {
     const uint32_t area = (uint32_t)a.area;
     const float areaf = (float)a.area, tsumf = (float)a.tsum;
     const int co = a.R == 2 ? 16 * (lg & 1) : 16 * lg;   // the lane's A / B column offset in a slot
-    for (int u = blockIdx.x; u < a.nunits; u += gridDim.x) {
+    // XCD-aware order (mode 0, one unit per workgroup): consecutive workgroups go to the 8 XCDs in turn, so XCD x
+    // takes the x-th contiguous eighth of the unit list (the units of a few sources: their top levels stay in its L2)
+    int u0 = blockIdx.x;
+    if (a.mode == 0 && (int)gridDim.x == a.nunits) {
+        const int x = blockIdx.x & 7, q = a.nunits >> 3, r = a.nunits & 7;
+        u0 = x * q + min(x, r) + (blockIdx.x >> 3);
+    }
+    for (int u = u0; u < a.nunits; u += gridDim.x) {
         const TopUnit U = a.units[u];
         if (a.mode == 1 && a.cand_cnt[U.job] < 0) continue;   // (uniform) taken from its list: no map needed
         const WarpJob& W = a.wjobs[U.job];
@@ -5261,17 +5273,17 @@ void launch_top_mma(const TopMmaArgs& a, hipStream_t st) {
     // exact-height forms for the two-row layout's common top templates (16 rows: a square template at MinReduceArea
     // 256, BASELINE configs[3]; 14: configs[2]), the masked small form for other heights up to 16
     if (top_mma_small(a) && a.th == 16) {
-        ensure_lds_attr((const void*)k_top_mma<8, 32, 16>, lds);
-        hipLaunchKernelGGL((k_top_mma<8, 32, 16>), dim3(grid), dim3(256), lds, st, a);
+        ensure_lds_attr((const void*)k_top_mma<8, 32, TM_CP2, 16>, lds);
+        hipLaunchKernelGGL((k_top_mma<8, 32, TM_CP2, 16>), dim3(grid), dim3(256), lds, st, a);
     } else if (top_mma_small(a) && a.th == 14) {
-        ensure_lds_attr((const void*)k_top_mma<7, 32, 14>, lds);
-        hipLaunchKernelGGL((k_top_mma<7, 32, 14>), dim3(grid), dim3(256), lds, st, a);
+        ensure_lds_attr((const void*)k_top_mma<7, 32, TM_CP2, 14>, lds);
+        hipLaunchKernelGGL((k_top_mma<7, 32, TM_CP2, 14>), dim3(grid), dim3(256), lds, st, a);
     } else if (top_mma_small(a)) {
-        ensure_lds_attr((const void*)k_top_mma<8, 32>, lds);
-        hipLaunchKernelGGL((k_top_mma<8, 32>), dim3(grid), dim3(256), lds, st, a);
+        ensure_lds_attr((const void*)k_top_mma<8, 32, TM_CP2>, lds);
+        hipLaunchKernelGGL((k_top_mma<8, 32, TM_CP2>), dim3(grid), dim3(256), lds, st, a);
     } else {
-        ensure_lds_attr((const void*)k_top_mma<16, 64>, lds);
-        hipLaunchKernelGGL((k_top_mma<16, 64>), dim3(grid), dim3(256), lds, st, a);
+        ensure_lds_attr((const void*)k_top_mma<16, 64, TM_CP1>, lds);
+        hipLaunchKernelGGL((k_top_mma<16, 64, TM_CP1>), dim3(grid), dim3(256), lds, st, a);
     }
 }
 
