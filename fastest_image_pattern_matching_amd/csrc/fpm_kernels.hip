@@ -1715,6 +1715,18 @@ __global__ __launch_bounds__(256) void k_nms_greedy(NmsArgs a, CandInitArgs ci, 
             const int tx = __builtin_amdgcn_readlane(x, l), ty = __builtin_amdgcn_readlane(y, l);
             const float tv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
             const int sx = (int)(tx - tw * (1 - ov)), sy = (int)(ty - th * (1 - ov));
+            if (!(tx >= sx && tx < sx + rw && ty >= sy && ty < sy + rh)) {
+                // (uniform) a painted rectangle that misses its own peak (e.g. MaxOverlap 0.8 on a 5-row template:
+                // int(2 * 5 * 0.2) = 1 row, starting a row above): the peak stays the map's maximum, so the reference
+                // takes it again with every remaining getNextMaxLoc call
+                if (lane == 0)
+                    for (int k = cnt; k < a.cap; ++k) {
+                        out[k].x = tx; out[k].y = ty; out[k].score = tv;
+                        if (ci_mode && k < kNmsInitCap) { spk[k].x = tx; spk[k].y = ty; spk[k].score = tv; }
+                    }
+                cnt = a.cap;
+                break;
+            }
             if (lane == 0) {
                 out[cnt].x = tx; out[cnt].y = ty; out[cnt].score = tv;
                 accx[cnt] = sx; accy[cnt] = sy;

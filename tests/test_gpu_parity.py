@@ -241,7 +241,8 @@ def test_top_fused_lds_threshold(gpu_matcher_factory, templates, monkeypatch):
     """k_top_fused forced (FPM_TOP_FUSED=1) on top canvases either side of its LDS limit (64 KB minus the kernel's
     static LDS, read with hipFuncGetAttributes): Dst10 at +-180 over square sources whose largest rotated top canvas
     needs 56.5 KB (364 px) up to ~67 KB (396 px) of dynamic LDS.  Below the limit the fused kernel runs, above it the
-    engine falls back to the split top layer (no fused launch beyond the limit); every search equals the oracle."""
+    engine falls back to another top-layer form (the matrix-core or the split one: no fused launch beyond the limit);
+    every search equals the oracle."""
     from fastest_image_pattern_matching_amd import _lib as L
 
     monkeypatch.setenv("FPM_TOP_FUSED", "1")
@@ -255,7 +256,8 @@ def test_top_fused_lds_threshold(gpu_matcher_factory, templates, monkeypatch):
         m.profile(True)
         m.profile_reset()
         got = [r.as_tuple() for r in m.match(s)]
-        fused[size] = m.profile_get(L.KERNEL_NAMES.index("top_warp"))[1] == 0   # the split form launches k_warp
+        # the split form launches k_warp, the matrix-core form its map fallback (top_map)
+        fused[size] = all(m.profile_get(L.KERNEL_NAMES.index(k))[1] == 0 for k in ("top_warp", "top_map"))
         m.profile(False)
         o = oracle.OracleMatcher().set(max_pos=3, tolerance_angle=180.0)
         assert o.learnPattern(t)

@@ -154,3 +154,22 @@ def test_plain_peaks_overlapping_rectangles(gpu_matcher_factory, templates, monk
     exp, ostats = _oracle([s], t, prm)
     got, stats, _ = _search(gpu_matcher_factory, [s], t, prm)
     assert got == exp and stats == ostats
+
+
+@pytest.mark.parametrize("form", ["default", "fallback", "split"])
+def test_rect_missing_its_peak(gpu_matcher_factory, monkeypatch, form):
+    """MaxOverlap 0.8 on a 107 x 35 template (top level 14 x 5): getNextMaxLoc paints int(2 * 5 * 0.2) = 1 row starting
+    a row above the peak, so the peak survives and the reference takes it again with every remaining call (14 equal
+    records per angle).  The greedy form reproduces the repeats; records, stats and results equal the oracle's."""
+    from tests.test_gpu_fuzz import _case
+
+    _set(monkeypatch, form)
+    s, t, prm = _case(24)
+    o = oracle.OracleMatcher().set(**prm)
+    assert o.learnPattern(t)
+    exp = o.match(s)
+    m = gpu_matcher_factory(**prm)
+    assert m.learnPattern(t)
+    got = [r.as_tuple() for r in m.match(s)]
+    assert m.last_candidates(0).tobytes() == o.candidates().tobytes()
+    assert got == exp and m.search_stats() == o.stats()
