@@ -12,8 +12,10 @@ ranks.  Multi-GPU: one process per GPU (torchrun), every rank searches its own s
 data-path collective); barrier + synchronize bracket the K timed steps and the max time over ranks is used.
 
 Also reported: the dominant kernel's roofline (HIP events around every launch on the library's stream, in a
-second pass of K steps over one context's share of the sources, so the timed pass carries no event overhead) and the CPU baseline (the oracle
-restatement, single thread, on a bounded sample of the same workload, rank 0 at N=1 only).
+second pass of K steps over one context's share of the sources, so the timed pass carries no event overhead) and the
+CPU baseline (the oracle restatement, single thread, on a bounded sample of the same workload, rank 0 at N=1 only).
+``roofline_issue`` puts the same kernel's instruction counters (committed SQ passes of the workload's kernel pass,
+scripts/pmc_bench.sh) against the chip's VALU issue, LDS-array and matrix-pipe cycles in its measured launch time.
 
 Roofline bytes are SURVEY.md §8(d)'s algorithmic bytes, reported by the library per search (fpm_search_bytes) and per
 kernel (fpm_profile_get): B_pyr + B_top + B_ref, where a refinement ROI costs its source footprint, the template
@@ -59,40 +61,82 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-TRAFFIC_CSV = os.path.join(REPO, "profiles", "latest", "pmc_traffic.csv")
-TRAFFIC_SOURCE = ("committed rocprofv3 --pmc snapshot profiles/latest/pmc_traffic.csv (scripts/pmc_bench.sh: separate "
-                  "FETCH_SIZE / WRITE_SIZE passes of bench.py --kernel-pass-only, FETCH_SIZE doubled for gfx950, mean per "
+# committed rocprofv3 --pmc snapshots of each workload's kernel pass (scripts/pmc_bench.sh TAG WORKLOAD)
+TRAFFIC_CSV = {"src7": os.path.join(REPO, "profiles", "latest", "pmc_traffic.csv"),
+               "config3": os.path.join(REPO, "profiles", "latest", "pmc_traffic_config3.csv")}
+TRAFFIC_SOURCE = ("committed rocprofv3 --pmc snapshot {} (scripts/pmc_bench.sh: separate FETCH_SIZE / WRITE_SIZE "
+                  "passes of bench.py --workload {} --kernel-pass-only, FETCH_SIZE doubled for gfx950, mean per "
                   "dispatch); not measured in this run")
+ISSUE_SOURCE = ("committed rocprofv3 --pmc snapshot {} (scripts/pmc_bench.sh: two SQ passes of bench.py --workload {} "
+                "--kernel-pass-only, mean per dispatch); counters not measured in this run, launch time measured live")
+SIMDS, CUS, CLOCK_GHZ = 1024, 256, 2.4   # MI355X_MICROARCH.md: 256 CUs x 4 SIMDs, 2.4 GHz peak engine clock
+VALU_ISSUE_CYCLES = 2                    # a wave64 VALU instruction issues over 2 cycles (32 lanes per cycle)
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` (a profiling index name, _lib.KERNEL_NAMES) from the committed PMC summary
-    (scripts/pmc_bench.sh: separate FETCH_SIZE / WRITE_SIZE passes over `bench.py --kernel-pass-only`, FETCH_SIZE
-    doubled for gfx950, per-dispatch means); None if not collected for this kernel."""
+def pmc_counters(kernel, workload):
+    """Per-launch means of every counter of `kernel` (a profiling index name, _lib.KERNEL_NAMES) in the committed PMC
+    snapshot of `workload`: every instantiation of the kernel's first matching symbol, weighted by its dispatches (the
+    same launches the kernel pass averages over).  {} if not collected."""
     import csv
 
     from fastest_image_pattern_matching_amd import _lib as L
 
-    if not os.path.exists(TRAFFIC_CSV):
-        return None
-    fetch, write = {}, {}   # kernel name -> (mean bytes per dispatch, dispatches)
-    with open(TRAFFIC_CSV) as fh:
+    path = TRAFFIC_CSV.get(workload)
+    if not path or not os.path.exists(path):
+        return {}
+    rows = {}   # kernel name -> counter -> (mean per dispatch, dispatches)
+    with open(path) as fh:
         for row in csv.DictReader(fh):
-            if row["counter"].startswith("FETCH_BYTES"):
-                fetch[row["kernel"]] = (float(row["mean_per_dispatch"]), int(row["dispatches"]))
-            elif row["counter"].startswith("WRITE_BYTES"):
-                write[row["kernel"]] = (float(row["mean_per_dispatch"]), int(row["dispatches"]))
-    # every instantiation of the kernel (one per pyramid layer for the templated ROI kernels), weighted by its
-    # dispatches: the mean per launch over the same launches the algorithmic bytes are averaged over
-    total, launches = 0.0, 0
+            if " @grid=" in row["kernel"]:
+                continue   # per-grid split entries (the aggregate row holds every dispatch)
+            rows.setdefault(row["kernel"], {})[row["counter"]] = (float(row["mean_per_dispatch"]),
+                                                                  int(row["dispatches"]))
     for sym in L.KERNEL_SYMBOLS.get(kernel, []):
-        for name, (f, n) in fetch.items():
-            if (name.startswith(f"fpm::{sym}(") or name.startswith(f"void fpm::{sym}<")) and name in write:
-                total += (f + write[name][0]) * n
-                launches += n
-        if launches:
-            break
-    return int(total / launches) if launches else None
+        names = [n for n in rows if n.startswith(f"fpm::{sym}(") or n.startswith(f"void fpm::{sym}<")]
+        if not names:
+            continue
+        out = {}
+        for c in {c for n in names for c in rows[n]}:
+            tot = sum(rows[n][c][0] * rows[n][c][1] for n in names if c in rows[n])
+            cnt = sum(rows[n][c][1] for n in names if c in rows[n])
+            out[c] = tot / cnt
+        return out
+    return {}
+
+
+def pmc_traffic(kernel, workload="src7"):
+    """HBM bytes per launch of `kernel` from the committed PMC snapshot of `workload` (FETCH_SIZE x2 for gfx950 +
+    WRITE_SIZE, per-dispatch means); None if not collected for this kernel."""
+    c = pmc_counters(kernel, workload)
+    f, w = c.get("FETCH_BYTES(x2 corrected, B)"), c.get("WRITE_BYTES(B)")
+    return int(f + w) if f is not None and w is not None else None
+
+
+def roofline_issue(kernel, workload, avg_s):
+    """The dominant kernel against the chip's issue and pipe capacities over its measured launch time: VALU issue
+    (SQ_INSTS_VALU x 2 cycles per wave64 instruction over 1024 SIMDs), the LDS array (SQ_LDS_IDX_ACTIVE over 256 CUs)
+    and the matrix pipe (SQ_VALU_MFMA_BUSY_CYCLES over 1024 SIMDs), from the committed SQ passes of the same kernel
+    pass (scripts/pmc_bench.sh); the largest fraction is the bound.  None if not collected."""
+    c = pmc_counters(kernel, workload)
+    if "SQ_INSTS_VALU" not in c or avg_s <= 0:
+        return None
+    cyc = CLOCK_GHZ * 1e9 * avg_s
+    fr = {"valu_issue": c["SQ_INSTS_VALU"] * VALU_ISSUE_CYCLES / (SIMDS * cyc)}
+    if "SQ_LDS_IDX_ACTIVE" in c:
+        fr["lds"] = c["SQ_LDS_IDX_ACTIVE"] / (CUS * cyc)
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in c:
+        fr["mfma_pipe"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * cyc)
+    bound = max(fr, key=fr.get)
+    per_wave = {k: round(c[k] / c["SQ_WAVES"], 1) for k in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD",
+                                                            "SQ_INSTS_VMEM_WR", "SQ_INSTS_SALU", "SQ_INSTS_MFMA")
+                if k in c and c.get("SQ_WAVES")}
+    return {"bound": bound, "frac": round(fr[bound], 4), "fracs": {k: round(v, 4) for k, v in fr.items()},
+            "kernel": kernel, "avg_launch_us": round(avg_s * 1e6, 3), "waves_per_launch": int(c.get("SQ_WAVES", 0)),
+            "per_wave": per_wave,
+            "definition": "issue / pipe cycles the kernel's counters need per launch / the cycles the chip has in its "
+                          "measured launch time (2.4 GHz): VALU 2 cycles per wave64 instruction per SIMD, LDS array "
+                          "cycles per CU, matrix-pipe busy cycles per SIMD",
+            "source": ISSUE_SOURCE.format(os.path.relpath(TRAFFIC_CSV[workload], REPO), workload)}
 
 
 def make_sources(templ, n, seed0):
@@ -206,7 +250,7 @@ def oracle_verify(templ, sources, refs, params):
     return len(sources)
 
 
-def kernel_pass(m, sources, steps, L):
+def kernel_pass(m, sources, steps, L, workload="src7"):
     """Kernel-level pass: one context over its share of the step's sources (the same launches as one context's pass
     in the timed run), eager launches with HIP events around each kernel on the library's stream (the kernels' own
     durations, not time shared with another context's stream).  Returns the per-kernel table and the roofline
@@ -228,13 +272,14 @@ def kernel_pass(m, sources, steps, L):
     avg_s = d["ms_total"] / d["launches"] * 1e-3
     bytes_per_launch = d["bytes"] / d["launches"]
     achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
-    traffic = pmc_traffic(dom)
+    traffic = pmc_traffic(dom, workload)
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": dom,
                 "avg_launch_us": round(avg_s * 1e6, 3), "algorithmic_bytes_per_launch": int(bytes_per_launch),
                 "bytes_definition": "SURVEY.md §8(d) share of this kernel per launch (fpm_profile_get)",
-                "traffic_source": TRAFFIC_SOURCE if traffic is not None else None}
-    return kern, roofline
+                "traffic_source": (TRAFFIC_SOURCE.format(os.path.relpath(TRAFFIC_CSV[workload], REPO), workload)
+                                   if traffic is not None else None)}
+    return kern, roofline, roofline_issue(dom, workload, avg_s)
 
 
 I8_MFMA_PEAK_TOPS = 5000.0           # MI355X_MICROARCH.md matrix-core table: I8 at 2x the BF16 rate (~2.5 PF dense)
@@ -387,9 +432,9 @@ def main():
     chunks = [sources[i * args.batch // G:(i + 1) * args.batch // G] for i in range(G)]
     # the kernel pass is one context's share of the step (chunks[0]), eager: the launches of the timed run's passes
     if args.kernel_pass_only:
-        kern, roofline = kernel_pass(m, chunks[0], args.steps, L)
+        kern, roofline, issue = kernel_pass(m, chunks[0], args.steps, L, args.workload)
         print(json.dumps({"kernel_pass_only": True, "steps": args.steps, "sources_per_step": len(chunks[0]),
-                          "kernels": kern, "roofline": roofline}), flush=True)
+                          "kernels": kern, "roofline": roofline, "roofline_issue": issue}), flush=True)
         return
     # single-search latency (host upload included) for the record, after one warm call builds the plan
     lat_e2e = lat_split = None
@@ -520,7 +565,7 @@ def main():
                                   "49 w_l h_l per live refinement ROI; 2 ops per MAC) / the timed wall time, vs the "
                                   "i8 MFMA dense peak"}
 
-    kern, roofline = kernel_pass(m, chunks[0], args.steps, L)
+    kern, roofline, issue = kernel_pass(m, chunks[0], args.steps, L, args.workload)
     # the refinement correlation kernel (k_roi_corr: the layers whose template is too large for k_roi_small, the
     # lowest ones) on its useful MACs per launch -- the banded GEMM also computes the (t, s) pairs outside the band
     roofline_corr = None
@@ -596,6 +641,7 @@ def main():
         "matches_per_search": n_matches,
         "kernels": kern,
         "roofline": roofline,
+        "roofline_issue": issue,
         "roofline_search": roofline_search,
         "roofline_mac": roofline_mac,
         "roofline_corr": roofline_corr,

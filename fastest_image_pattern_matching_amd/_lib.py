@@ -25,14 +25,15 @@ FPM_E_INTERNAL = -6
 (K_PYR, K_TOP_WARP, K_TOP_NCC, K_TOP_NMS, K_CAND_INIT, K_ROI_TABLES, K_ROI_WARP, K_ROI_CORR, K_ROI_EVAL, K_ROI_SMALL,
  K_CAND_STEP, K_TOP_MAP) = range(12)
 # profiling index -> kernel (include/fpm.h FPM_K_*); top_ncc is k_top_mma (matrix-core top layer) where it applies, else
-# k_ncc_tile for templates up to 128 x 64; top_map = k_top_mma's fallback launch (full maps for the jobs its lists left)
+# k_ncc_tile for templates up to 128 x 64; top_map = k_top_map, the matrix-core form's fallback (full maps for the jobs
+# its lists left)
 KERNEL_NAMES = ["pyr_down", "top_warp", "top_ncc", "top_nms", "cand_init", "roi_tables", "roi_warp", "roi_corr",
                 "roi_eval", "roi_small", "cand_step", "top_map"]
 KERNEL_SYMBOLS = {"pyr_down": ["k_pyr_down_s", "k_pyr_down"], "top_warp": ["k_warp"],
                   "top_ncc": ["k_top_mma", "k_ncc_tile", "k_ncc_map"],
                   "top_nms": ["k_nms_greedy", "k_nms"], "cand_init": ["k_cand_init"], "roi_tables": ["k_roi_tables"],
                   "roi_warp": ["k_roi_warp3", "k_roi_warp"], "roi_corr": ["k_roi_corr"], "roi_eval": ["k_roi_eval"],
-                  "roi_small": ["k_roi_small"], "cand_step": ["k_cand_step"], "top_map": ["k_top_mma"]}
+                  "roi_small": ["k_roi_small"], "cand_step": ["k_cand_step"], "top_map": ["k_top_map"]}
 
 
 class Params(C.Structure):

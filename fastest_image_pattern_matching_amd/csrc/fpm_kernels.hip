@@ -4968,11 +4968,9 @@ __device__ __forceinline__ void tm_planes(uint32_t p0, uint32_t p1, uint32_t& wi
 
 // TH > 0: the template height as a compile-time constant (two-row slots, NQM = (TH + 1) / 2, every slot exact: no
 // masks); TH == 0: any height up to the form's bounds, rows past th masked
-// The exact-height two-row forms (<= 40 KB of LDS at the BASELINE shapes) are held to 128 registers: 4 workgroups
-// per CU.
-template <int NQM, int RR, int TM_CP, int TH = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RR == 32 && TH > 0 ? 4 : 1)))
-void k_top_mma(TopMmaArgs a) {
+// MODE 0: the candidate lists (kernel k_top_mma); MODE 1: the full maps of the jobs the lists left (k_top_map).
+template <int NQM, int RR, int TM_CP, int TH, int MODE>
+__device__ __forceinline__ void top_mma_body(const TopMmaArgs& a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t tm_lds[];
     constexpr int PS = RR * TM_CP;   // plane stride of the ring: I', lo(I'^2) ^ 0x80, hi(I'^2)
     uint8_t* const ring = tm_lds;
@@ -5004,13 +5002,13 @@ void k_top_mma(TopMmaArgs a) {
     // XCD-aware order (mode 0, one unit per workgroup): consecutive workgroups go to the 8 XCDs in turn, so XCD x
     // takes the x-th contiguous eighth of the unit list (the units of a few sources: their top levels stay in its L2)
     int u0 = blockIdx.x;
-    if (a.mode == 0 && (int)gridDim.x == a.nunits) {
+    if (MODE == 0 && (int)gridDim.x == a.nunits) {
         const int x = blockIdx.x & 7, q = a.nunits >> 3, r = a.nunits & 7;
         u0 = x * q + min(x, r) + (blockIdx.x >> 3);
     }
     for (int u = u0; u < a.nunits; u += gridDim.x) {
         const TopUnit U = a.units[u];
-        if (a.mode == 1 && a.cand_cnt[U.job] < 0) continue;   // (uniform) taken from its list: no map needed
+        if (MODE == 1 && a.cand_cnt[U.job] < 0) continue;   // (uniform) taken from its list: no map needed
         const WarpJob& W = a.wjobs[U.job];
         const NccJob& NJ = a.njobs[U.job];
         const int mw = NJ.ow;
@@ -5215,7 +5213,7 @@ void k_top_mma(TopMmaArgs a) {
                 }
                 uint32_t pm = 0;
                 const bool colok = xo < swu;
-                if (a.mode == 0 && a.prefilter) {
+                if (MODE == 0 && a.prefilter) {
                     typedef float f2_t __attribute__((ext_vector_type(2)));
                     const f2_t ar2 = {areaf, areaf}, ts2 = {tsumf, tsumf}, e2 = {a.E, a.E}, k2 = {a.thrK, a.thrK};
 #pragma unroll
@@ -5245,14 +5243,14 @@ void k_top_mma(TopMmaArgs a) {
                     const uint32_t qs = i == 0 ? wq[0] : i == 1 ? wq[1] : i == 2 ? wq[2] : wq[3];
                     const double num = (double)(float)(double)cc;   // TM_CCORR's f32 result
                     const float sc = ccoeff(num, (double)ws, (double)qs, a.mean, a.norm, a.inv_area);
-                    if (a.mode == 1) {
+                    if (MODE == 1) {
                         NJ.out[(size_t)(yo0 + i) * mw + U.x0 + xo] = sc;
                     } else if ((double)sc >= a.thr) {
                         tk |= 1u << i;
                         if (i == 0) sv0 = sc; else if (i == 1) sv1 = sc; else if (i == 2) sv2 = sc; else sv3 = sc;
                     }
                 }
-                if (a.mode == 0 && __ballot(tk != 0)) {   // (wave-uniform; rare)
+                if (MODE == 0 && __ballot(tk != 0)) {   // (wave-uniform; rare)
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const bool take = (tk >> i) & 1u;
@@ -5277,6 +5275,29 @@ void k_top_mma(TopMmaArgs a) {
     }
 }
 
+// The exact-height two-row forms (<= 40 KB of LDS at the BASELINE shapes) are held to 128 registers: 4 workgroups
+// per CU.
+template <int NQM, int RR, int TM_CP, int TH = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RR == 32 && TH > 0 ? 4 : 1)))
+void k_top_mma(TopMmaArgs a) {
+    top_mma_body<NQM, RR, TM_CP, TH, 0>(a);
+}
+template <int NQM, int RR, int TM_CP, int TH = 0>
+__global__ __launch_bounds__(256) void k_top_map(TopMmaArgs a) {
+    top_mma_body<NQM, RR, TM_CP, TH, 1>(a);
+}
+
+template <int NQM, int RR, int CP, int TH = 0>
+static void launch_top_form(const TopMmaArgs& a, int grid, size_t lds, hipStream_t st) {
+    if (a.mode == 0) {
+        ensure_lds_attr((const void*)k_top_mma<NQM, RR, CP, TH>, lds);
+        hipLaunchKernelGGL((k_top_mma<NQM, RR, CP, TH>), dim3(grid), dim3(256), lds, st, a);
+    } else {
+        ensure_lds_attr((const void*)k_top_map<NQM, RR, CP, TH>, lds);
+        hipLaunchKernelGGL((k_top_map<NQM, RR, CP, TH>), dim3(grid), dim3(256), lds, st, a);
+    }
+}
+
 void launch_top_mma(const TopMmaArgs& a, hipStream_t st) {
     if (a.nunits <= 0) return;
     const size_t lds = top_mma_lds(a);
@@ -5284,19 +5305,10 @@ void launch_top_mma(const TopMmaArgs& a, hipStream_t st) {
     const int grid = a.mode == 1 ? std::min(a.nunits, 4 * device_cus()) : a.nunits;
     // exact-height forms for the two-row layout's common top templates (16 rows: a square template at MinReduceArea
     // 256, BASELINE configs[3]; 14: configs[2]), the masked small form for other heights up to 16
-    if (top_mma_small(a) && a.th == 16) {
-        ensure_lds_attr((const void*)k_top_mma<8, 32, TM_CP2, 16>, lds);
-        hipLaunchKernelGGL((k_top_mma<8, 32, TM_CP2, 16>), dim3(grid), dim3(256), lds, st, a);
-    } else if (top_mma_small(a) && a.th == 14) {
-        ensure_lds_attr((const void*)k_top_mma<7, 32, TM_CP2, 14>, lds);
-        hipLaunchKernelGGL((k_top_mma<7, 32, TM_CP2, 14>), dim3(grid), dim3(256), lds, st, a);
-    } else if (top_mma_small(a)) {
-        ensure_lds_attr((const void*)k_top_mma<8, 32, TM_CP2>, lds);
-        hipLaunchKernelGGL((k_top_mma<8, 32, TM_CP2>), dim3(grid), dim3(256), lds, st, a);
-    } else {
-        ensure_lds_attr((const void*)k_top_mma<16, 64, TM_CP1>, lds);
-        hipLaunchKernelGGL((k_top_mma<16, 64, TM_CP1>), dim3(grid), dim3(256), lds, st, a);
-    }
+    if (top_mma_small(a) && a.th == 16) launch_top_form<8, 32, TM_CP2, 16>(a, grid, lds, st);
+    else if (top_mma_small(a) && a.th == 14) launch_top_form<7, 32, TM_CP2, 14>(a, grid, lds, st);
+    else if (top_mma_small(a)) launch_top_form<8, 32, TM_CP2>(a, grid, lds, st);
+    else launch_top_form<16, 64, TM_CP1>(a, grid, lds, st);
 }
 
 void launch_top_greedy(const NmsArgs& a0, int njobs, int max_cells, hipStream_t st, const CandInitArgs* ci) {

@@ -232,7 +232,7 @@ int fpm_search_bytes(const fpm_ctx* ctx, int64_t* b_pyr, int64_t* b_top, int64_t
 #define FPM_K_ROI_EVAL 8    /* k_roi_eval     K8 row fold, CCOEFF, argmax, 3x3, candidate step    */
 #define FPM_K_ROI_SMALL 9   /* k_roi_small    K6-K8 in one kernel for small templates             */
 #define FPM_K_CAND_STEP 10  /* k_cand_step    candidate step after k_roi_small                    */
-#define FPM_K_TOP_MAP 11    /* k_top_mma mode 1: full maps of the jobs the list path left (fallback) */
+#define FPM_K_TOP_MAP 11    /* k_top_map: full maps of the jobs the list path left (fallback) */
 #define FPM_K_COUNT 12
 int fpm_profile_enable(fpm_ctx* ctx, int32_t enable);
 int fpm_profile_reset(fpm_ctx* ctx);
