@@ -90,6 +90,8 @@ struct Plan {
     int a0 = 0, nang_all = 0;                  // this plan's angles = [a0, a0 + nang) of the full top-layer list
     int shard = 0, shards = 1;                 // angle shard the plan was built for (fpm_set_angle_shard)
     bool by_block = false;
+    uint32_t step_layers = 0;                  // bit d: the last pass launched k_cand_step for layer depth d (profiling)
+    bool top_lists = false;                    // the last pass took its top-layer peaks from k_top_mma's lists
     std::vector<double> angles, layer_score;
     std::vector<TopAngle> top;
     std::vector<AngleNode> top_nodes;
@@ -751,6 +753,8 @@ int enqueue_search(fpm_ctx* ctx) {
     uint8_t* dsrc = ctx->d_src.as<uint8_t>();
     const SrcLevel& top = ctx->src[L];
     const TmplLevel& tt = ctx->tmpl[L];
+    P.step_layers = 0;   // (set again by the launches recorded below)
+    P.top_lists = false;
     // small canvases with the plain peak path: the whole top layer as one kernel (k_top_fused), canvas and map in
     // LDS, when there are enough (source, angle) jobs to fill the chip: one workgroup runs a job's warp, map and
     // peak loop serially (33 us for a single Src7 source's 41 jobs against 24 us for the three split kernels; 75.5
@@ -855,10 +859,11 @@ int enqueue_search(fpm_ctx* ctx) {
         ga.cand = P.d_ncand.as<int32_t>(); ga.cand_val = P.d_tcandv.as<float>();
         ga.cand_cnt = ta.cand_cnt; ga.cand_cap = P.tcand_cap;
         ga.reset_untaken = P.by_block ? 1 : 0;
-        {
+        {   // (its bytes, the map term of B_top the lists stand in for, are added when the pass completes)
             ProfScope ps(ctx, FPM_K_TOP_NMS, 0);
             launch_top_greedy(ga, J, P.max_cells, st, ci_ok ? &ca : nullptr);
         }
+        P.top_lists = true;
         {   // the maps the lists could not give (overflow, or a shape the greedy form does not take): full maps
             ProfScope ps(ctx, FPM_K_TOP_MAP, 0);
             ta.mode = 1;
@@ -1045,6 +1050,7 @@ int enqueue_search(fpm_ctx* ctx) {
                 ra.live_out_count = livecnt + d + 1;
             }
             launch_cand_step(ra, P.C, st);
+            P.step_layers |= 1u << d;
         }
         if (ra.step) {
             cur_list ^= 1;
@@ -1519,11 +1525,18 @@ int complete_staged(fpm_ctx* ctx, std::vector<std::vector<fpm_result>>& results,
         ctx->alg_bytes[2] = br;
     }
     if (ctx->prof && P.nang > 0) {   // per-kernel share of B_ref (the live counts are known only now)
+        // the matrix-core top layer never writes its maps: the peak extraction over them (the greedy form on the
+        // lists) is charged the map term of B_top, 4 |R_a| per source and angle
+        if (P.top_lists)
+            for (int a = 0; a < P.nang; ++a) ctx->kp[FPM_K_TOP_NMS].bytes += 4LL * P.map_w[a] * P.map_h[a] * P.S;
         for (int d = 0; d < P.L; ++d) {
             const int l = P.L - 1 - d;
             const TmplLevel& t = ctx->tmpl[l];
             const int64_t rois = (int64_t)lc[d] * P.n3;
             const int64_t foot = (int64_t)(t.w + 6) * (t.h + 6), tmpl = (int64_t)t.w * t.h;
+            if (P.step_layers & (1u << d))   // the step: its candidates' records and state (design state, not §8(d))
+                ctx->kp[FPM_K_CAND_STEP].bytes +=
+                    (int64_t)lc[d] * (P.n3 * (int64_t)sizeof(RoiRecord) + 2 * (int64_t)sizeof(CandState) + 4);
             if (roi_small_fits(t.w, t.h)) {   // one kernel: footprint + template in, the 7x7 scores out
                 ctx->kp[FPM_K_ROI_SMALL].bytes += rois * (foot + tmpl + 49 * 4);
                 continue;
