@@ -4913,6 +4913,8 @@ constexpr int TM_CP2 = 224, TM_CP1 = 288;
 constexpr int TM_FTP = 44;           // sampling footprint buffer: row pitch (bytes; an odd word count spreads the
 constexpr int TM_FTB = 44 * 40;      // taps over the banks) and size per wave (a 16 x 32 tile of a rotation covers at
                                      // most 37 x 37 source pixels + taps)
+// TOPMMA_ABL (measurement builds only, scripts/gpu_abl.sh; the product is 0): 1 = no sampling, 3 = no MFMA loop, 4 = no
+// epilogue, 5 = no staging loads, 6 = no gather (1, 5 and 6 leave garbage in the ring: their exact paths run far more)
 #ifndef TOPMMA_ABL
 #define TOPMMA_ABL 0
 #endif
