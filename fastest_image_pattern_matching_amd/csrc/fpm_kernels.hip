@@ -3130,6 +3130,13 @@ __device__ __forceinline__ void band_mfma_regs(const fpm_v4i* A, const uint8_t* 
 // per row and wave, the scratch already flipped): no staging registers and no VALU per staged row
 // DB (with DMA): two row buffers; the next item's rows are issued into the other buffer once this item's are in LDS,
 // so an item waits for rows requested one item earlier (the LDS holds a second kBandSrc x SBp buffer after the rest)
+// wave priority of the GEMM phase (s_setprio): 1 = the banded GEMM and its row-result epilogue at priority 1 (the
+// product: the item's matrix work is not held behind the co-resident waves' staging and statistics VALU; Src7 kernel
+// pass 196.5 -> 185.7 us per k_roi_corr launch averaged over the layers, profiles/r06_prio/), 2 = the GEMM alone,
+// 0 = none
+#ifndef FPM_CORR_PRIO
+#define FPM_CORR_PRIO 1
+#endif
 template <int MODE, bool GA, int WPE, int NK = 0, bool PFR = true, int RS = 1, bool SE = false, bool DMA = false,
           bool DB = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_roi_corr(RoiArgs a) {
@@ -3432,17 +3439,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         };
         if (RS == 2) partials();   // before the banded GEMM (the same wave's MFMA work follows)
         const bool active = kMmaRows * mt < rb && kMmaRows * nt < nsrc;   // wave-uniform
+        if (FPM_CORR_PRIO == 1) __builtin_amdgcn_s_setprio(1);   // the GEMM and its epilogue
         if (MODE != 2 && active) {
             int sr = kMmaRows * nt + n;
             if (sr >= nsrc) sr = 0;   // column outside the band: computed, never stored
             const uint8_t* bp = SB + (size_t)sr * SBp + 16 * g;
             fpm_v4i acc[7];
+            if (FPM_CORR_PRIO == 2) __builtin_amdgcn_s_setprio(1);
             if (NK > 0)
                 band_mfma_regs<NA>(Areg, bp, a.nk, acc);
             else if (GA)
                 band_mfma_ga(a.tmpl8 + (size_t)(T0 + kMmaRows * mt + n) * a.tp8 + 16 * g, bp, a.nk, acc);
             else
                 band_mfma(TB + (size_t)(kMmaRows * mt + n) * TBp + 16 * g, bp, a.nk, acc);
+            if (FPM_CORR_PRIO == 2) __builtin_amdgcn_s_setprio(0);
             // D_dx: col = lane & 15 -> source row 16*nt + n, row = 4*(lane >> 4) + r -> template row 16*mt + 4g + r
             uint32_t* rs_out = a.rowsum + (((size_t)th * 49 + 3) & ~(size_t)3) * slot + (size_t)T0 * 49;   // uniform
             const uint32_t kFix = 16384u * (uint32_t)tw;
@@ -3477,6 +3487,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 }
             }
         }
+        if (FPM_CORR_PRIO == 1) __builtin_amdgcn_s_setprio(0);
         if (RS == 1) partials();
         if (RS == 0 && MODE != 6 && tid < 2 * 49) {   // per-16-row-chunk partials of the window sums
             const int h = tid / 49, k = tid - h * 49;
@@ -4918,6 +4929,13 @@ constexpr int TM_FTB = 44 * 40;      // taps over the banks) and size per wave (
 #ifndef TOPMMA_ABL
 #define TOPMMA_ABL 0
 #endif
+// wave priorities (s_setprio) of the band's phases: 4 = the tiles (MFMA loop and epilogue) at priority 1, the sampling
+// at 0 (the product: a wave's matrix instructions are not held behind the other waves' sampling VALU on its SIMD;
+// configs[3] 735.6 -> 677-678 us per launch, profiles/r06_prio/), 1 = the MFMA loop only (678-689), 2 = the
+// sampling at 1 instead (721.7), 3 = MFMA loop 2 / sampling 1 (681), 0 = none (735.6; measurement builds)
+#ifndef TOPMMA_PRIO
+#define TOPMMA_PRIO 4
+#endif
 
 bool top_mma_fits(int tw, int th) { return tw >= 1 && th >= 1 && ((tw <= 17 && th <= 32) || (tw <= 49 && th <= 16)); }
 
@@ -5035,6 +5053,8 @@ __device__ __forceinline__ void top_mma_body(const TopMmaArgs& a) {
             const int rs = yb == U.y0 ? yb : yb + th - 1;
             const int re = min(yb + TM_BH + th - 1, U.y0 + nrows);
             __syncthreads();   // tables ready / the previous band's tiles are done with the ring rows replaced now
+            if (TOPMMA_PRIO == 2 || TOPMMA_PRIO == 3) __builtin_amdgcn_s_setprio(1);
+            if (TOPMMA_PRIO == 4) __builtin_amdgcn_s_setprio(0);
             // ---- the band's new canvas rows (cv::warpAffine with k_warp's integers), flipped to i8.  One wave per
             // sampling tile of 16 rows x 32 columns: the tile's source footprint (the box of its clamped tap coordinates:
             // the fixed-point coordinates are monotone in x and y, so the corners bound it; coordinates clamped into
@@ -5156,11 +5176,14 @@ __device__ __forceinline__ void top_mma_body(const TopMmaArgs& a) {
                     wave_sync();   // the buffer is reused by the wave's next tile
                 }
             }
+            if (TOPMMA_PRIO == 2 || TOPMMA_PRIO == 3) __builtin_amdgcn_s_setprio(0);
             __syncthreads();
             // ---- the band's 16 x 16 output tiles, one wave each: NQM slots unrolled (A and B of every slot requested
             // before the first MFMA; slots >= nq read zero B)
             for (int nb = wv; nb < nbu; nb += 4) {
                 fpm_v4i acc = zero4, acc1 = zero4, accl = zero4, acch = zero4;
+                if (TOPMMA_PRIO == 1 || TOPMMA_PRIO == 4) __builtin_amdgcn_s_setprio(1);
+                if (TOPMMA_PRIO == 3) __builtin_amdgcn_s_setprio(2);
                 if (TOPMMA_ABL != 3) {
                     // slot q's fragments (three planes) are requested two slots ahead of its MFMAs
                     const uint8_t* abase = ring + 16 * nb + co;
@@ -5194,6 +5217,7 @@ __device__ __forceinline__ void top_mma_body(const TopMmaArgs& a) {
                         acch = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[2], ones, acch, 0, 0, 0);
                     }
                 }
+                if (TOPMMA_PRIO == 1 || TOPMMA_PRIO == 3) __builtin_amdgcn_s_setprio(0);
                 if (TOPMMA_ABL == 4) {
                     if (acc[0] == 0x12345 && acc1[1] == 0x777) a.cand_cnt[0] = acc[2] + acc1[3] + accl[0] + acch[1];
                     continue;
