@@ -364,6 +364,21 @@ int plan_top_mma(fpm_ctx* ctx, Plan& P, const TmplLevel& tt) {
         seg = cand;
         if (n * S >= 2048) break;
     }
+    // plain-peak searches with few work units (< 128 workgroups: a lone Src7 search's 41 small maps make 82) and few
+    // peaks per map (MaxPos <= 10, the reference's own s_BlockMax threshold) run faster on the split kernels, whose
+    // grids cover the chip: device 0.233 vs 0.248 ms for the lone Src7 search.  Many peaks per map keep the lists, whose
+    // greedy pass beats k_nms's painted-rectangle loop even on one map (Src3 / Dst3 at 0 deg, MaxPos 38, 3 units: 0.170
+    // vs 0.229 ms), and so do s_BlockMax searches and many-unit sweeps (profiles/r06_lone/); FPM_TOP_MMA=1 keeps the form
+    {
+        long nunits = 0;
+        for (int a = 0; a < P.nang; ++a)
+            if (P.map_w[a] > 0 && P.map_h[a] > 0)
+                nunits += (long)((P.map_w[a] + sw - 1) / sw) * ((P.map_h[a] + std::min(seg, P.map_h[a]) - 1) /
+                                                               std::min(seg, P.map_h[a]));
+        if (!(env && atoi(env) == 1) && !P.by_block && ctx->prm.max_pos <= 10 && nunits * S < 128 &&
+            ncc_tile_fits(tt.w, tt.h))
+            return FPM_OK;
+    }
     int max_rows = 0;
     for (int s = 0; s < S; ++s)
         for (int a = 0; a < P.nang; ++a) {

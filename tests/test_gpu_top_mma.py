@@ -3,10 +3,11 @@ oracle, on the BASELINE configs whose top layer it serves and on template shapes
 (gfx950 required).
 
 Forms, chosen per fresh context (the switches are read when its plan is built / its search recorded):
-  default               k_top_mma wherever the plan admits it (except where the fused small-canvas kernel applies)
+  default               k_top_mma wherever the plan admits it (except where the fused small-canvas kernel applies, and
+                        plain-peak searches with MaxPos <= 10 and fewer than 128 work units: the split kernels)
   FPM_TOP_MMA=0         the split k_warp -> k_ncc_tile -> k_nms chain (or k_top_fused)
   FPM_TOP_MMA=1         k_top_mma also where k_top_fused would apply
-  FPM_TOP_LIST_CAP=1    lists of one entry: every map with two or more outputs >= the layer score overflows and takes
+  FPM_TOP_LIST_CAP=1    (with FPM_TOP_MMA=1) lists of one entry: every map with two or more outputs >= the layer score overflows and takes
                         the fallback (k_top_mma mode 1 writes its full map, the split peak kernels take it)
 Every result field and every per-layer live count equals the oracle's (bit-identical).
 """
@@ -21,7 +22,7 @@ from tests.test_gpu_parity import assert_same_results
 pytestmark = pytest.mark.gpu
 
 FORMS = {"default": {}, "split": {"FPM_TOP_MMA": "0"}, "forced": {"FPM_TOP_MMA": "1"},
-         "fallback": {"FPM_TOP_LIST_CAP": "1"}}
+         "fallback": {"FPM_TOP_MMA": "1", "FPM_TOP_LIST_CAP": "1"}}
 
 
 def _set(monkeypatch, form):
@@ -123,7 +124,7 @@ def _wide_scene(tw, th, seed, angles):
     return s, t
 
 
-@pytest.mark.parametrize("form", ["default", "fallback"])
+@pytest.mark.parametrize("form", ["forced", "fallback"])
 @pytest.mark.parametrize("shape", [(80, 14, 256), (40, 28, 512), (34, 60, 1024), (6, 60, 256)])
 def test_template_shapes(gpu_matcher_factory, monkeypatch, form, shape):
     """Top templates at the edges of the kernel's layouts: 20 x 4 (one-row slots of 64 columns, two pyramid levels),
@@ -142,7 +143,7 @@ def test_template_shapes(gpu_matcher_factory, monkeypatch, form, shape):
 def test_plain_peaks_overlapping_rectangles(gpu_matcher_factory, templates, monkeypatch):
     """Plain getNextMaxLoc from the lists with MaxOverlap 0.6 (painted rectangles smaller than the template, so
     peaks sit close) and TargetNum 8 on a dense grid of copies: the greedy key is the row-major position."""
-    _set(monkeypatch, "default")
+    _set(monkeypatch, "forced")
     t = templates["Dst10"]
     s = synth.noise(700, 520, 128, 8, 5)
     k = 0
@@ -156,14 +157,17 @@ def test_plain_peaks_overlapping_rectangles(gpu_matcher_factory, templates, monk
     assert got == exp and stats == ostats
 
 
-@pytest.mark.parametrize("form", ["default", "fallback", "split"])
+@pytest.mark.parametrize("form", ["forced", "forced_fallback", "split"])
 def test_rect_missing_its_peak(gpu_matcher_factory, monkeypatch, form):
     """MaxOverlap 0.8 on a 107 x 35 template (top level 14 x 5): getNextMaxLoc paints int(2 * 5 * 0.2) = 1 row starting
     a row above the peak, so the peak survives and the reference takes it again with every remaining call (14 equal
-    records per angle).  The greedy form reproduces the repeats; records, stats and results equal the oracle's."""
+    records per angle).  The greedy form reproduces the repeats (forced: a lone plain search this small takes the
+    split kernels by default); records, stats and results equal the oracle's."""
     from tests.test_gpu_fuzz import _case
 
-    _set(monkeypatch, form)
+    _set(monkeypatch, "split" if form == "split" else "forced")
+    if form == "forced_fallback":
+        monkeypatch.setenv("FPM_TOP_LIST_CAP", "1")
     s, t, prm = _case(24)
     o = oracle.OracleMatcher().set(**prm)
     assert o.learnPattern(t)
