@@ -229,6 +229,12 @@ class TemplateMatcher:
         """Search the staged sources and return each source's candidate records, skipping the host tail
         (fpm_match_staged_finish with out = NULL): the per-rank step of an angle-sharded search."""
         self.match_staged_launch()
+        return self.match_staged_candidates_finish()
+
+    def match_staged_candidates_finish(self) -> List[np.ndarray]:
+        """Wait for a pass enqueued by match_staged_launch and return each source's candidate records (the second
+        half of match_staged_candidates: a stream of passes over two contexts overlaps one's device pass with the
+        other's record exchange and merge)."""
         n = (C.c_int32 * self._staged)()
         rc = self._check(self._lib.fpm_match_staged_finish(self._ctx, None, 0, n), "match_staged_finish")
         if rc != L.FPM_OK:
